@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""bench.py — publish-time route lookup throughput on MI355X.
+
+Metric (BASELINE.json): topics matched/sec (node) at 10M filters, 1/2/4/8
+GPUs, with the HBM-roofline fraction of the dominant kernel.
+
+A *step* is one pass of the hot path — tokenise + NFA walk (+ heavy path) +
+CSR finalisation, i.e. emqx_router:match_routes/1's filter sets for a whole
+batch — over one batch of synthetic topics already resident in HBM.
+
+Layouts (emqx_amd/dist.py):
+  replicate (default)  every GPU holds the 10M-filter table and matches its own
+                       10M-topic batch; no data-path collective -> "weak".
+  shard                filters split over the GPUs, rank 0's batch broadcast,
+                       counts all-gathered, ids gathered over RCCL -> "strong".
+
+    python bench.py [--gpus N --steps K --warmup W] [--config c2] [--mode replicate]
+
+Rank 0 prints ONE JSON line on stdout; progress goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "topics matched/sec (node) at 10M filters, 1/2/4/8 GPUs; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    "c1": "C1: 1M filters (depth 4-8, 20% wildcard) x 10M-topic batch per GPU",
+    "c2": "C2: 10M wildcard filters (depth 4-8, '+' p=.15, '#' p=.5) x 10M-topic batch per GPU",
+    "c3": "C3: 10M wildcard filters, depth-16 topics, '+' p=.35, '#' p=.7",
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def levels_sum(blob: np.ndarray, off: np.ndarray) -> int:
+    nbytes = int(off[-1])
+    return int(np.count_nonzero(blob[:nbytes] == ord("/"))) + (len(off) - 1)
+
+
+def cpu_baseline(f, t, match_mode: int, seconds: float) -> dict:
+    """C++ restatement of emqx_trie (compact) + route lookup, timed on host cores."""
+    from oracle.cpp import OracleTrie
+    threads = max(1, min(16, os.cpu_count() or 1))
+    o = OracleTrie(True, match_mode)
+    t0 = time.time()
+    o.add(f.blob, f.off)
+    build_s = time.time() - t0
+    probe = min(t.n, 20_000 * threads)
+    sub = t.subset(np.arange(probe))
+    t0 = time.time()
+    o.match_count(sub.blob, sub.off, threads)
+    dt = max(time.time() - t0, 1e-3)
+    n = int(min(t.n, max(probe, probe * seconds / dt)))
+    sub = t.subset(np.arange(n))
+    t0 = time.time()
+    m = o.match_count(sub.blob, sub.off, threads)
+    dt = time.time() - t0
+    return {"value": n / dt, "unit": "topics/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} topics of the same batch, {threads} threads, static partition; "
+                      f"C++ restatement of emqx_trie compact DFS + lookup_routes (oracle/trie_oracle.cpp), "
+                      f"not BEAM; {m} matches; table build {build_s:.1f}s untimed",
+            "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--filters", type=int, default=None, help="override filter count")
+    ap.add_argument("--topics", type=int, default=None, help="override topics per batch")
+    ap.add_argument("--mode", default="replicate", choices=["replicate", "shard"])
+    ap.add_argument("--match", default="routes", choices=["routes", "trie"])
+    ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+
+    from emqx_amd import build as B
+    if not os.path.exists(B.LIB):
+        B.build_all()
+    import torch
+    import torch.distributed as dist
+    from emqx_amd import _lib as L
+    from emqx_amd import synth
+    from emqx_amd.engine import GpuMatcher
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    mode = L.EGM_MODE_ROUTES if args.match == "routes" else L.EGM_MODE_TRIE
+
+    c = synth.CONFIGS[args.config]
+    seed = synth.SEED_BASE + synth.CONFIG_INDEX[args.config]
+    nf = args.filters or c["n_filters"]
+    nt = args.topics or c["n_topics"]
+    t0 = time.time()
+    f = synth.filters(nf, c["dmin"], c["dmax"], c["wc"], c["p_plus"], c["p_hash"], seed=seed)
+    tseed = seed + (7919 * rank if args.mode == "replicate" else 0)
+    t = synth.topics(nt, f, c["dmin"], c["dmax"], seed=tseed)
+    log(f"[rank {rank}] generated {f.n} filters, {t.n} topics in {time.time() - t0:.1f}s")
+
+    gm = GpuMatcher(local, max_batch=nt)
+    t0 = time.time()
+    if args.mode == "shard" and world > 1:
+        from emqx_amd.dist import shard_of
+        from emqx_amd.engine import pack_strings
+        sh = shard_of(f, world)
+        idx = np.nonzero(sh == rank)[0]
+        fl = f.to_list()
+        blob, off = pack_strings([fl[i] for i in idx])
+        gm.build(blob, off, idx.astype(np.uint32))
+    else:
+        gm.build(f.blob, f.off)
+    tstats = gm.stats()
+    log(f"[rank {rank}] table built in {time.time() - t0:.1f}s: {tstats}")
+
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    n = t.n
+    nbytes = int(t.off[-1])
+    d_blob = torch.from_numpy(t.blob).to(dev)
+    d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+    cap = max(4 * n, 1 << 20)
+    d_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
+
+    def run_local():
+        gm.match_device(d_blob.data_ptr(), nbytes, d_off.data_ptr(), n, mode, sp, d_row.data_ptr(),
+                        d_ids.data_ptr(), cap)
+
+    exchange = None
+    if args.mode == "shard" and world > 1:
+        from emqx_amd.dist import ShardExchange
+
+        def local_match(tb, to, nn):
+            gm.match_device(tb.data_ptr(), tb.numel(), to.data_ptr(), nn, mode, sp, d_row.data_ptr(),
+                            d_ids.data_ptr(), cap)
+            m = int(d_row[nn].item())
+            return d_row, d_ids[:m]
+
+        exchange = ShardExchange(rank, world, dev, local_match)
+
+    def step():
+        if exchange is None:
+            run_local()
+        elif rank == 0:
+            exchange.step(d_blob, d_off)
+        else:
+            exchange.step()
+
+    # warmup (also sizes the id buffer)
+    for _ in range(max(1, args.warmup)):
+        step()
+        torch.cuda.synchronize(dev)
+        st = gm.last_stats()
+        if st["overflow"]:
+            cap = int(st["n_ids"] * 1.25) + 1024
+            d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
+            log(f"[rank {rank}] grew id buffer to {cap}")
+    st = gm.last_stats()
+    assert st["overflow"] == 0 and st["errors"] == 0, st
+
+    gm.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    tim = gm.get_timing()
+    st = gm.last_stats()
+    gm.set_timing(False)
+
+    units_per_step = n * world if (args.mode == "replicate" or world == 1) else n
+    value = units_per_step * args.steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- roofline (dominant kernel = k_walk), SURVEY §8d byte model ----
+    sum_d = levels_sum(t.blob, t.off)
+    n_ids = st["n_ids"]
+    visited = st["visited"]
+    walk_bytes = 8 * sum_d + 32 * visited + 4 * (n_ids + n)
+    walk_ms = tim["walk_ms"] / max(1, tim["walk_launches"])
+    achieved = walk_bytes / (walk_ms * 1e-3) / 1e9
+    path_bytes = (nbytes + 4 * n) + 16 * sum_d + 32 * visited + 4 * (n_ids + n)
+
+    if rank == 0:
+        cpu = None
+        if args.cpu_baseline == "auto" and world == 1:
+            log("[rank 0] timing the CPU baseline ...")
+            cpu = cpu_baseline(f, t, mode, args.cpu_seconds)
+        line = {
+            "metric": METRIC, "value": value, "unit": "topics/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "weak" if (args.mode == "replicate" or world == 1) else "strong",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": WORKLOADS[args.config], "filters": f.n, "topics_per_step": units_per_step,
+                       "topics_per_gpu": n, "match": "emqx_router:match_routes" if args.match == "routes"
+                       else "emqx_trie:match", "parallelism": f"{args.mode}{world}",
+                       "table": tstats},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_walk", "kernel_ms": walk_ms, "bytes_per_launch": walk_bytes,
+                         "path_frac": path_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS},
+            "stats": {"ids_per_step": n_ids, "visited_per_step": visited, "levels_per_step": sum_d,
+                      "deferred_chunks": st["deferred_chunks"]},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    gm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

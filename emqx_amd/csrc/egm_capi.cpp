@@ -1,0 +1,674 @@
+// egm_capi.cpp — the C-ABI of libemqx_gpu_match.so (include/emqx_gpu_match.h).
+//
+// Owns: one HIP stream per context, the staged host table (egm_table.cpp),
+// the committed device epochs (double-buffered through shared_ptr so a batch
+// in flight keeps the epoch it started with — the race-free analogue of the
+// reference's mnesia transactions around emqx_trie:insert/delete,
+// apps/emqx/src/emqx_router.erl:252-303), and the per-batch workspaces.
+#include <hip/hip_runtime_api.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/emqx_gpu_match.h"
+#include "egm_kernels.h"
+#include "egm_table.h"
+
+using namespace egm;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    release();
+    size_t b = bytes < 256 ? 256 : bytes;
+    hipError_t e = hipMalloc(&p, b);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = b;
+    return hipSuccess;
+  }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+
+struct Epoch {
+  DevBuf nodes, hash_child, edges, dict, dict_blob, dict_off;
+  DevTable view{};
+  uint64_t id = 0;
+  uint64_t n_filters = 0, n_nodes = 0, n_edges = 0, n_words = 0, bytes = 0;
+};
+
+template <class T>
+static hipError_t upload(DevBuf& b, const std::vector<T>& v) {
+  size_t bytes = v.size() * sizeof(T);
+  hipError_t e = b.ensure(bytes ? bytes : 16);
+  if (e != hipSuccess) return e;
+  if (bytes) e = hipMemcpy(b.p, v.data(), bytes, hipMemcpyHostToDevice);
+  return e;
+}
+
+}  // namespace
+
+struct egm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::recursive_mutex mu;
+  HostTable table;
+  std::shared_ptr<Epoch> cur;
+  uint64_t next_epoch = 1;
+  std::string err;
+
+  // per-batch workspace
+  DevBuf wid, lv, tfl, off_tmp, cnt, ids_tmp, deferred, tile_sums, stats;
+  DevBuf in_blob, in_off, out_row, out_ids;
+  uint32_t heavy_waves = 256;
+  MatchStats last{};
+  bool last_pending = false;
+  hipStream_t last_stream = nullptr;
+
+  // fan-out
+  DevBuf sub_row, sub_ids, f_dc, f_dpos, f_tiles, f_ovf, f_mrow, f_mids, f_drow, f_dfid, f_dsub;
+  uint32_t n_fid_slots = 0;
+
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_walk;   // pairs
+  std::vector<hipEvent_t> ev_fan;
+  std::vector<hipEvent_t> ev_free;
+  double walk_ms = 0, fan_ms = 0;
+  uint64_t walk_n = 0, fan_n = 0;
+
+  int fail(int code, const std::string& m) {
+    err = m;
+    return code;
+  }
+  int hip_fail(hipError_t e, const char* where) {
+    err = std::string(where) + ": " + hipGetErrorString(e);
+    return EGM_E_DEVICE;
+  }
+  hipEvent_t take_event() {
+    if (!ev_free.empty()) {
+      hipEvent_t e = ev_free.back();
+      ev_free.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    hipEventCreate(&e);
+    return e;
+  }
+  void drain_timing() {
+    for (size_t i = 0; i + 1 < ev_walk.size(); i += 2) {
+      float ms = 0;
+      hipEventSynchronize(ev_walk[i + 1]);
+      hipEventElapsedTime(&ms, ev_walk[i], ev_walk[i + 1]);
+      walk_ms += ms;
+      ++walk_n;
+      ev_free.push_back(ev_walk[i]);
+      ev_free.push_back(ev_walk[i + 1]);
+    }
+    ev_walk.clear();
+    for (size_t i = 0; i + 1 < ev_fan.size(); i += 2) {
+      float ms = 0;
+      hipEventSynchronize(ev_fan[i + 1]);
+      hipEventElapsedTime(&ms, ev_fan[i], ev_fan[i + 1]);
+      fan_ms += ms;
+      ++fan_n;
+      ev_free.push_back(ev_fan[i]);
+      ev_free.push_back(ev_fan[i + 1]);
+    }
+    ev_fan.clear();
+  }
+};
+
+static int set_device(egm_ctx* c) {
+  hipError_t e = hipSetDevice(c->device);
+  return e == hipSuccess ? 0 : c->hip_fail(e, "hipSetDevice");
+}
+
+static int commit_locked(egm_ctx* c, uint64_t* epoch) {
+  auto ep = std::make_shared<Epoch>();
+  const HostTable& t = c->table;
+  hipError_t e;
+  if ((e = upload(ep->nodes, t.nodes)) != hipSuccess) return c->hip_fail(e, "upload nodes");
+  if ((e = upload(ep->hash_child, t.hash_child)) != hipSuccess) return c->hip_fail(e, "upload hash_child");
+  if ((e = upload(ep->edges, t.edges)) != hipSuccess) return c->hip_fail(e, "upload edges");
+  if ((e = upload(ep->dict, t.dict)) != hipSuccess) return c->hip_fail(e, "upload dict");
+  if ((e = upload(ep->dict_blob, t.dict_blob)) != hipSuccess) return c->hip_fail(e, "upload dict_blob");
+  if ((e = upload(ep->dict_off, t.dict_off)) != hipSuccess) return c->hip_fail(e, "upload dict_off");
+  ep->view.nodes = ep->nodes.as<NodeRec>();
+  ep->view.hash_child = ep->hash_child.as<uint32_t>();
+  ep->view.edges = ep->edges.as<EdgeSlot>();
+  ep->view.edge_mask = t.edge_mask();
+  ep->view.dict = ep->dict.as<DictSlot>();
+  ep->view.dict_mask = t.dict_mask();
+  ep->view.dict_blob = ep->dict_blob.as<uint8_t>();
+  ep->view.dict_off = ep->dict_off.as<uint64_t>();
+  ep->n_filters = t.n_filters();
+  ep->n_nodes = t.n_nodes_live();
+  ep->n_edges = t.n_edges();
+  ep->n_words = t.n_words();
+  ep->bytes = ep->nodes.cap + ep->hash_child.cap + ep->edges.cap + ep->dict.cap + ep->dict_blob.cap +
+              ep->dict_off.cap;
+  ep->id = c->next_epoch++;
+  // readers holding the previous shared_ptr keep it alive until they finish;
+  // make sure no queued kernel still reads it before it can be freed
+  hipStreamSynchronize(c->stream);
+  c->cur = ep;
+  if (epoch) *epoch = ep->id;
+  return EGM_OK;
+}
+
+static int ensure_work(egm_ctx* c, uint32_t n, uint64_t blob_bytes, uint64_t ids_cap) {
+  hipError_t e;
+  const uint64_t nn = (uint64_t)n + 1;
+  if ((e = c->wid.ensure((blob_bytes + nn) * 4)) != hipSuccess) return c->hip_fail(e, "wid");
+  if ((e = c->lv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "lv");
+  if ((e = c->tfl.ensure(nn)) != hipSuccess) return c->hip_fail(e, "tfl");
+  if ((e = c->off_tmp.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "off_tmp");
+  if ((e = c->cnt.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "cnt");
+  if ((e = c->ids_tmp.ensure((ids_cap + 1) * 4)) != hipSuccess) return c->hip_fail(e, "ids_tmp");
+  if ((e = c->deferred.ensure((n / WALK_CHUNK + 2) * 4)) != hipSuccess) return c->hip_fail(e, "deferred");
+  if ((e = c->tile_sums.ensure((scan_tiles(n) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "tile_sums");
+  if ((e = c->stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "stats");
+  return EGM_OK;
+}
+
+static MatchWork work_view(egm_ctx* c, uint64_t ids_cap) {
+  MatchWork w{};
+  w.wid = c->wid.as<uint32_t>();
+  w.lv = c->lv.as<uint32_t>();
+  w.tfl = c->tfl.as<uint8_t>();
+  w.off_tmp = c->off_tmp.as<uint64_t>();
+  w.cnt = c->cnt.as<uint32_t>();
+  w.ids_tmp = c->ids_tmp.as<uint32_t>();
+  w.ids_cap = ids_cap;
+  w.deferred = c->deferred.as<uint32_t>();
+  w.heavy_stack = nullptr;
+  w.heavy_waves = c->heavy_waves;
+  w.heavy_stack_cap = 0;
+  w.tile_sums = c->tile_sums.as<uint64_t>();
+  w.stats = c->stats.as<MatchStats>();
+  return w;
+}
+
+static int run_match(egm_ctx* c, const Epoch& ep, const uint8_t* d_blob, const uint32_t* d_off, uint32_t n,
+                     int mode, hipStream_t s, uint64_t* d_row, uint32_t* d_ids, uint64_t ids_cap) {
+  MatchWork w = work_view(c, ids_cap);
+  MatchOut o{d_row, d_ids, ids_cap};
+  hipEvent_t evp[2] = {nullptr, nullptr};
+  if (c->timing) {
+    evp[0] = c->take_event();
+    evp[1] = c->take_event();
+  }
+  hipError_t e = launch_match(ep.view, d_blob, d_off, n, mode, w, o, s, c->timing ? evp : nullptr);
+  if (c->timing) {
+    c->ev_walk.push_back(evp[0]);
+    c->ev_walk.push_back(evp[1]);
+  }
+  if (e != hipSuccess) return c->hip_fail(e, "launch_match");
+  c->last_pending = true;
+  c->last_stream = s;
+  return EGM_OK;
+}
+
+static int sync_last(egm_ctx* c) {
+  if (!c->last_pending) return EGM_OK;
+  hipError_t e = hipStreamSynchronize(c->last_stream);
+  if (e != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize");
+  e = hipMemcpy(&c->last, c->stats.p, sizeof(MatchStats), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return c->hip_fail(e, "stats readback");
+  c->last_pending = false;
+  return EGM_OK;
+}
+
+static bool valid_offsets(const uint32_t* off, uint32_t n) {
+  if (!off) return false;
+  for (uint32_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i]) return false;
+  return true;
+}
+
+extern "C" {
+
+const char* egm_version(void) { return "emqx_gpu_match 0.1 (gfx950)"; }
+
+int egm_open(const egm_config* cfg, egm_ctx** out) {
+  if (!out) return EGM_E_INVAL;
+  *out = nullptr;
+  egm_ctx* c = new (std::nothrow) egm_ctx();
+  if (!c) return EGM_E_NOMEM;
+  c->device = cfg ? cfg->device : 0;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= c->device || c->device < 0) {
+    delete c;
+    return EGM_E_DEVICE;
+  }
+  if (set_device(c) != 0 || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return EGM_E_DEVICE;
+  }
+  if (commit_locked(c, nullptr) != EGM_OK) {  // empty epoch
+    hipStreamDestroy(c->stream);
+    delete c;
+    return EGM_E_DEVICE;
+  }
+  if (cfg && cfg->max_batch) ensure_work(c, cfg->max_batch, (uint64_t)cfg->max_batch * 64, (uint64_t)cfg->max_batch * 4);
+  *out = c;
+  return EGM_OK;
+}
+
+void egm_close(egm_ctx* c) {
+  if (!c) return;
+  {
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    set_device(c);
+    hipStreamSynchronize(c->stream);
+    c->drain_timing();
+    for (hipEvent_t e : c->ev_free) hipEventDestroy(e);
+    c->cur.reset();
+  }
+  hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* egm_last_error(egm_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int egm_table_build(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, const uint32_t* ids) {
+  if (!c || (n && (!blob || !valid_offsets(off, n)))) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  c->table.clear();
+  for (uint32_t i = 0; i < n; ++i) {
+    int r = c->table.insert(blob + off[i], off[i + 1] - off[i], ids ? ids[i] : i, nullptr);
+    if (r < 0) return c->fail(EGM_E_INVAL, "bad or duplicate filter id at index " + std::to_string(i));
+  }
+  c->table.relayout();
+  return commit_locked(c, nullptr);
+}
+
+int egm_table_apply_delta(egm_ctx* c, const egm_delta* ins, const egm_delta* del) {
+  if (!c) return EGM_E_INVAL;
+  if (ins && ins->n && (!ins->blob || !valid_offsets(ins->offsets, ins->n))) return EGM_E_INVAL;
+  if (del && del->n && (!del->blob || !valid_offsets(del->offsets, del->n))) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (ins)
+    for (uint32_t i = 0; i < ins->n; ++i) {
+      int r = c->table.insert(ins->blob + ins->offsets[i], ins->offsets[i + 1] - ins->offsets[i],
+                              ins->ids ? ins->ids[i] : NONE, nullptr);
+      if (r < 0) return c->fail(EGM_E_INVAL, "bad or duplicate filter id at insert " + std::to_string(i));
+    }
+  if (del)
+    for (uint32_t i = 0; i < del->n; ++i)
+      c->table.remove(del->blob + del->offsets[i], del->offsets[i + 1] - del->offsets[i]);
+  return EGM_OK;
+}
+
+int egm_table_commit(egm_ctx* c, uint64_t* epoch) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  return commit_locked(c, epoch);
+}
+
+int egm_table_empty(egm_ctx* c) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  return c->cur->n_filters == 0 ? 1 : 0;
+}
+
+int egm_table_stats(egm_ctx* c, uint64_t* nf, uint64_t* nn, uint64_t* ne, uint64_t* nw, uint64_t* bytes) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (nf) *nf = c->cur->n_filters;
+  if (nn) *nn = c->cur->n_nodes;
+  if (ne) *ne = c->cur->n_edges;
+  if (nw) *nw = c->cur->n_words;
+  if (bytes) *bytes = c->cur->bytes;
+  return EGM_OK;
+}
+
+int egm_filter_id(egm_ctx* c, const uint8_t* f, uint32_t len, uint32_t* id) {
+  if (!c || (!f && len) || !id) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  uint32_t r = c->table.lookup(f, len);
+  if (r == NONE) return EGM_E_NOTFOUND;
+  *id = r;
+  return EGM_OK;
+}
+
+int egm_filter_bytes(egm_ctx* c, uint32_t id, const uint8_t** bytes, uint32_t* len) {
+  if (!c || !bytes || !len) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  const uint8_t* p = c->table.filter_bytes(id, len);
+  if (!p) return EGM_E_NOTFOUND;
+  *bytes = p;
+  return EGM_OK;
+}
+
+int egm_match_device(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_off, uint32_t n,
+                     int mode, void* hip_stream, uint64_t* d_row, uint32_t* d_ids, uint64_t ids_cap,
+                     uint8_t* d_flags) {
+  if (!c || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES) || !d_row) return EGM_E_INVAL;
+  if (n && (!d_blob || !d_off || ((uintptr_t)d_blob & 3))) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  int r = ensure_work(c, n, blob_bytes, ids_cap);
+  if (r) return r;
+  std::shared_ptr<Epoch> ep = c->cur;
+  r = run_match(c, *ep, d_blob, d_off, n, mode, s, d_row, d_ids, ids_cap);
+  if (r) return r;
+  if (d_flags && n) {
+    hipError_t e = hipMemcpyAsync(d_flags, c->tfl.p, n, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return c->hip_fail(e, "flags copy");
+  }
+  return EGM_OK;
+}
+
+int egm_last_stats(egm_ctx* c, uint64_t* n_ids, uint64_t* visited, uint32_t* n_def, uint32_t* overflow,
+                   uint32_t* n_error) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  int r = sync_last(c);
+  if (r) return r;
+  if (n_ids) *n_ids = c->last.cursor;
+  if (visited) *visited = c->last.visited;
+  if (n_def) *n_def = c->last.n_deferred;
+  if (overflow) *overflow = c->last.overflow;
+  if (n_error) *n_error = c->last.errors;
+  return EGM_OK;
+}
+
+int egm_set_timing(egm_ctx* c, int enable) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  c->drain_timing();
+  c->timing = enable != 0;
+  c->walk_ms = c->fan_ms = 0;
+  c->walk_n = c->fan_n = 0;
+  return EGM_OK;
+}
+
+int egm_get_timing(egm_ctx* c, double* walk_ms, uint64_t* walk_n, double* fan_ms, uint64_t* fan_n) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  c->drain_timing();
+  if (walk_ms) *walk_ms = c->walk_ms;
+  if (walk_n) *walk_n = c->walk_n;
+  if (fan_ms) *fan_ms = c->fan_ms;
+  if (fan_n) *fan_n = c->fan_n;
+  return EGM_OK;
+}
+
+int egm_match_batch(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, int mode,
+                    egm_result** out) {
+  if (!c || !out || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES)) return EGM_E_INVAL;
+  if (n && (!off || !valid_offsets(off, n) || (!blob && off[n] > off[0]))) return EGM_E_INVAL;
+  *out = nullptr;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  hipStream_t s = c->stream;
+  // stage inputs (rebased so offsets start at 0)
+  const uint32_t base0 = n ? off[0] : 0;
+  const uint64_t bytes = n ? (uint64_t)off[n] - base0 : 0;
+  std::vector<uint32_t> loff(n + 1);
+  for (uint32_t i = 0; i <= n; ++i) loff[i] = n ? off[i] - base0 : 0;
+  hipError_t e;
+  if ((e = c->in_blob.ensure(bytes + 16)) != hipSuccess) return c->hip_fail(e, "in_blob");
+  if ((e = c->in_off.ensure(((uint64_t)n + 1) * 4)) != hipSuccess) return c->hip_fail(e, "in_off");
+  if (bytes && (e = hipMemcpyAsync(c->in_blob.p, blob + base0, bytes, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return c->hip_fail(e, "H2D blob");
+  if ((e = hipMemcpyAsync(c->in_off.p, loff.data(), ((uint64_t)n + 1) * 4, hipMemcpyHostToDevice, s)) !=
+      hipSuccess)
+    return c->hip_fail(e, "H2D offsets");
+  std::shared_ptr<Epoch> ep = c->cur;
+  uint64_t cap = (uint64_t)n * 4 + 1024;
+  if (c->ids_tmp.cap / 4 > cap + 1) cap = c->ids_tmp.cap / 4 - 1;
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    int r = ensure_work(c, n, bytes, cap);
+    if (r) return r;
+    if ((e = c->out_row.ensure(((uint64_t)n + 1) * 8)) != hipSuccess) return c->hip_fail(e, "out_row");
+    if ((e = c->out_ids.ensure((cap + 1) * 4)) != hipSuccess) return c->hip_fail(e, "out_ids");
+    r = run_match(c, *ep, c->in_blob.as<uint8_t>(), c->in_off.as<uint32_t>(), n, mode, s,
+                  c->out_row.as<uint64_t>(), c->out_ids.as<uint32_t>(), cap);
+    if (r) return r;
+    r = sync_last(c);
+    if (r) return r;
+    if (!c->last.overflow) break;
+    cap = c->last.cursor + 1024;
+    if (attempt == 2) return c->fail(EGM_E_NOMEM, "ids capacity");
+  }
+  const uint64_t nids = c->last.cursor;
+  // one allocation: struct + arrays (egm_result_free == free)
+  size_t sz = sizeof(egm_result);
+  size_t o_counts = sz;
+  sz += ((uint64_t)n * 4 + 7) & ~7ull;
+  size_t o_row = sz;
+  sz += ((uint64_t)n + 1) * 8;
+  size_t o_ids = sz;
+  sz += ((nids * 4) + 7) & ~7ull;
+  size_t o_flags = sz;
+  sz += n + 8;
+  uint8_t* mem = (uint8_t*)malloc(sz);
+  if (!mem) return c->fail(EGM_E_NOMEM, "result");
+  egm_result* res = (egm_result*)mem;
+  memset(res, 0, sizeof(*res));
+  res->n_topics = n;
+  res->n_ids = nids;
+  res->counts = (uint32_t*)(mem + o_counts);
+  res->row_ptr = (uint64_t*)(mem + o_row);
+  res->ids = (uint32_t*)(mem + o_ids);
+  res->flags = (uint8_t*)(mem + o_flags);
+  res->epoch = ep->id;
+  res->visited = c->last.visited;
+  res->n_error = c->last.errors;
+  if ((e = hipMemcpy(res->row_ptr, c->out_row.p, ((uint64_t)n + 1) * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
+      (nids && (e = hipMemcpy(res->ids, c->out_ids.p, nids * 4, hipMemcpyDeviceToHost)) != hipSuccess) ||
+      (n && (e = hipMemcpy(res->flags, c->tfl.p, n, hipMemcpyDeviceToHost)) != hipSuccess)) {
+    free(mem);
+    return c->hip_fail(e, "D2H result");
+  }
+  if (res->row_ptr[n] != nids) {
+    free(mem);
+    return c->fail(EGM_E_DEVICE, "row_ptr total mismatch");
+  }
+  uint32_t heavy = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    res->counts[i] = (uint32_t)(res->row_ptr[i + 1] - res->row_ptr[i]);
+    heavy += (res->flags[i] & TF_HEAVY) ? 1 : 0;
+  }
+  res->n_heavy = heavy;
+  *out = res;
+  if (res->n_error) {
+    c->err = "some topics exceeded the heavy-path frontier stack (flag EGM_TF_ERROR)";
+    return EGM_E_OVERFLOW;
+  }
+  return EGM_OK;
+}
+
+// ---------------------------------------------------------------- fan-out --
+int egm_subs_build(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint32_t* subs) {
+  if (!c || !row) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  for (uint32_t i = 0; i < n_slots; ++i)
+    if (row[i + 1] < row[i]) return EGM_E_INVAL;
+  const uint64_t ns = row[n_slots];
+  if (ns && !subs) return EGM_E_INVAL;
+  hipError_t e;
+  hipStreamSynchronize(c->stream);
+  if ((e = c->sub_row.ensure(((uint64_t)n_slots + 1) * 8)) != hipSuccess) return c->hip_fail(e, "sub_row");
+  if ((e = c->sub_ids.ensure(ns * 4 + 16)) != hipSuccess) return c->hip_fail(e, "sub_ids");
+  if ((e = hipMemcpy(c->sub_row.p, row, ((uint64_t)n_slots + 1) * 8, hipMemcpyHostToDevice)) != hipSuccess)
+    return c->hip_fail(e, "H2D sub_row");
+  if (ns && (e = hipMemcpy(c->sub_ids.p, subs, ns * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    return c->hip_fail(e, "H2D subs");
+  c->n_fid_slots = n_slots;
+  return EGM_OK;
+}
+
+static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids, uint32_t n, hipStream_t s,
+                      uint64_t* d_drow, uint32_t* d_fid, uint32_t* d_sub, uint64_t cap, uint64_t* total) {
+  uint64_t nids = 0;
+  hipError_t e = hipMemcpyAsync(&nids, d_mrow + n, 8, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return c->hip_fail(e, "match_row readback");
+  if (nids >= 0xFFFFFFF0ull) return c->fail(EGM_E_INVAL, "too many matched ids for one fan-out batch");
+  if ((e = c->f_dc.ensure((nids + 1) * 4)) != hipSuccess) return c->hip_fail(e, "f_dc");
+  if ((e = c->f_dpos.ensure((nids + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_dpos");
+  if ((e = c->f_tiles.ensure((scan_tiles((uint32_t)nids) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_tiles");
+  if ((e = c->f_ovf.ensure(16)) != hipSuccess) return c->hip_fail(e, "f_ovf");
+  SubTable st{c->sub_row.as<uint64_t>(), c->sub_ids.as<uint32_t>(), c->n_fid_slots};
+  hipEvent_t evp[2] = {nullptr, nullptr};
+  if (c->timing) {
+    evp[0] = c->take_event();
+    evp[1] = c->take_event();
+  }
+  e = launch_fanout(st, d_mrow, d_mids, n, nids, d_drow, d_fid, d_sub, cap, c->f_dc.as<uint32_t>(),
+                    c->f_dpos.as<uint64_t>(), c->f_tiles.as<uint64_t>(), c->f_ovf.as<unsigned int>(), s,
+                    c->timing ? evp : nullptr);
+  if (c->timing) {
+    c->ev_fan.push_back(evp[0]);
+    c->ev_fan.push_back(evp[1]);
+  }
+  if (e != hipSuccess) return c->hip_fail(e, "launch_fanout");
+  if (total) {
+    unsigned int ovf = 0;
+    if ((e = hipMemcpyAsync(total, d_drow + n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(&ovf, c->f_ovf.p, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+      return c->hip_fail(e, "fanout readback");
+    if (ovf) return EGM_E_OVERFLOW;
+  }
+  return EGM_OK;
+}
+
+int egm_fanout_device(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids, uint32_t n, void* hip_stream,
+                      uint64_t* d_drow, uint32_t* d_fid, uint32_t* d_sub, uint64_t cap) {
+  if (!c || !d_mrow || !d_drow) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  return run_fanout(c, d_mrow, d_mids, n, s, d_drow, d_fid, d_sub, cap, nullptr);
+}
+
+int egm_fanout_batch(egm_ctx* c, const egm_result* m, egm_delivery** out) {
+  if (!c || !m || !out) return EGM_E_INVAL;
+  *out = nullptr;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  hipStream_t s = c->stream;
+  const uint32_t n = m->n_topics;
+  const uint64_t nids = m->row_ptr[n];
+  hipError_t e;
+  if ((e = c->f_mrow.ensure(((uint64_t)n + 1) * 8)) != hipSuccess) return c->hip_fail(e, "f_mrow");
+  if ((e = c->f_mids.ensure(nids * 4 + 16)) != hipSuccess) return c->hip_fail(e, "f_mids");
+  if ((e = hipMemcpyAsync(c->f_mrow.p, m->row_ptr, ((uint64_t)n + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return c->hip_fail(e, "H2D match rows");
+  if (nids && (e = hipMemcpyAsync(c->f_mids.p, m->ids, nids * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return c->hip_fail(e, "H2D match ids");
+  uint64_t cap = nids * 2 + 1024, total = 0;
+  if ((e = c->f_drow.ensure(((uint64_t)n + 1) * 8)) != hipSuccess) return c->hip_fail(e, "f_drow");
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if ((e = c->f_dfid.ensure(cap * 4)) != hipSuccess) return c->hip_fail(e, "f_dfid");
+    if ((e = c->f_dsub.ensure(cap * 4)) != hipSuccess) return c->hip_fail(e, "f_dsub");
+    int r = run_fanout(c, c->f_mrow.as<uint64_t>(), c->f_mids.as<uint32_t>(), n, s, c->f_drow.as<uint64_t>(),
+                       c->f_dfid.as<uint32_t>(), c->f_dsub.as<uint32_t>(), cap, &total);
+    if (r == EGM_OK) break;
+    if (r != EGM_E_OVERFLOW || attempt == 1) return r;
+    cap = total + 1024;
+  }
+  size_t sz = sizeof(egm_delivery);
+  size_t o_row = sz;
+  sz += ((uint64_t)n + 1) * 8;
+  size_t o_fid = sz;
+  sz += (total * 4 + 7) & ~7ull;
+  size_t o_sub = sz;
+  sz += (total * 4 + 7) & ~7ull;
+  uint8_t* mem = (uint8_t*)malloc(sz);
+  if (!mem) return c->fail(EGM_E_NOMEM, "delivery");
+  egm_delivery* d = (egm_delivery*)mem;
+  d->n_topics = n;
+  d->n_deliveries = total;
+  d->row_ptr = (uint64_t*)(mem + o_row);
+  d->fid = (uint32_t*)(mem + o_fid);
+  d->sub = (uint32_t*)(mem + o_sub);
+  if ((e = hipMemcpy(d->row_ptr, c->f_drow.p, ((uint64_t)n + 1) * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
+      (total && (e = hipMemcpy(d->fid, c->f_dfid.p, total * 4, hipMemcpyDeviceToHost)) != hipSuccess) ||
+      (total && (e = hipMemcpy(d->sub, c->f_dsub.p, total * 4, hipMemcpyDeviceToHost)) != hipSuccess)) {
+    free(mem);
+    return c->hip_fail(e, "D2H deliveries");
+  }
+  *out = d;
+  return EGM_OK;
+}
+
+void egm_result_free(void* r) { free(r); }
+
+// ---------------------------------------------------- host-only image API --
+struct egm_image {
+  HostTable t;
+};
+
+egm_image* egm_image_new(void) { return new (std::nothrow) egm_image(); }
+void egm_image_free(egm_image* im) { delete im; }
+int egm_image_insert(egm_image* im, const uint8_t* f, uint32_t len, uint32_t id) {
+  if (!im || (!f && len)) return EGM_E_INVAL;
+  return im->t.insert(f, len, id, nullptr);
+}
+int egm_image_remove(egm_image* im, const uint8_t* f, uint32_t len) {
+  if (!im || (!f && len)) return EGM_E_INVAL;
+  return im->t.remove(f, len);
+}
+void egm_image_relayout(egm_image* im) {
+  if (im) im->t.relayout();
+}
+int egm_image_get_view(egm_image* im, egm_image_view* v) {
+  if (!im || !v) return EGM_E_INVAL;
+  const HostTable& t = im->t;
+  v->nodes = t.nodes.data();
+  v->n_nodes = t.nodes.size();
+  v->hash_child = t.hash_child.data();
+  v->edges = t.edges.data();
+  v->n_edge_slots = t.edges.size();
+  v->edge_mask = t.edge_mask();
+  v->dict = t.dict.data();
+  v->n_dict_slots = t.dict.size();
+  v->dict_mask = t.dict_mask();
+  v->dict_blob = t.dict_blob.data();
+  v->dict_off = t.dict_off.data();
+  v->n_words = t.n_words();
+  v->n_filters = t.n_filters();
+  v->n_live_nodes = t.n_nodes_live();
+  v->n_edges = t.n_edges();
+  return EGM_OK;
+}
+int egm_shard_assign(const uint8_t* blob, const uint32_t* off, uint32_t n, uint32_t g, uint32_t* out) {
+  if (!off || !out || g == 0 || (n && !blob)) return EGM_E_INVAL;
+  for (uint32_t i = 0; i < n; ++i) out[i] = filter_shard(blob + off[i], off[i + 1] - off[i], g);
+  return EGM_OK;
+}
+uint64_t egm_word_hash(const uint8_t* p, uint32_t len) { return word_hash(p, len); }
+uint32_t egm_edge_bucket(uint32_t parent, uint32_t w, uint32_t mask) { return edge_bucket(parent, w, mask); }
+
+}  // extern "C"

@@ -1,0 +1,109 @@
+// egm_common.h — layouts and hash functions shared by the host table builder
+// (egm_table.cpp, g++) and the gfx950 kernels (egm_kernels.hip, hipcc).
+//
+// The reference keeps the wildcard index as string keys {Prefix,0}/{Filter,1}
+// in a mnesia ordered_set (apps/emqx/src/emqx_trie.erl:45-51,61-71) and probes
+// it once per visited prefix (:192-206).  Here the same filter set is a
+// word-level trie flattened into three HBM arrays:
+//
+//   nodes[]  16 B  {plus_child, hash_fid, term_fid, meta}
+//   edges[]  64 B buckets of four 16 B slots {parent, word_id, child, child_flags}
+//   dict[]   32 B slots {hash64, word_id, len, inline bytes[16]}  (+ blob for long words)
+//
+// A literal transition is one bucket read keyed by (node, word_id); word ids
+// come from the dictionary with byte-exact verification, so a 64-bit hash
+// collision can never create a false edge.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define EGM_HD __host__ __device__ __forceinline__
+#else
+#define EGM_HD inline
+#endif
+
+namespace egm {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;        // empty id / "no child"
+constexpr uint32_t TOMB = 0xFFFFFFFEu;        // deleted edge slot (parent field)
+
+// word ids reserved for topic words that are not literal dictionary words
+constexpr uint32_t WID_NONE = 0xFFFFFFFFu;    // literal word absent from every filter
+constexpr uint32_t WID_PLUS = 0xFFFFFFFDu;    // the word '+'
+constexpr uint32_t WID_HASH = 0xFFFFFFFCu;    // the word '#'
+constexpr uint32_t WID_MAX  = 0xFFFFFFF0u;    // real ids are < WID_MAX
+
+// node flag bits (4 bits, carried in work items and edge slots)
+constexpr uint32_t F_LIT  = 1u;   // has >= 1 literal child
+constexpr uint32_t F_PLUS = 2u;   // has a '+' child
+constexpr uint32_t F_HASH = 4u;   // "P/#" is a filter (hash_fid valid)
+constexpr uint32_t F_TERM = 8u;   // "P" itself is a filter (term_fid valid)
+
+// per-topic flags (egm_result.flags)
+constexpr uint8_t TF_WILDCARD = 1;   // topic has a '+' or '#' word (emqx_topic.erl:53-62)
+constexpr uint8_t TF_DOLLAR   = 2;   // first word starts with '$' (emqx_trie.erl:208-215)
+constexpr uint8_t TF_HEAVY    = 4;   // matched by the overflow (heavy) kernel
+constexpr uint8_t TF_ERROR    = 8;   // could not be matched (see egm_last_error)
+
+constexpr int EDGE_BUCKET = 4;       // slots per 64 B bucket
+
+struct NodeRec {          // 16 B, one dwordx4 load
+  uint32_t plus_child;    // node reached by '+', or NONE
+  uint32_t hash_fid;      // filter id of "P/#", or NONE
+  uint32_t term_fid;      // filter id of "P", or NONE
+  uint32_t meta;          // [0:4) flags of plus_child, [4:8) own flags
+};
+
+struct EdgeSlot {         // 16 B
+  uint32_t parent;        // NONE = empty, TOMB = deleted
+  uint32_t wid;
+  uint32_t child;
+  uint32_t child_flags;
+};
+
+struct DictSlot {         // 32 B
+  uint64_t hash;
+  uint32_t wid;           // NONE = empty
+  uint32_t len;
+  uint8_t inl[16];        // first min(len,16) bytes
+};
+
+static_assert(sizeof(NodeRec) == 16, "NodeRec");
+static_assert(sizeof(EdgeSlot) == 16, "EdgeSlot");
+static_assert(sizeof(DictSlot) == 32, "DictSlot");
+
+// ---- hashing (identical on host and device) --------------------------------
+constexpr uint64_t FNV_BASIS = 0xcbf29ce484222325ull;
+constexpr uint64_t FNV_PRIME = 0x100000001b3ull;
+
+EGM_HD uint64_t mix64(uint64_t x) {   // murmur3 fmix64
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+EGM_HD uint64_t fnv_step(uint64_t h, uint8_t b) { return (h ^ b) * FNV_PRIME; }
+
+EGM_HD uint64_t word_hash_finish(uint64_t fnv, uint32_t len) {
+  return mix64(fnv ^ ((uint64_t)len << 56));
+}
+
+EGM_HD uint64_t word_hash(const uint8_t* p, uint32_t len) {
+  uint64_t h = FNV_BASIS;
+  for (uint32_t i = 0; i < len; ++i) h = fnv_step(h, p[i]);
+  return word_hash_finish(h, len);
+}
+
+EGM_HD uint32_t edge_bucket(uint32_t parent, uint32_t wid, uint32_t mask) {
+  return (uint32_t)(mix64(((uint64_t)parent << 32) | wid) & mask);
+}
+
+// filter -> shard assignment for multi-GPU filter sharding
+EGM_HD uint32_t filter_shard(const uint8_t* p, uint32_t len, uint32_t n_shards) {
+  return (uint32_t)(word_hash(p, len) % n_shards);
+}
+
+}  // namespace egm

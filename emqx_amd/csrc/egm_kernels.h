@@ -1,0 +1,76 @@
+// egm_kernels.h — host-callable launchers for the gfx950 kernels in
+// egm_kernels.hip.  Plain pointers only (device pointers unless stated).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include "egm_common.h"
+
+namespace egm {
+
+struct DevTable {                 // one epoch of the filter graph in HBM
+  const NodeRec* nodes;
+  const uint32_t* hash_child;
+  const EdgeSlot* edges;
+  uint32_t edge_mask;             // n_buckets - 1
+  const DictSlot* dict;
+  uint32_t dict_mask;
+  const uint8_t* dict_blob;
+  const uint64_t* dict_off;
+};
+
+struct MatchStats {               // device-side counters, zeroed per batch
+  unsigned long long cursor;      // ids reserved in ids_tmp
+  unsigned long long visited;     // NFA states expanded (light + heavy)
+  unsigned int n_deferred;        // chunks handed to the heavy kernel
+  unsigned int heavy_next;        // heavy work counter
+  unsigned int overflow;          // ids_tmp capacity exceeded
+  unsigned int errors;            // topics the heavy kernel could not finish
+  unsigned int pad[2];
+};
+
+struct MatchWork {                // per-batch device workspace
+  uint32_t* wid;                  // [blob_bytes + n] word ids, topic t at off[t] + t
+  uint32_t* lv;                   // [n] levels
+  uint8_t* tfl;                   // [n] TF_* flags
+  uint64_t* off_tmp;              // [n] start of topic t's ids in ids_tmp
+  uint32_t* cnt;                  // [n] number of ids of topic t
+  uint32_t* ids_tmp;              // [ids_cap] chunk-ordered ids
+  uint64_t ids_cap;
+  uint32_t* deferred;             // [n / CHUNK + 1] chunk ids for the heavy kernel
+  uint2* heavy_stack;             // [heavy_waves * heavy_stack_cap]
+  uint32_t heavy_waves;
+  uint32_t heavy_stack_cap;
+  uint64_t* tile_sums;            // scan scratch
+  MatchStats* stats;
+};
+
+struct MatchOut {                 // CSR result (device)
+  uint64_t* row_ptr;              // [n + 1]
+  uint32_t* ids;                  // [ids_cap]
+  uint64_t ids_cap;
+};
+
+// launch sizing shared with the host (egm_capi.cpp)
+constexpr int WALK_CHUNK = 128;   // topics per wave chunk
+int walk_grid_blocks(uint32_t n_topics);
+size_t scan_tiles(uint32_t n);
+
+// Timing hooks: when ev != nullptr, ev[0]/ev[1] bracket the walk kernel.
+hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n,
+                        int mode, const MatchWork& w, const MatchOut& out, hipStream_t s,
+                        hipEvent_t* ev_walk);
+
+// Fan-out (emqx_broker:dispatch/2, emqx_broker.erl:283-324): expand each
+// topic's filter ids through the filter -> subscriber CSR.
+struct SubTable {
+  const uint64_t* row;            // [n_fid_slots + 1] indexed by filter id
+  const uint32_t* subs;           // subscriber ids; bit 31 set = shared group id
+  uint32_t n_fid_slots;
+};
+hipError_t launch_fanout(const SubTable& st, const uint64_t* match_row, const uint32_t* match_ids,
+                         uint32_t n, uint64_t nids, uint64_t* deliv_row, uint32_t* deliv_fid,
+                         uint32_t* deliv_sub, uint64_t deliv_cap, uint32_t* dcount, uint64_t* dpos,
+                         uint64_t* tile_sums, unsigned int* overflow, hipStream_t s, hipEvent_t* ev);
+
+}  // namespace egm

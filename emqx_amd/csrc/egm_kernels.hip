@@ -1,0 +1,734 @@
+// egm_kernels.hip — gfx950 kernels for publish-time route lookup.
+//
+// Replaces, per batch of publish topics:
+//   emqx_topic:words/1            apps/emqx/src/emqx_topic.erl:153-164   -> k_tokenise
+//   emqx_trie:match/1 (+ do_match, match_compact, 'match_#', lookup_topic,
+//   has_prefix)                   apps/emqx/src/emqx_trie.erl:100-114,190-270 -> k_walk / k_heavy
+//   emqx_router:match_routes/1    apps/emqx/src/emqx_router.erl:129-141  -> mode EGM_MODE_ROUTES
+//   emqx_broker:dispatch/2        apps/emqx/src/emqx_broker.erl:283-324  -> k_fanout_*
+//
+// The walk is an NFA frontier expansion over the word-level trie (egm_common.h).
+// One wavefront owns a chunk of WALK_CHUNK topics; its work items
+// (node, level, topic, flags) live in an LDS stack.  Each iteration pops up to
+// 64 items (one per lane), issues the two independent loads an item needs (the
+// node record and the literal-edge bucket), and compacts the produced matches
+// and children back into LDS with __ballot / mbcnt.  At the end of a chunk the
+// staged matches are counting-sorted by topic and written with a single
+// atomic reservation.  Chunks whose frontier or match count overflows LDS are
+// re-run by k_heavy (one topic per wave, 64 KB LDS stack, count-then-fill).
+//
+// This is pointer chasing over hashed edges — HBM / latency bound; no MFMA.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "egm_kernels.h"
+
+namespace egm {
+
+constexpr int MODE_TRIE = 0;
+constexpr int MODE_ROUTES = 1;
+
+constexpr int WALK_WAVES = 4;        // waves per 256-thread block
+constexpr int WALK_STACK = 512;      // items per wave
+constexpr int WALK_STAGE = 1024;     // staged matches per wave chunk
+constexpr int WALK_WORDS = 1024;     // staged topic word ids per wave chunk
+constexpr int HEAVY_STACK = 8192;    // items (64 KB LDS) per heavy wave
+constexpr int TOK_BLOCK = 256;
+constexpr int TOK_LDS = 16384;
+constexpr int SCAN_TILE = 2048;      // counts per scan tile (256 threads x 8)
+
+static_assert(WALK_CHUNK <= 256 && WALK_CHUNK % 64 == 0, "chunk");
+
+// ------------------------------------------------------------ primitives ----
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint32_t popc(uint64_t m) { return (uint32_t)__popcll(m); }
+
+// Make one lane's LDS writes visible to the other lanes of the same wave.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t* total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// item = (node, meta); meta = level[0:17) | t[17:25) | flags[25:29) | wc<<29 | exact<<30
+__device__ __forceinline__ uint32_t mk_meta(uint32_t level, uint32_t t, uint32_t fl, uint32_t wc,
+                                            uint32_t ex) {
+  return level | (t << 17) | (fl << 25) | (wc << 29) | (ex << 30);
+}
+
+__device__ __forceinline__ uint4 ld16(const void* p) { return *(const uint4*)p; }
+
+// ------------------------------------------------------------ dictionary ----
+__device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t k) {
+  uint32_t w = (k < 8) ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
+  return (w >> (8 * (k & 3))) & 0xFFu;
+}
+
+// Byte-exact dictionary probe (linear probing over 32 B slots).
+__device__ uint32_t dict_probe(const DevTable& tab, uint64_t h, const uint8_t* p, uint32_t len) {
+  uint32_t i = (uint32_t)h & tab.dict_mask;
+  for (;;) {
+    const uint8_t* sp = (const uint8_t*)(tab.dict + i);
+    uint4 a = ld16(sp);  // {hash lo, hash hi, wid, len}
+    if (a.z == NONE) return WID_NONE;
+    if (a.x == (uint32_t)h && a.y == (uint32_t)(h >> 32) && a.w == len) {
+      bool eq = true;
+      if (len <= 16) {
+        uint4 b = ld16(sp + 16);
+        for (uint32_t k = 0; k < len; ++k) eq &= byte_of(b, k) == p[k];
+      } else {
+        const uint8_t* q = tab.dict_blob + tab.dict_off[a.z];
+        for (uint32_t k = 0; k < len; ++k) eq &= q[k] == p[k];
+      }
+      if (eq) return a.z;
+    }
+    i = (i + 1) & tab.dict_mask;
+  }
+}
+
+// -------------------------------------------------------------- tokenise ----
+// emqx_topic:words/1 (emqx_topic.erl:153-164) + wildcard/1 (:53-62) for a
+// batch: one lane per topic, the block's bytes staged in LDS by 4-byte loads.
+// Output: level count, TF_* flags and one word id per level at wid[off[t]+t+l].
+__global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint8_t* __restrict__ blob,
+                                                        const uint32_t* __restrict__ off, uint32_t n,
+                                                        uint32_t* __restrict__ wid, uint32_t* __restrict__ lv,
+                                                        uint8_t* __restrict__ tfl) {
+  __shared__ __attribute__((aligned(16))) uint32_t sw[TOK_LDS / 4];
+  const uint32_t t0 = blockIdx.x * TOK_BLOCK;
+  if (t0 >= n) return;
+  const uint32_t t1 = min(t0 + (uint32_t)TOK_BLOCK, n);
+  const uint32_t s = off[t0], e = off[t1];
+  const uint32_t sa = s & ~3u;
+  const bool staged = (e - sa) <= (uint32_t)TOK_LDS;
+  uint8_t* sb = (uint8_t*)sw;
+  if (staged) {
+    const uint32_t ew = e & ~3u;
+    const uint32_t nfull = (ew - sa) >> 2;
+    const uint32_t* src = (const uint32_t*)(blob + sa);
+    for (uint32_t i = threadIdx.x; i < nfull; i += TOK_BLOCK) sw[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < e - ew; i += TOK_BLOCK) sb[ew - sa + i] = blob[ew + i];
+  }
+  __syncthreads();
+  const uint32_t t = t0 + threadIdx.x;
+  if (t >= t1) return;
+  const uint32_t ts = off[t], len = off[t + 1] - ts;
+  const uint8_t* p = staged ? sb + (ts - sa) : blob + ts;
+  const uint32_t base = ts + t;
+  uint32_t l = 0, ws = 0;
+  uint8_t fl = (len > 0 && p[0] == '$') ? TF_DOLLAR : 0;
+  uint64_t h = FNV_BASIS;
+  for (uint32_t i = 0; i <= len; ++i) {
+    if (i < len) {
+      const uint8_t c = p[i];
+      if (c != '/') {
+        h = fnv_step(h, c);
+        continue;
+      }
+    }
+    const uint32_t wl = i - ws;
+    uint32_t w;
+    if (wl == 1 && p[ws] == '+') {
+      w = WID_PLUS;
+      fl |= TF_WILDCARD;
+    } else if (wl == 1 && p[ws] == '#') {
+      w = WID_HASH;
+      fl |= TF_WILDCARD;
+    } else {
+      w = dict_probe(tab, word_hash_finish(h, wl), p + ws, wl);
+    }
+    wid[base + l] = w;
+    ++l;
+    ws = i + 1;
+    h = FNV_BASIS;
+  }
+  lv[t] = l;
+  tfl[t] = fl;
+}
+
+// ------------------------------------------------------------ NFA expand ----
+// Literal transition: one 64 B bucket of four {parent, wid, child, flags}
+// slots; slots fill in probe order, so the first empty slot ends the search.
+__device__ __forceinline__ uint32_t edge_probe(const DevTable& tab, uint32_t node, uint32_t w,
+                                               uint32_t* cfl) {
+  uint32_t b = edge_bucket(node, w, tab.edge_mask);
+  for (;;) {
+    const EdgeSlot* bp = tab.edges + (size_t)b * EDGE_BUCKET;
+#pragma unroll
+    for (int k = 0; k < EDGE_BUCKET; ++k) {
+      uint4 s = ld16(bp + k);
+      if (s.x == node && s.y == w) {
+        *cfl = s.w;
+        return s.z;
+      }
+      if (s.x == NONE) return NONE;
+    }
+    b = (b + 1) & tab.edge_mask;
+  }
+}
+
+struct Expand {
+  uint32_t e0, e1;     // emitted filter ids ('P/#', 'P')
+  uint2 c0, c1;        // children (literal, '+')
+  bool h0, h1, hc0, hc1;
+};
+
+// Expand one (node, level) state of topic t.  This is match_compact/4's body
+// (emqx_trie.erl:251-266) without the string keys:
+//   'match_#'(Prefix)          -> e0 = hash_fid of node (every level <= D)
+//   recurse Prefix/Word        -> c0 = literal child
+//   recurse Prefix/'+'         -> c1 = plus child
+//   lookup_topic(Topic, IsWc)  -> e1 = term_fid at level == D if the path
+//                                 took a '+' (TRIE mode) / always (ROUTES)
+//   do_match/1's '$' rule      -> at the root of a '$' topic no '#'/'+'
+//                                 (:208-215), and the single-word probe
+//                                 lookup_topic(Prefix) -> e1 at D == 1
+// `exact` items walk a wildcard topic as a literal key (ROUTES mode only:
+// lookup_routes(Topic) of emqx_router.erl:129-134).
+__device__ __forceinline__ void expand(const DevTable& tab, int mode, uint2 it, uint32_t D,
+                                       uint32_t tflags, uint32_t w, Expand& x) {
+  const uint32_t node = it.x, meta = it.y;
+  const uint32_t level = meta & 0x1FFFFu;
+  const uint32_t tm = meta & (0xFFu << 17);
+  const uint32_t fl = (meta >> 25) & 0xFu, wc = (meta >> 29) & 1u, ex = (meta >> 30) & 1u;
+  const bool atend = level == D;
+  x.h0 = x.h1 = x.hc0 = x.hc1 = false;
+  if (!ex) {
+    const bool rootd = (level == 0) && (tflags & TF_DOLLAR);
+    const bool want_hash = (fl & F_HASH) && !rootd;
+    const bool want_term =
+        atend && (fl & F_TERM) && (mode == MODE_ROUTES || wc || (D == 1 && (tflags & TF_DOLLAR)));
+    const bool want_plus = !atend && (fl & F_PLUS) && !rootd;
+    const bool want_lit = !atend && (fl & F_LIT) && w < WID_MAX;
+    uint4 rec = make_uint4(NONE, NONE, NONE, 0);
+    if (want_hash || want_term || want_plus) rec = ld16(tab.nodes + node);
+    uint32_t cfl = 0, child = NONE;
+    if (want_lit) child = edge_probe(tab, node, w, &cfl);
+    x.e0 = rec.y;
+    x.h0 = want_hash;
+    x.e1 = rec.z;
+    x.h1 = want_term;
+    x.c0 = make_uint2(child, (level + 1) | tm | (cfl << 25) | (wc << 29));
+    x.hc0 = child != NONE;
+    x.c1 = make_uint2(rec.x, (level + 1) | tm | ((rec.w & 0xFu) << 25) | (1u << 29));
+    x.hc1 = want_plus;
+  } else {
+    const uint4 rec = ld16(tab.nodes + node);
+    if (atend) {
+      x.e1 = rec.z;
+      x.h1 = rec.z != NONE;
+      return;
+    }
+    uint32_t child = NONE, cfl = 0;
+    if (w == WID_PLUS) child = rec.x;
+    else if (w == WID_HASH) child = tab.hash_child[node];
+    else if (w < WID_MAX) child = edge_probe(tab, node, w, &cfl);
+    x.c0 = make_uint2(child, (level + 1) | tm | (1u << 30));
+    x.hc0 = child != NONE;
+  }
+}
+
+// ------------------------------------------------------------------ walk ----
+struct alignas(16) WaveLds {
+  uint2 stack[WALK_STACK];
+  uint32_t stage_fid[WALK_STAGE];
+  uint32_t words[WALK_WORDS];
+  uint32_t tbase[WALK_CHUNK];   // word base: LDS index (staged) or wid index
+  uint32_t tinfo[WALK_CHUNK];   // levels | flags << 24
+  uint32_t cnt[WALK_CHUNK];
+  uint8_t stage_t[WALK_STAGE];
+};
+
+__global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const uint32_t* __restrict__ off,
+                                                          uint32_t n, int mode, MatchWork w) {
+  __shared__ WaveLds lds_all[WALK_WAVES];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  WaveLds& L = lds_all[wave];
+  const uint32_t nwaves = gridDim.x * WALK_WAVES;
+  const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  const uint32_t root_fl = (tab.nodes[0].meta >> 4) & 0xFu;
+  uint64_t visited = 0;
+
+  for (uint32_t c = blockIdx.x * WALK_WAVES + wave; c < nchunks; c += nwaves) {
+    const uint32_t t0 = c * WALK_CHUNK;
+    const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
+
+    // ---- topic info + word staging (word bases are any disjoint layout) ----
+    uint32_t dsum = 0;
+    uint32_t dl[WALK_CHUNK / 64];
+#pragma unroll
+    for (int k = 0; k < WALK_CHUNK / 64; ++k) {
+      const uint32_t j = lane + 64 * k;
+      uint32_t D = 0, f = 0;
+      if (j < nt) {
+        D = w.lv[t0 + j];
+        f = w.tfl[t0 + j];
+      }
+      dl[k] = D;
+      dsum += D;
+      L.tinfo[j] = D | (f << 24);
+      L.cnt[j] = 0;
+    }
+    uint32_t wtotal;
+    uint32_t wb = wave_excl_scan(dsum, lane, &wtotal);
+    const bool staged = wtotal <= (uint32_t)WALK_WORDS;
+#pragma unroll
+    for (int k = 0; k < WALK_CHUNK / 64; ++k) {
+      const uint32_t j = lane + 64 * k;
+      if (j < nt) {
+        const uint32_t gb = off[t0 + j] + t0 + j;
+        if (staged) {
+          L.tbase[j] = wb;
+          const uint32_t* src = w.wid + gb;
+          uint32_t i = 0;
+          for (; i + 4 <= dl[k]; i += 4) {
+            uint32_t a0 = src[i], a1 = src[i + 1], a2 = src[i + 2], a3 = src[i + 3];
+            L.words[wb + i] = a0;
+            L.words[wb + i + 1] = a1;
+            L.words[wb + i + 2] = a2;
+            L.words[wb + i + 3] = a3;
+          }
+          for (; i < dl[k]; ++i) L.words[wb + i] = src[i];
+          wb += dl[k];
+        } else {
+          L.tbase[j] = gb;
+        }
+      }
+    }
+    wave_sync();
+
+    uint32_t next = 0, sp = 0, nstage = 0;
+    bool ovf = false;
+    for (;;) {
+      if (sp < 64 && next < nt) {  // refill with new roots
+        const uint32_t k = min(64u - sp, nt - next);
+        bool has = false;
+        uint2 it = make_uint2(0, 0);
+        if (lane < k) {
+          const uint32_t j = next + lane;
+          const uint32_t f = L.tinfo[j] >> 24;
+          if (!(f & TF_WILDCARD)) {
+            has = true;
+            it = make_uint2(0, mk_meta(0, j, root_fl, 0, 0));
+          } else if (mode == MODE_ROUTES) {
+            has = true;
+            it = make_uint2(0, mk_meta(0, j, 0, 0, 1));
+          }
+        }
+        const uint64_t b = __ballot(has);
+        if (has) L.stack[sp + mbcnt(b)] = it;
+        sp += popc(b);
+        next += k;
+        wave_sync();
+      }
+      if (sp == 0) {
+        if (next >= nt) break;
+        continue;
+      }
+      const uint32_t take = min(64u, sp);
+      const uint32_t bi = sp - take;
+      const bool act = lane < take;
+      uint2 it = make_uint2(0, 0);
+      if (act) it = L.stack[bi + lane];
+      sp = bi;
+      wave_sync();
+
+      Expand x;
+      x.h0 = x.h1 = x.hc0 = x.hc1 = false;
+      uint32_t t = 0;
+      if (act) {
+        t = (it.y >> 17) & 0xFFu;
+        const uint32_t ti = L.tinfo[t];
+        const uint32_t D = ti & 0xFFFFFFu, tf = ti >> 24;
+        const uint32_t level = it.y & 0x1FFFFu;
+        uint32_t wd = WID_NONE;
+        if (level < D) wd = staged ? L.words[L.tbase[t] + level] : w.wid[L.tbase[t] + level];
+        expand(tab, mode, it, D, tf, wd, x);
+      }
+      // emits -> stage (matches of one chunk, tagged with the topic)
+      const uint64_t b0 = __ballot(x.h0), b1 = __ballot(x.h1);
+      const uint32_t n0 = popc(b0), ne = n0 + popc(b1);
+      if (nstage + ne > (uint32_t)WALK_STAGE) {
+        ovf = true;
+        break;
+      }
+      if (x.h0) {
+        const uint32_t p = nstage + mbcnt(b0);
+        L.stage_fid[p] = x.e0;
+        L.stage_t[p] = (uint8_t)t;
+        atomicAdd(&L.cnt[t], 1u);
+      }
+      if (x.h1) {
+        const uint32_t p = nstage + n0 + mbcnt(b1);
+        L.stage_fid[p] = x.e1;
+        L.stage_t[p] = (uint8_t)t;
+        atomicAdd(&L.cnt[t], 1u);
+      }
+      nstage += ne;
+      // children -> stack
+      const uint64_t c0 = __ballot(x.hc0), c1 = __ballot(x.hc1);
+      const uint32_t m0 = popc(c0), nc = m0 + popc(c1);
+      if (sp + nc > (uint32_t)WALK_STACK) {
+        ovf = true;
+        break;
+      }
+      if (x.hc0) L.stack[sp + mbcnt(c0)] = x.c0;
+      if (x.hc1) L.stack[sp + m0 + mbcnt(c1)] = x.c1;
+      sp += nc;
+      visited += take;
+      wave_sync();
+    }
+    wave_sync();
+
+    if (ovf) {  // hand the whole chunk to k_heavy
+      if (lane == 0) {
+        const uint32_t d = atomicAdd(&w.stats->n_deferred, 1u);
+        w.deferred[d] = c;
+      }
+      for (uint32_t j = lane; j < nt; j += 64) {
+        w.cnt[t0 + j] = 0;
+        w.off_tmp[t0 + j] = 0;
+      }
+      wave_sync();
+      continue;
+    }
+
+    // ---- flush: per-topic counts -> one reservation -> counting sort ----
+    uint32_t cl[WALK_CHUNK / 64];
+    uint32_t csum = 0;
+#pragma unroll
+    for (int k = 0; k < WALK_CHUNK / 64; ++k) {
+      const uint32_t j = lane * (WALK_CHUNK / 64) + k;   // consecutive per lane
+      cl[k] = (j < nt) ? L.cnt[j] : 0u;
+      csum += cl[k];
+    }
+    uint32_t ctotal;
+    uint32_t cb = wave_excl_scan(csum, lane, &ctotal);
+    unsigned long long base = 0;
+    if (lane == 0 && ctotal) base = atomicAdd(&w.stats->cursor, (unsigned long long)ctotal);
+    base = __shfl(base, 0, 64);
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < WALK_CHUNK / 64; ++k) {
+      const uint32_t j = lane * (WALK_CHUNK / 64) + k;
+      if (j < nt) {
+        w.off_tmp[t0 + j] = base + cb;
+        w.cnt[t0 + j] = cl[k];
+        L.cnt[j] = cb;
+      }
+      cb += cl[k];
+    }
+    wave_sync();
+    if (base + ctotal > w.ids_cap) {
+      if (lane == 0) atomicOr(&w.stats->overflow, 1u);
+    } else {
+      for (uint32_t i = lane; i < nstage; i += 64) {
+        const uint32_t tt = L.stage_t[i];
+        const uint32_t p = atomicAdd(&L.cnt[tt], 1u);
+        w.ids_tmp[base + p] = L.stage_fid[i];
+      }
+    }
+    wave_sync();
+  }
+  if (lane == 0 && visited) atomicAdd(&w.stats->visited, (unsigned long long)visited);
+}
+
+// ----------------------------------------------------------------- heavy ----
+// Topics of deferred chunks: one wave per topic, 64 KB LDS stack, two passes
+// (count, then fill at a reserved offset) so the output needs no staging.
+__global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __restrict__ off, uint32_t n,
+                                              int mode, MatchWork w) {
+  __shared__ uint2 stk[HEAVY_STACK];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t root_fl = (tab.nodes[0].meta >> 4) & 0xFu;
+  const uint32_t total = w.stats->n_deferred * (uint32_t)WALK_CHUNK;
+  uint64_t visited = 0;
+  for (;;) {
+    uint32_t idx = 0;
+    if (lane == 0) idx = atomicAdd(&w.stats->heavy_next, 1u);
+    idx = __shfl(idx, 0, 64);
+    if (idx >= total) break;
+    const uint32_t t = w.deferred[idx / WALK_CHUNK] * WALK_CHUNK + idx % WALK_CHUNK;
+    if (t >= n) continue;
+    const uint32_t D = w.lv[t], tf = w.tfl[t], gb = off[t] + t;
+    if ((tf & TF_WILDCARD) && mode == MODE_TRIE) {
+      if (lane == 0) {
+        w.cnt[t] = 0;
+        w.off_tmp[t] = 0;
+        w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
+      }
+      continue;
+    }
+    const uint2 root = (tf & TF_WILDCARD) ? make_uint2(0, mk_meta(0, 0, 0, 0, 1))
+                                          : make_uint2(0, mk_meta(0, 0, root_fl, 0, 0));
+    unsigned long long base = 0;
+    uint32_t count = 0;
+    bool err = false, fits = true;
+    for (int pass = 0; pass < 2 && !err; ++pass) {
+      uint32_t sp = 1, k = 0;
+      if (lane == 0) stk[0] = root;
+      wave_sync();
+      while (sp) {
+        const uint32_t take = min(64u, sp), bi = sp - take;
+        const bool act = lane < take;
+        uint2 it = make_uint2(0, 0);
+        if (act) it = stk[bi + lane];
+        sp = bi;
+        wave_sync();
+        Expand x;
+        x.h0 = x.h1 = x.hc0 = x.hc1 = false;
+        if (act) {
+          const uint32_t level = it.y & 0x1FFFFu;
+          const uint32_t wd = level < D ? w.wid[gb + level] : WID_NONE;
+          expand(tab, mode, it, D, tf, wd, x);
+        }
+        const uint64_t b0 = __ballot(x.h0), b1 = __ballot(x.h1);
+        const uint32_t n0 = popc(b0);
+        if (pass == 1 && fits) {
+          if (x.h0) w.ids_tmp[base + k + mbcnt(b0)] = x.e0;
+          if (x.h1) w.ids_tmp[base + k + n0 + mbcnt(b1)] = x.e1;
+        }
+        k += n0 + popc(b1);
+        const uint64_t c0 = __ballot(x.hc0), c1 = __ballot(x.hc1);
+        const uint32_t m0 = popc(c0), nc = m0 + popc(c1);
+        if (sp + nc > (uint32_t)HEAVY_STACK) {
+          err = true;
+          break;
+        }
+        if (x.hc0) stk[sp + mbcnt(c0)] = x.c0;
+        if (x.hc1) stk[sp + m0 + mbcnt(c1)] = x.c1;
+        sp += nc;
+        if (pass == 0) visited += take;
+        wave_sync();
+      }
+      wave_sync();
+      if (pass == 0 && !err) {
+        count = k;
+        if (lane == 0 && count) base = atomicAdd(&w.stats->cursor, (unsigned long long)count);
+        base = __shfl(base, 0, 64);
+        fits = base + count <= w.ids_cap;
+        if (!fits && lane == 0) atomicOr(&w.stats->overflow, 1u);
+      }
+    }
+    if (lane == 0) {
+      if (err) {
+        atomicAdd(&w.stats->errors, 1u);
+        w.cnt[t] = 0;
+        w.off_tmp[t] = 0;
+        w.tfl[t] = (uint8_t)(tf | TF_HEAVY | TF_ERROR);
+      } else {
+        w.cnt[t] = count;
+        w.off_tmp[t] = base;
+        w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
+      }
+    }
+  }
+  if (lane == 0 && visited) atomicAdd(&w.stats->visited, (unsigned long long)visited);
+}
+
+// ------------------------------------------------------------------ scan ----
+// counts u32[n] -> row_ptr u64[n+1] (exclusive), three launches.
+__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t* __restrict__ cnt, uint32_t n,
+                                                     uint64_t* __restrict__ tile_sums) {
+  __shared__ uint64_t part[4];
+  const uint32_t i0 = blockIdx.x * SCAN_TILE + threadIdx.x * 8;
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (i0 + k < n) s += cnt[i0 + k];
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_down(s, d, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+__global__ __launch_bounds__(1024) void k_scan_top(uint64_t* __restrict__ tile_sums, uint32_t ntiles) {
+  __shared__ uint64_t wsum[16];
+  __shared__ uint64_t carry_s;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < ntiles; b0 += 1024) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint64_t v = i < ntiles ? tile_sums[i] : 0;
+    uint64_t x = v;
+    for (int d = 1; d < 64; d <<= 1) {
+      uint64_t y = __shfl_up(x, d, 64);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint64_t pre = carry_s;
+    for (uint32_t k = 0; k < wv; ++k) pre += wsum[k];
+    if (i < ntiles) tile_sums[i] = pre + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry_s = pre + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tile_sums[ntiles] = carry_s;
+}
+
+__global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__ cnt, uint32_t n,
+                                                    const uint64_t* __restrict__ tile_sums, uint32_t ntiles,
+                                                    uint64_t* __restrict__ row_ptr) {
+  __shared__ uint64_t wsum[4];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t i0 = blockIdx.x * SCAN_TILE + threadIdx.x * 8;
+  uint32_t v[8];
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    v[k] = (i0 + k < n) ? cnt[i0 + k] : 0u;
+    s += v[k];
+  }
+  uint64_t x = s;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  uint64_t pre = tile_sums[blockIdx.x];
+  for (uint32_t k = 0; k < wv; ++k) pre += wsum[k];
+  pre += x - s;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (i0 + k < n) row_ptr[i0 + k] = pre;
+    pre += v[k];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) row_ptr[n] = tile_sums[ntiles];
+}
+
+// chunk-ordered ids -> CSR rows (one lane per topic)
+__global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ off_tmp,
+                                                 const uint32_t* __restrict__ cnt,
+                                                 const uint32_t* __restrict__ ids_tmp, uint32_t n,
+                                                 const uint64_t* __restrict__ row_ptr,
+                                                 uint32_t* __restrict__ ids, uint64_t ids_cap,
+                                                 MatchStats* stats) {
+  if (stats->overflow) return;
+  if (row_ptr[n] > ids_cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, 2u);
+    return;
+  }
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const uint32_t c = cnt[t];
+    const uint64_t s = off_tmp[t], d = row_ptr[t];
+    for (uint32_t k = 0; k < c; ++k) ids[d + k] = ids_tmp[s + k];
+  }
+}
+
+// ------------------------------------------------------------- launchers ----
+int walk_grid_blocks(uint32_t n) {
+  const uint32_t chunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  uint32_t blocks = (chunks + WALK_WAVES - 1) / WALK_WAVES;
+  const uint32_t cap = 256 * 8;  // grid-stride beyond ~8 blocks per CU
+  if (blocks > cap) blocks = cap;
+  return blocks ? (int)blocks : 1;
+}
+
+size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
+
+static void scan_counts(const uint32_t* cnt, uint32_t n, uint64_t* tile_sums, uint64_t* row_ptr,
+                        hipStream_t s) {
+  const uint32_t ntiles = (uint32_t)scan_tiles(n);
+  if (ntiles) hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(256), 0, s, cnt, n, tile_sums);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, tile_sums, ntiles);
+  if (ntiles) hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(256), 0, s, cnt, n, tile_sums, ntiles, row_ptr);
+  else hipLaunchKernelGGL(k_scan_apply, dim3(1), dim3(256), 0, s, cnt, n, tile_sums, ntiles, row_ptr);
+}
+
+hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n,
+                        int mode, const MatchWork& w, const MatchOut& out, hipStream_t s,
+                        hipEvent_t* ev_walk) {
+  hipError_t e = hipMemsetAsync(w.stats, 0, sizeof(MatchStats), s);
+  if (e != hipSuccess) return e;
+  if (n == 0) {
+    return hipMemsetAsync(out.row_ptr, 0, sizeof(uint64_t), s);
+  }
+  hipLaunchKernelGGL(k_tokenise, dim3((n + TOK_BLOCK - 1) / TOK_BLOCK), dim3(TOK_BLOCK), 0, s, tab, blob,
+                     off, n, w.wid, w.lv, w.tfl);
+  if (ev_walk) hipEventRecord(ev_walk[0], s);
+  hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64 * WALK_WAVES), 0, s, tab, off, n, mode, w);
+  if (ev_walk) hipEventRecord(ev_walk[1], s);
+  hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
+  scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);
+  hipLaunchKernelGGL(k_compact, dim3(min((n + 255) / 256, 4096u)), dim3(256), 0, s, w.off_tmp, w.cnt,
+                     w.ids_tmp, n, out.row_ptr, out.ids, out.ids_cap, w.stats);
+  return hipGetLastError();
+}
+
+// --------------------------------------------------------------- fan-out ----
+// emqx_broker:dispatch/2 (emqx_broker.erl:283-308): every subscriber of every
+// matched filter, the {shard, Topic, I} bags flattened into the same list
+// (:297-308, emqx_broker_helper.erl:82-86), shared groups as (filter, group)
+// entries (emqx_broker.erl:246-247).  Flattened over match entries: count ->
+// scan -> fill, so a 2 000-subscriber filter costs one lane's loop, not a
+// whole topic's.
+__global__ __launch_bounds__(256) void k_fan_count(const uint32_t* __restrict__ mids, uint64_t nids,
+                                                   SubTable st, uint32_t* __restrict__ dc) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nids;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t f = mids[i];
+    dc[i] = f < st.n_fid_slots ? (uint32_t)(st.row[f + 1] - st.row[f]) : 0u;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fan_rows(const uint64_t* __restrict__ mrow, uint32_t n,
+                                                  const uint64_t* __restrict__ dpos, uint64_t* __restrict__ drow) {
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t <= n; t += gridDim.x * blockDim.x)
+    drow[t] = dpos[mrow[t]];
+}
+
+__global__ __launch_bounds__(256) void k_fan_fill(const uint32_t* __restrict__ mids, uint64_t nids, SubTable st,
+                                                  const uint32_t* __restrict__ dc, const uint64_t* __restrict__ dpos,
+                                                  uint32_t* __restrict__ dfid, uint32_t* __restrict__ dsub,
+                                                  uint64_t cap, unsigned int* overflow) {
+  if (dpos[nids] > cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *overflow = 1u;
+    return;
+  }
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nids;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t f = mids[i], c = dc[i];
+    if (!c) continue;
+    const uint64_t s0 = st.row[f], d = dpos[i];
+    for (uint32_t k = 0; k < c; ++k) {
+      dfid[d + k] = f;
+      dsub[d + k] = st.subs[s0 + k];
+    }
+  }
+}
+
+hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_t* mids, uint32_t n,
+                         uint64_t nids, uint64_t* drow, uint32_t* dfid, uint32_t* dsub, uint64_t cap,
+                         uint32_t* dc, uint64_t* dpos, uint64_t* tile_sums, unsigned int* overflow,
+                         hipStream_t s, hipEvent_t* ev) {
+  hipError_t e = hipMemsetAsync(overflow, 0, 4, s);
+  if (e != hipSuccess) return e;
+  if (ev) hipEventRecord(ev[0], s);
+  const uint32_t g = (uint32_t)std::min<uint64_t>((nids + 255) / 256 + 1, 8192);
+  if (nids) hipLaunchKernelGGL(k_fan_count, dim3(g), dim3(256), 0, s, mids, nids, st, dc);
+  scan_counts(dc, (uint32_t)nids, tile_sums, dpos, s);
+  hipLaunchKernelGGL(k_fan_rows, dim3(std::min<uint32_t>(n / 256 + 1, 8192)), dim3(256), 0, s, mrow, n, dpos, drow);
+  if (nids) hipLaunchKernelGGL(k_fan_fill, dim3(g), dim3(256), 0, s, mids, nids, st, dc, dpos, dfid, dsub, cap, overflow);
+  if (ev) hipEventRecord(ev[1], s);
+  return hipGetLastError();
+}
+
+}  // namespace egm

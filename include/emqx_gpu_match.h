@@ -1,0 +1,187 @@
+/*
+ * emqx_gpu_match.h — C-ABI of libemqx_gpu_match.so, the MI355X (gfx950)
+ * drop-in for EMQX's publish-time route lookup.
+ *
+ * Each entry point replaces a reference interface (EMQ X 5.0-alpha.3, paths
+ * relative to the reference root):
+ *
+ *   egm_table_build / egm_table_apply_delta / egm_table_commit
+ *       <- emqx_trie:insert/1, delete/1   apps/emqx/src/emqx_trie.erl:82-96
+ *          (driven by emqx_router:do_add_route/2, do_delete_route/2,
+ *           apps/emqx/src/emqx_router.erl:114-125,164-170,230-248)
+ *   egm_table_empty       <- emqx_trie:empty/0        emqx_trie.erl:117-118
+ *   egm_match_batch (EGM_MODE_TRIE)
+ *                         <- emqx_trie:match/1        emqx_trie.erl:99-114
+ *   egm_match_batch (EGM_MODE_ROUTES)
+ *                         <- emqx_router:match_routes/1's filter set
+ *                                                      emqx_router.erl:128-145
+ *   egm_fanout_batch      <- emqx_broker:dispatch/2 subscriber expansion
+ *                                                      emqx_broker.erl:283-324
+ *   egm_filter_bytes      <- the filter binaries match/1 returns (id -> bytes)
+ *
+ * Conventions: plain pointers and sizes only; every function returns 0 or a
+ * negative EGM_E* code and never throws; host buffers are borrowed for the
+ * duration of the call; results are library-allocated and released with
+ * egm_result_free().  One context = one HIP device; calls on a context are
+ * serialised internally (a dirty-scheduler NIF may call from any thread).
+ */
+#ifndef EMQX_GPU_MATCH_H
+#define EMQX_GPU_MATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EGM_OK 0
+#define EGM_E_INVAL (-1)     /* bad argument (mirrors the reference's function_clause) */
+#define EGM_E_NOMEM (-2)     /* host or device allocation failed */
+#define EGM_E_DEVICE (-3)    /* HIP runtime / kernel failure */
+#define EGM_E_OVERFLOW (-4)  /* a topic's frontier exceeded the heavy-path stack */
+#define EGM_E_STATE (-5)     /* call not valid in the current state */
+#define EGM_E_NOTFOUND (-6)  /* unknown filter id */
+
+/* Match semantics. */
+#define EGM_MODE_TRIE 0   /* emqx_trie:match/1 over the table's filters            */
+#define EGM_MODE_ROUTES 1 /* filters whose routes emqx_router:match_routes/1 returns */
+
+/* egm_result.flags[i] bits */
+#define EGM_TF_WILDCARD 1u /* topic has a '+' or '#' word (TRIE mode: no matches) */
+#define EGM_TF_DOLLAR 2u   /* first word starts with '$'                          */
+#define EGM_TF_HEAVY 4u    /* matched by the overflow (heavy) kernel              */
+#define EGM_TF_ERROR 8u    /* not matched: frontier exceeded the heavy stack      */
+
+typedef struct egm_ctx egm_ctx;
+
+typedef struct egm_config {
+  int32_t device;        /* HIP device ordinal                                        */
+  int32_t compact_mode;  /* broker.perf.trie_compaction (emqx_trie.erl:272-276);
+                            match sets do not depend on it — kept for API parity      */
+  uint32_t max_batch;    /* expected topics per call (pre-sizes workspaces; 0 = lazy) */
+  uint32_t linger_us;    /* host batcher linger hint (emqx_batch.erl:50-81)           */
+} egm_config;
+
+typedef struct egm_delta {
+  const uint8_t* blob;      /* filters back to back                                 */
+  const uint32_t* offsets;  /* [n+1] byte offsets into blob                         */
+  uint32_t n;
+  const uint32_t* ids;      /* optional [n] filter ids for inserts (NULL = assign)  */
+} egm_delta;
+
+typedef struct egm_result {
+  uint32_t n_topics;
+  uint64_t n_ids;
+  uint32_t* counts;    /* [n_topics]    matches per topic                           */
+  uint64_t* row_ptr;   /* [n_topics+1]  CSR row starts                              */
+  uint32_t* ids;       /* [n_ids]       filter ids (a set per row, no duplicates)   */
+  uint8_t* flags;      /* [n_topics]    EGM_TF_* bits                               */
+  uint64_t epoch;      /* table epoch the batch was matched against                 */
+  uint64_t visited;    /* NFA states expanded (instrumentation)                     */
+  uint32_t n_heavy;    /* topics routed through the heavy kernel                    */
+  uint32_t n_error;    /* topics flagged EGM_TF_ERROR                               */
+} egm_result;
+
+typedef struct egm_delivery {
+  uint32_t n_topics;
+  uint64_t n_deliveries;
+  uint64_t* row_ptr;   /* [n_topics+1]                                              */
+  uint32_t* fid;       /* [n_deliveries] matched filter id                          */
+  uint32_t* sub;       /* [n_deliveries] subscriber id, or group id | 0x80000000    */
+} egm_delivery;
+
+/* ---- context ---- */
+int egm_open(const egm_config* cfg, egm_ctx** out);
+void egm_close(egm_ctx* ctx);
+const char* egm_last_error(egm_ctx* ctx);
+const char* egm_version(void);
+
+/* ---- filter table (emqx_trie content) ---- */
+/* Replace the whole table with n filters; filter_ids optional (NULL = 0..n-1
+   in order).  Duplicate filters keep their first id (insert/1 is idempotent).
+   Publishes a new epoch. */
+int egm_table_build(egm_ctx* ctx, const uint8_t* filters_blob, const uint32_t* offsets, uint32_t n,
+                    const uint32_t* filter_ids);
+/* Stage inserts then deletes (either may be NULL); visible after commit. */
+int egm_table_apply_delta(egm_ctx* ctx, const egm_delta* ins, const egm_delta* del);
+/* Publish the staged table as a new epoch (readers in flight keep the old). */
+int egm_table_commit(egm_ctx* ctx, uint64_t* epoch);
+/* 1 if the committed table holds no filter, 0 otherwise. */
+int egm_table_empty(egm_ctx* ctx);
+/* Counts of the committed table: filters, trie nodes, literal edges, words. */
+int egm_table_stats(egm_ctx* ctx, uint64_t* n_filters, uint64_t* n_nodes, uint64_t* n_edges,
+                    uint64_t* n_words, uint64_t* device_bytes);
+/* Filter id of given bytes in the staged table, or EGM_E_NOTFOUND. */
+int egm_filter_id(egm_ctx* ctx, const uint8_t* filter, uint32_t len, uint32_t* id);
+/* Bytes of a filter id (pointer valid until the next table mutation). */
+int egm_filter_bytes(egm_ctx* ctx, uint32_t id, const uint8_t** bytes, uint32_t* len);
+
+/* ---- matching ---- */
+/* Host buffers in, CSR result out (allocated; free with egm_result_free). */
+int egm_match_batch(egm_ctx* ctx, const uint8_t* topics_blob, const uint32_t* topic_offsets,
+                    uint32_t n_topics, int mode, egm_result** out);
+
+/* Device-resident variant: d_blob (4-byte aligned, blob_bytes >= d_offsets[n])
+   and d_offsets are device pointers (d_offsets[0] == 0); results stay in device buffers owned by the caller
+   (d_row_ptr[n+1], d_ids[ids_cap], d_flags[n] may be NULL).  Asynchronous on
+   `hip_stream` (NULL = the context's stream).  After the stream completes,
+   d_row_ptr[n] holds the number of ids; egm_last_stats() reports overflow. */
+int egm_match_device(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_offsets,
+                     uint32_t n_topics, int mode, void* hip_stream, uint64_t* d_row_ptr, uint32_t* d_ids,
+                     uint64_t ids_cap, uint8_t* d_flags);
+/* Synchronises the last device batch and reports its counters.  overflow != 0
+   means ids_cap was too small (rerun with a larger buffer). */
+int egm_last_stats(egm_ctx* ctx, uint64_t* n_ids, uint64_t* visited, uint32_t* n_deferred_chunks,
+                   uint32_t* overflow, uint32_t* n_error);
+/* Enable per-kernel timing with HIP events on the launch stream (0/1) and read
+   the accumulated walk-kernel time (ms) and launch count. */
+int egm_set_timing(egm_ctx* ctx, int enable);
+int egm_get_timing(egm_ctx* ctx, double* walk_ms, uint64_t* walk_launches, double* fanout_ms,
+                   uint64_t* fanout_launches);
+
+/* ---- subscriber fan-out (emqx_broker:dispatch/2) ---- */
+/* filter id -> subscriber ids CSR (sub | 0x80000000 marks a shared group id). */
+int egm_subs_build(egm_ctx* ctx, const uint64_t* row_ptr, uint32_t n_fid_slots, const uint32_t* subs);
+int egm_fanout_batch(egm_ctx* ctx, const egm_result* matched, egm_delivery** out);
+/* Device variant over a device CSR match result. */
+int egm_fanout_device(egm_ctx* ctx, const uint64_t* d_match_row, const uint32_t* d_match_ids,
+                      uint32_t n_topics, void* hip_stream, uint64_t* d_deliv_row, uint32_t* d_fid,
+                      uint32_t* d_sub, uint64_t deliv_cap);
+
+void egm_result_free(void* result);
+
+/* ---- host-only table image (diagnostics; needs no device) ----
+   Builds the same HBM image egm_table_commit uploads, so the layout can be
+   inspected and tested on a host without a GPU. */
+typedef struct egm_image egm_image;
+typedef struct egm_image_view {
+  const void* nodes;      uint64_t n_nodes;      /* 16 B {plus_child, hash_fid, term_fid, meta} */
+  const uint32_t* hash_child;
+  const void* edges;      uint64_t n_edge_slots; /* 16 B {parent, word, child, child_flags}, 4 per bucket */
+  uint32_t edge_mask;                            /* buckets - 1 */
+  const void* dict;       uint64_t n_dict_slots; /* 32 B {hash64, word, len, inline[16]} */
+  uint32_t dict_mask;
+  const uint8_t* dict_blob; const uint64_t* dict_off; uint64_t n_words;
+  uint64_t n_filters; uint64_t n_live_nodes; uint64_t n_edges;
+} egm_image_view;
+egm_image* egm_image_new(void);
+void egm_image_free(egm_image* im);
+/* 0 inserted, 1 already present, <0 error (id NONE = 0xFFFFFFFF assigns) */
+int egm_image_insert(egm_image* im, const uint8_t* filter, uint32_t len, uint32_t id);
+/* 0 removed, 1 absent */
+int egm_image_remove(egm_image* im, const uint8_t* filter, uint32_t len);
+void egm_image_relayout(egm_image* im);
+int egm_image_get_view(egm_image* im, egm_image_view* out);
+/* Filter -> shard for multi-GPU filter sharding: out[i] =
+   word_hash(filter i) mod n_shards.  Host-only. */
+int egm_shard_assign(const uint8_t* blob, const uint32_t* offsets, uint32_t n, uint32_t n_shards,
+                     uint32_t* out);
+/* the 64-bit word hash and the edge bucket function the kernels use */
+uint64_t egm_word_hash(const uint8_t* p, uint32_t len);
+uint32_t egm_edge_bucket(uint32_t parent, uint32_t word, uint32_t mask);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EMQX_GPU_MATCH_H */

@@ -1,0 +1,260 @@
+"""GPU parity: the HIP path through the C-ABI vs the pinned oracle.
+
+Bit-exact set equality per topic (ids sorted within each row — the reference's
+own suites compare with lists:sort).  Small cases against the Python
+restatement, config-sized cases against the C++ restatement, full sizes through
+size-independent properties (shard union, determinism, sampled oracle rows).
+"""
+import random
+
+import numpy as np
+import pytest
+
+from emqx_amd import _lib as L
+from emqx_amd import synth
+from emqx_amd.engine import GpuMatcher, pack_strings
+from oracle import trie_ref as R
+from oracle.cpp import OracleTrie, canonical
+from tests.kat import b, load
+from tests.test_capi_cpu import rand_filter, rand_topic
+
+pytestmark = pytest.mark.gpu
+
+MODES = [L.EGM_MODE_TRIE, L.EGM_MODE_ROUTES]
+
+
+@pytest.fixture(scope="module")
+def gm():
+    m = GpuMatcher(0)
+    yield m
+    m.close()
+
+
+def sets_of(res, names=None):
+    out = []
+    for i in range(len(res.row_ptr) - 1):
+        r = res.row(i)
+        assert len(r) == len(set(r.tolist())), "duplicate ids in a row"
+        out.append(sorted(names[int(x)] for x in r) if names is not None else sorted(r.tolist()))
+    return out
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_reference_kats(gm, mode):
+    K = load()
+    for case in K["trie_cases"]:
+        gm.build_strings([])
+        live = {}
+        nxt = 0
+        for op in case["ops"]:
+            if op[0] == "insert":
+                f = b(op[1])
+                if f not in live.values():
+                    gm.apply(inserts=[f], insert_ids=[nxt])
+                    live[nxt] = f
+                    nxt += 1
+                gm.commit()
+            elif op[0] == "delete":
+                f = b(op[1])
+                gm.apply(deletes=[f])
+                for k in [k for k, v in live.items() if v == f]:
+                    del live[k]
+                gm.commit()
+            elif op[0] == "assert_empty":
+                assert gm.empty() is op[1]
+        if not case["queries"]:
+            continue
+        res = gm.match_strings([b(q) for q, _ in case["queries"]], mode)
+        got = sets_of(res, live)
+        for i, (q, exp) in enumerate(case["queries"]):
+            want = sorted(b(x) for x in exp) if mode == L.EGM_MODE_TRIE else sorted(
+                R.routes_semantics(b(q), live.values()))
+            assert got[i] == want, (case["name"], q)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_random_small_with_deltas(gm, seed):
+    rng = random.Random(seed)
+    filters = list(dict.fromkeys([rand_filter(rng) for _ in range(300)] + [b"$x", b"a/b", b"$", b""]))
+    gm.build_strings(filters)
+    live = dict(enumerate(filters))
+    topics = [rand_topic(rng) for _ in range(2000)] + [b"", b"$", b"/", b"a/b", b"$x", b"+", b"#", b"a/+/#"]
+    for rnd in range(3):
+        for mode in MODES:
+            res = gm.match_strings(topics, mode)
+            got = sets_of(res, live)
+            for i, t in enumerate(topics):
+                want = R.trie_semantics(t, live.values()) if mode == 0 else R.routes_semantics(t, live.values())
+                assert got[i] == sorted(want), (rnd, mode, t)
+            wc = np.array([R.wildcard(t) for t in topics])
+            assert np.array_equal((res.flags & L.EGM_TF_WILDCARD) != 0, wc)
+        # mutate: delete a slice, insert new filters with fresh ids
+        dels = [live[k] for k in list(live)[rnd::4]]
+        news = list(dict.fromkeys(f for f in (rand_filter(rng) for _ in range(60)) if f not in live.values()))
+        base = 10_000 * (rnd + 1)
+        gm.apply(inserts=news, deletes=dels, insert_ids=list(range(base, base + len(news))))
+        for k in [k for k, v in live.items() if v in set(dels)]:
+            del live[k]
+        for j, f in enumerate(news):
+            if f not in set(dels):
+                live[base + j] = f
+        gm.commit()
+
+
+def test_deep_and_long(gm):
+    T = b"a/b/c/d/e/f/g/h/i/j/k/l/m/n/o/p/q/r/s/t/u/v/w/x/y/z"
+    deep = b"/".join(b"l%d" % i for i in range(300))
+    filters = [b"#", T + b"/#", T + b"/+", b"/".join([b"+"] * 26) + b"/#",
+               b"a/+/c/+/e/+/g/+/i/+/k/+/m/+/o/+/q/+/s/+/u/+/w/+/y/+/#", deep, deep + b"/#",
+               b"/".join([b"+"] * 299) + b"/+", b"x" * 5000 + b"/+"]
+    gm.build_strings(filters)
+    topics = [T, T + b"/1", deep, deep + b"/more", b"x" * 5000 + b"/y", b"/".join([b"q"] * 300)]
+    for mode in MODES:
+        res = gm.match_strings(topics, mode)
+        got = sets_of(res, dict(enumerate(filters)))
+        for i, t in enumerate(topics):
+            want = R.trie_semantics(t, filters) if mode == 0 else R.routes_semantics(t, filters)
+            assert got[i] == sorted(want), (mode, t[:40])
+
+
+def test_heavy_path_wide_frontier(gm):
+    # every filter of depth 11 over {'+', 'k<l>'} : a matching topic hits 2^11
+    # filters, far above the per-wave LDS stage -> chunk deferred to k_heavy
+    D = 11
+    filters = []
+    for m in range(1 << D):
+        filters.append(b"/".join(b"+" if (m >> l) & 1 else b"k%d" % l for l in range(D)))
+    filters += [b"#", b"k0/#"]
+    gm.build_strings(filters)
+    topics = [b"/".join(b"k%d" % l for l in range(D)), b"k0/zz", b"/".join(b"k%d" % l for l in range(D - 1)) +
+              b"/no"] + [b"p/q/r"] * 300
+    res = gm.match_strings(topics, L.EGM_MODE_TRIE)
+    assert res.n_heavy > 0 and res.n_error == 0
+    got = sets_of(res)
+    assert len(got[0]) == (1 << D) - 1 + 1 + 1   # all but the all-literal filter, + '#', 'k0/#'
+    names = dict(enumerate(filters))
+    for i, t in enumerate(topics[:3]):
+        assert [names[x] for x in got[i]] == sorted(R.trie_semantics(t, filters))
+    rr = gm.match_strings(topics, L.EGM_MODE_ROUTES)
+    assert sets_of(rr)[0] == sorted(got[0] + [0])   # + the exact filter k0/../k10
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_config_c0_vs_cpp_oracle(gm, mode):
+    f, t = synth.config("c0")
+    gm.build(f.blob, f.off)
+    res = gm.match(t.blob, t.off, mode)
+    o = OracleTrie(True, mode)
+    o.add(f.blob, f.off)
+    row, ids = o.match(t.blob, t.off, threads=8)
+    assert np.array_equal(res.row_ptr, row)
+    assert np.array_equal(canonical(res.row_ptr, res.ids), canonical(row, ids))
+    assert res.visited > 0
+
+
+def test_golden_fixture(gm):
+    import gzip
+    import json
+    import os
+    p = os.path.join(os.path.dirname(__file__), "golden", "c0_small.json.gz")
+    with gzip.open(p, "rt") as fh:
+        g = json.load(fh)
+    filters = [x.encode() for x in g["filters"]]
+    topics = [x.encode() for x in g["topics"]]
+    gm.build_strings(filters)
+    for mode, key in ((L.EGM_MODE_TRIE, "trie"), (L.EGM_MODE_ROUTES, "routes")):
+        res = gm.match_strings(topics, mode)
+        got = sets_of(res)
+        assert got == [sorted(x) for x in g[key]], key
+
+
+def test_device_api_matches_host_api(gm):
+    import torch
+    f, t = synth.config("c0", n_topics=50_000)
+    gm.build(f.blob, f.off)
+    host = gm.match(t.blob, t.off, L.EGM_MODE_TRIE)
+    dev = torch.device("cuda:0")
+    d_blob = torch.from_numpy(t.blob).to(dev)
+    d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+    n = t.n
+    cap = len(host.ids) + 1024
+    d_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
+    d_fl = torch.zeros(n, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_TRIE, s, d_row.data_ptr(),
+                    d_ids.data_ptr(), cap, d_fl.data_ptr())
+    st = gm.last_stats()
+    assert st["overflow"] == 0 and st["n_ids"] == len(host.ids)
+    row = d_row.cpu().numpy().view(np.uint64)
+    ids = d_ids.cpu().numpy().view(np.uint32)[: len(host.ids)]
+    assert np.array_equal(row, host.row_ptr)
+    assert np.array_equal(canonical(row, ids), canonical(host.row_ptr, host.ids))
+    assert np.array_equal(d_fl.cpu().numpy(), host.flags)
+    # too-small capacity reports overflow instead of writing past the buffer
+    gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_TRIE, s, d_row.data_ptr(),
+                    d_ids.data_ptr(), 16, 0)
+    assert gm.last_stats()["overflow"] != 0
+
+
+def test_logical_shards_union(gm):
+    """Filter sharding: union over shards == whole table."""
+    f, t = synth.config("c0", n_topics=30_000)
+    fl = f.to_list()
+    G = 3
+    from emqx_amd.dist import shard_of
+    sh = shard_of(f, G)
+    parts = []
+    for g in range(G):
+        idx = np.nonzero(sh == g)[0]
+        m = GpuMatcher(0)
+        blob, off = pack_strings([fl[i] for i in idx])
+        m.build(blob, off, idx.astype(np.uint32))
+        parts.append(m.match(t.blob, t.off, L.EGM_MODE_TRIE))
+        m.close()
+    gm.build(f.blob, f.off)
+    whole = gm.match(t.blob, t.off, L.EGM_MODE_TRIE)
+    from emqx_amd.dist import merge_shard_results
+    row, ids = merge_shard_results([(p.row_ptr, p.ids) for p in parts])
+    assert np.array_equal(row, whole.row_ptr)
+    assert np.array_equal(canonical(row, ids), canonical(whole.row_ptr, whole.ids))
+
+
+def test_fanout_vs_oracle(gm):
+    f, t = synth.config("c0", n_topics=20_000)
+    gm.build(f.blob, f.off)
+    res = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    row, subs = synth.subscribers(f.n, p_big=0.002, n_big=2000, p_share=0.1)
+    gm.subs_build(row, subs)
+    drow, dfid, dsub = gm.fanout(res)
+    # oracle: per topic, the multiset of (filter, sub) over matched filters
+    for i in range(0, t.n, 97):
+        want = []
+        for fid in res.row(i).tolist():
+            want += [(fid, int(s)) for s in subs[row[fid]:row[fid + 1]]]
+        got = list(zip(dfid[drow[i]:drow[i + 1]].tolist(), dsub[drow[i]:drow[i + 1]].tolist()))
+        assert sorted(got) == sorted(want)
+    assert drow[-1] == sum(int(row[x + 1] - row[x]) for x in res.ids.tolist())
+
+
+@pytest.mark.slow
+def test_full_size_c1_properties(gm):
+    """C1 at full size: 1M filters x 10M topics.  Sampled rows vs the C++
+    oracle, row totals vs oracle count, determinism across runs."""
+    f, t = synth.config("c1")
+    gm.build(f.blob, f.off)
+    a = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    b2 = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    assert np.array_equal(a.row_ptr, b2.row_ptr)
+    assert np.array_equal(canonical(a.row_ptr, a.ids), canonical(b2.row_ptr, b2.ids))
+    o = OracleTrie(True, 1)
+    o.add(f.blob, f.off)
+    rng = np.random.default_rng(5)
+    idx = np.sort(rng.choice(t.n, 200_000, replace=False))
+    sub = t.subset(idx)
+    row, ids = o.match(sub.blob, sub.off, threads=16)
+    got_row = np.zeros(len(idx) + 1, np.uint64)
+    got_row[1:] = np.cumsum(np.diff(a.row_ptr)[idx])
+    assert np.array_equal(got_row, row)
+    got_ids = np.concatenate([a.row(int(i)) for i in idx])
+    assert np.array_equal(canonical(got_row, got_ids), canonical(row, ids))

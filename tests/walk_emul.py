@@ -1,0 +1,103 @@
+"""Test-side emulation of the kernels' NFA walk over a host-built table image.
+
+Used only to check, on a machine without a GPU, that the HBM image produced by
+the host table builder (egm_table.cpp, exposed through TableImage) encodes the
+filter set: tokenise -> byte-exact dictionary probe -> edge bucket probe ->
+frontier expansion, exactly as egm_kernels.hip does it.  Not a product path.
+"""
+import numpy as np
+
+NONE = 0xFFFFFFFF
+WID_NONE, WID_PLUS, WID_HASH, WID_MAX = 0xFFFFFFFF, 0xFFFFFFFD, 0xFFFFFFFC, 0xFFFFFFF0
+F_LIT, F_PLUS, F_HASH, F_TERM = 1, 2, 4, 8
+
+
+class Emul:
+    def __init__(self, img, arrays):
+        self.img = img
+        self.a = arrays
+        self.blob = arrays["dict_blob"].tobytes()
+
+    def word_id(self, w: bytes) -> int:
+        a = self.a
+        h = self.img.word_hash(w)
+        i = h & a["dict_mask"]
+        while True:
+            s = a["dict"][i]
+            wid = int(s[2])
+            if wid == NONE:
+                return WID_NONE
+            sh = int(s[0]) | (int(s[1]) << 32)
+            if sh == h and int(s[3]) == len(w):
+                o0, o1 = int(a["dict_off"][wid]), int(a["dict_off"][wid + 1])
+                if self.blob[o0:o1] == w:
+                    return wid
+            i = (i + 1) & a["dict_mask"]
+
+    def edge(self, node, w):
+        a = self.a
+        b = self.img.edge_bucket(node, w, a["edge_mask"])
+        while True:
+            for k in range(4):
+                s = a["edges"][b * 4 + k]
+                if int(s[0]) == node and int(s[1]) == w:
+                    return int(s[2]), int(s[3])
+                if int(s[0]) == NONE:
+                    return NONE, 0
+            b = (b + 1) & a["edge_mask"]
+
+    def match(self, topic: bytes, mode: int = 0):
+        a = self.a
+        ws = topic.split(b"/")
+        wids = []
+        wild = False
+        for w in ws:
+            if w == b"+":
+                wids.append(WID_PLUS); wild = True
+            elif w == b"#":
+                wids.append(WID_HASH); wild = True
+            else:
+                wids.append(self.word_id(w))
+        dollar = topic[:1] == b"$"
+        D = len(ws)
+        out = []
+        nodes = a["nodes"]
+        if wild:
+            if mode == 0:
+                return out
+            node = 0
+            for l in range(D):
+                w = wids[l]
+                if w == WID_PLUS:
+                    node = int(nodes[node][0])
+                elif w == WID_HASH:
+                    node = int(a["hash_child"][node])
+                elif w < WID_MAX:
+                    node = self.edge(node, w)[0]
+                else:
+                    node = NONE
+                if node == NONE:
+                    return out
+            if int(nodes[node][2]) != NONE:
+                out.append(int(nodes[node][2]))
+            return out
+        root_fl = (int(nodes[0][3]) >> 4) & 0xF
+        stack = [(0, 0, root_fl, 0)]
+        while stack:
+            node, level, fl, wc = stack.pop()
+            rec = nodes[node]
+            atend = level == D
+            rootd = level == 0 and dollar
+            if (fl & F_HASH) and not rootd:
+                out.append(int(rec[1]))
+            if atend and (fl & F_TERM) and (mode == 1 or wc or (D == 1 and dollar)):
+                out.append(int(rec[2]))
+            if atend:
+                continue
+            if (fl & F_LIT) and wids[level] < WID_MAX:
+                c, cf = self.edge(node, wids[level])
+                if c != NONE:
+                    stack.append((c, level + 1, cf, wc))
+            if (fl & F_PLUS) and not rootd:
+                stack.append((int(rec[0]), level + 1, int(rec[3]) & 0xF, 1))
+        return out
