@@ -147,7 +147,10 @@ def main():
     tstats = gm.stats()
     log(f"[rank {rank}] table built in {time.time() - t0:.1f}s: {tstats}")
 
-    stream = torch.cuda.current_stream(dev)
+    # one explicit stream for every kernel and copy of the step (the library
+    # and torch share one HIP runtime: emqx_amd._lib loads torch first)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     n = t.n
     nbytes = int(t.off[-1])

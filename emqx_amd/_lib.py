@@ -81,6 +81,7 @@ SIGNATURES = {
     "egm_match_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, _P, _P, C.c_uint64, _P]),
     "egm_last_stats": (C.c_int, [_P, _u64p, _u64p, _u32p, _u32p, _u32p]),
     "egm_set_timing": (C.c_int, [_P, C.c_int]),
+    "egm_set_debug": (C.c_int, [_P, C.c_uint32]),
     "egm_get_timing": (C.c_int, [_P, C.POINTER(C.c_double), _u64p, C.POINTER(C.c_double), _u64p]),
     "egm_subs_build": (C.c_int, [_P, _P, C.c_uint32, _P]),
     "egm_fanout_batch": (C.c_int, [_P, C.POINTER(egm_result), C.POINTER(C.POINTER(egm_delivery))]),
@@ -108,6 +109,16 @@ def load() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built — run `python -m emqx_amd.build` "
                           "(the HIP path has no CPU fallback)")
+    # PyTorch-ROCm bundles its own HIP/HSA runtime (torch/lib/libamdhip64.so,
+    # SONAME libamdhip64.so.7).  Loading torch first lets this library's
+    # NEEDED libamdhip64.so.7 bind to that runtime, so device pointers and
+    # streams are shared with torch in one runtime.  Loaded the other way
+    # round, torch would map a second HIP/HSA runtime into the process.
+    # Standalone users (the Erlang NIF) resolve /opt/rocm/lib via RUNPATH.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

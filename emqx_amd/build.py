@@ -66,7 +66,7 @@ def build_lib(verbose=False, force=False) -> str:
             _run(["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__",
                   f"-I{ROCM}/include", "-c", src, "-o", o], verbose)
         objs.append(o)
-    if force or _stale(LIB, objs):
+    if force or _stale(LIB, objs + [os.path.abspath(__file__)]):
         _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs, verbose)
     return LIB
 

@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -78,9 +79,11 @@ struct egm_ctx {
   std::string err;
 
   // per-batch workspace
-  DevBuf wid, lv, tfl, off_tmp, cnt, ids_tmp, deferred, tile_sums, stats;
+  DevBuf wid, lv, tfl, off_tmp, cnt, ids_tmp, pieces, deferred, tile_sums, stats;
+  uint64_t pieces_cap = 0;
   DevBuf in_blob, in_off, out_row, out_ids;
   uint32_t heavy_waves = 256;
+  uint32_t debug = 0;
   MatchStats last{};
   bool last_pending = false;
   hipStream_t last_stream = nullptr;
@@ -186,6 +189,11 @@ static int ensure_work(egm_ctx* c, uint32_t n, uint64_t blob_bytes, uint64_t ids
   if ((e = c->off_tmp.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "off_tmp");
   if ((e = c->cnt.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "cnt");
   if ((e = c->ids_tmp.ensure((ids_cap + 1) * 4)) != hipSuccess) return c->hip_fail(e, "ids_tmp");
+  // a piece holds >= 1 id; typical batches use ~1.2 pieces per topic
+  uint64_t pcap = std::max<uint64_t>(nn * 2 + 4096, ids_cap / 4);
+  if (pcap > ids_cap + nn) pcap = ids_cap + nn;
+  if ((e = c->pieces.ensure(pcap * 16)) != hipSuccess) return c->hip_fail(e, "pieces");
+  c->pieces_cap = c->pieces.cap / 16;
   if ((e = c->deferred.ensure((n / WALK_CHUNK + 2) * 4)) != hipSuccess) return c->hip_fail(e, "deferred");
   if ((e = c->tile_sums.ensure((scan_tiles(n) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "tile_sums");
   if ((e = c->stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "stats");
@@ -201,12 +209,15 @@ static MatchWork work_view(egm_ctx* c, uint64_t ids_cap) {
   w.cnt = c->cnt.as<uint32_t>();
   w.ids_tmp = c->ids_tmp.as<uint32_t>();
   w.ids_cap = ids_cap;
+  w.pieces = c->pieces.as<uint4>();
+  w.pieces_cap = c->pieces_cap;
   w.deferred = c->deferred.as<uint32_t>();
   w.heavy_stack = nullptr;
   w.heavy_waves = c->heavy_waves;
   w.heavy_stack_cap = 0;
   w.tile_sums = c->tile_sums.as<uint64_t>();
   w.stats = c->stats.as<MatchStats>();
+  w.debug = c->debug;
   return w;
 }
 
@@ -396,6 +407,13 @@ int egm_last_stats(egm_ctx* c, uint64_t* n_ids, uint64_t* visited, uint32_t* n_d
   if (n_def) *n_def = c->last.n_deferred;
   if (overflow) *overflow = c->last.overflow;
   if (n_error) *n_error = c->last.errors;
+  return EGM_OK;
+}
+
+int egm_set_debug(egm_ctx* c, uint32_t flags) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  c->debug = flags;
   return EGM_OK;
 }
 

@@ -22,12 +22,17 @@ struct DevTable {                 // one epoch of the filter graph in HBM
 struct MatchStats {               // device-side counters, zeroed per batch
   unsigned long long cursor;      // ids reserved in ids_tmp
   unsigned long long visited;     // NFA states expanded (light + heavy)
+  unsigned long long pieces;      // pieces reserved
   unsigned int n_deferred;        // chunks handed to the heavy kernel
   unsigned int heavy_next;        // heavy work counter
-  unsigned int overflow;          // ids_tmp capacity exceeded
+  unsigned int overflow;          // ids_tmp / pieces capacity exceeded
   unsigned int errors;            // topics the heavy kernel could not finish
-  unsigned int pad[2];
 };
+
+// A piece is one flush's run of a topic's ids in ids_tmp:
+// {topic, count | HEAVY_PIECE, offset lo, offset hi}.  CSR rows are assembled
+// from pieces; light-walk pieces of a topic later re-run by k_heavy are ignored.
+constexpr uint32_t HEAVY_PIECE = 0x80000000u;
 
 struct MatchWork {                // per-batch device workspace
   uint32_t* wid;                  // [blob_bytes + n] word ids, topic t at off[t] + t
@@ -37,13 +42,18 @@ struct MatchWork {                // per-batch device workspace
   uint32_t* cnt;                  // [n] number of ids of topic t
   uint32_t* ids_tmp;              // [ids_cap] chunk-ordered ids
   uint64_t ids_cap;
+  uint4* pieces;                  // [pieces_cap]
+  uint64_t pieces_cap;
   uint32_t* deferred;             // [n / CHUNK + 1] chunk ids for the heavy kernel
   uint2* heavy_stack;             // [heavy_waves * heavy_stack_cap]
   uint32_t heavy_waves;
   uint32_t heavy_stack_cap;
   uint64_t* tile_sums;            // scan scratch
   MatchStats* stats;
+  uint32_t debug;                 // DEBUG_* bits
 };
+
+constexpr uint32_t DEBUG_FORCE_HEAVY = 1u;   // every chunk goes to k_heavy (test coverage)
 
 struct MatchOut {                 // CSR result (device)
   uint64_t* row_ptr;              // [n + 1]

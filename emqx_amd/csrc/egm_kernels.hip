@@ -250,9 +250,60 @@ struct alignas(16) WaveLds {
   uint32_t words[WALK_WORDS];
   uint32_t tbase[WALK_CHUNK];   // word base: LDS index (staged) or wid index
   uint32_t tinfo[WALK_CHUNK];   // levels | flags << 24
-  uint32_t cnt[WALK_CHUNK];
+  uint32_t cnt[WALK_CHUNK];     // ids per topic, whole chunk
+  uint32_t fcnt[WALK_CHUNK];    // ids per topic in the current stage
   uint8_t stage_t[WALK_STAGE];
 };
+
+__device__ __forceinline__ uint4 mk_piece(uint32_t t, uint32_t count, unsigned long long off) {
+  return make_uint4(t, count, (uint32_t)off, (uint32_t)(off >> 32));
+}
+
+// Write the stage out: one atomic reservation of ids and of pieces, per-topic
+// runs by counting sort in LDS, one piece per topic present.
+__device__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane, const MatchWork& w) {
+  constexpr int PER = WALK_CHUNK / 64;
+  uint32_t fl[PER];
+  uint32_t s = 0, np = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    fl[k] = L.fcnt[lane * PER + k];   // consecutive topics per lane
+    s += fl[k];
+    np += fl[k] ? 1u : 0u;
+  }
+  uint32_t tot, ptot;
+  uint32_t ex = wave_excl_scan(s, lane, &tot);
+  uint32_t pex = wave_excl_scan(np, lane, &ptot);
+  unsigned long long base = 0, pbase = 0;
+  if (lane == 0) {
+    base = atomicAdd(&w.stats->cursor, (unsigned long long)tot);
+    pbase = atomicAdd(&w.stats->pieces, (unsigned long long)ptot);
+  }
+  base = __shfl(base, 0, 64);
+  pbase = __shfl(pbase, 0, 64);
+  const bool ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
+  if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t j = lane * PER + k;
+    if (fl[k] && ok) w.pieces[pbase + pex++] = mk_piece(t0 + j, fl[k], base + ex);
+    L.fcnt[j] = ex;   // becomes the scatter cursor
+    L.cnt[j] += fl[k];
+    ex += fl[k];
+  }
+  wave_sync();
+  if (ok) {
+    for (uint32_t i = lane; i < nstage; i += 64) {
+      const uint32_t tt = L.stage_t[i];
+      const uint32_t p = atomicAdd(&L.fcnt[tt], 1u);
+      w.ids_tmp[base + p] = L.stage_fid[i];
+    }
+  }
+  wave_sync();
+#pragma unroll
+  for (int k = 0; k < PER; ++k) L.fcnt[lane * PER + k] = 0;
+  wave_sync();
+}
 
 __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const uint32_t* __restrict__ off,
                                                           uint32_t n, int mode, MatchWork w) {
@@ -283,6 +334,7 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
       dsum += D;
       L.tinfo[j] = D | (f << 24);
       L.cnt[j] = 0;
+      L.fcnt[j] = 0;
     }
     uint32_t wtotal;
     uint32_t wb = wave_excl_scan(dsum, lane, &wtotal);
@@ -313,8 +365,8 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
     wave_sync();
 
     uint32_t next = 0, sp = 0, nstage = 0;
-    bool ovf = false;
-    for (;;) {
+    bool ovf = (w.debug & DEBUG_FORCE_HEAVY) != 0;
+    for (; !ovf;) {
       if (sp < 64 && next < nt) {  // refill with new roots
         const uint32_t k = min(64u - sp, nt - next);
         bool has = false;
@@ -360,27 +412,7 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
         if (level < D) wd = staged ? L.words[L.tbase[t] + level] : w.wid[L.tbase[t] + level];
         expand(tab, mode, it, D, tf, wd, x);
       }
-      // emits -> stage (matches of one chunk, tagged with the topic)
-      const uint64_t b0 = __ballot(x.h0), b1 = __ballot(x.h1);
-      const uint32_t n0 = popc(b0), ne = n0 + popc(b1);
-      if (nstage + ne > (uint32_t)WALK_STAGE) {
-        ovf = true;
-        break;
-      }
-      if (x.h0) {
-        const uint32_t p = nstage + mbcnt(b0);
-        L.stage_fid[p] = x.e0;
-        L.stage_t[p] = (uint8_t)t;
-        atomicAdd(&L.cnt[t], 1u);
-      }
-      if (x.h1) {
-        const uint32_t p = nstage + n0 + mbcnt(b1);
-        L.stage_fid[p] = x.e1;
-        L.stage_t[p] = (uint8_t)t;
-        atomicAdd(&L.cnt[t], 1u);
-      }
-      nstage += ne;
-      // children -> stack
+      // children -> stack (checked first: an overflow abandons the chunk)
       const uint64_t c0 = __ballot(x.hc0), c1 = __ballot(x.hc1);
       const uint32_t m0 = popc(c0), nc = m0 + popc(c1);
       if (sp + nc > (uint32_t)WALK_STACK) {
@@ -390,59 +422,43 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
       if (x.hc0) L.stack[sp + mbcnt(c0)] = x.c0;
       if (x.hc1) L.stack[sp + m0 + mbcnt(c1)] = x.c1;
       sp += nc;
+      // emits -> stage, flushed to global pieces whenever it would overflow
+      const uint64_t b0 = __ballot(x.h0), b1 = __ballot(x.h1);
+      const uint32_t n0 = popc(b0), ne = n0 + popc(b1);
+      if (nstage + ne > (uint32_t)WALK_STAGE) {
+        wave_sync();
+        flush_stage(L, nstage, t0, lane, w);
+        nstage = 0;
+      }
+      if (x.h0) {
+        const uint32_t p = nstage + mbcnt(b0);
+        L.stage_fid[p] = x.e0;
+        L.stage_t[p] = (uint8_t)t;
+        atomicAdd(&L.fcnt[t], 1u);
+      }
+      if (x.h1) {
+        const uint32_t p = nstage + n0 + mbcnt(b1);
+        L.stage_fid[p] = x.e1;
+        L.stage_t[p] = (uint8_t)t;
+        atomicAdd(&L.fcnt[t], 1u);
+      }
+      nstage += ne;
       visited += take;
       wave_sync();
     }
     wave_sync();
 
-    if (ovf) {  // hand the whole chunk to k_heavy
+    if (ovf) {  // frontier exceeded the LDS stack: hand the chunk to k_heavy
       if (lane == 0) {
         const uint32_t d = atomicAdd(&w.stats->n_deferred, 1u);
         w.deferred[d] = c;
       }
-      for (uint32_t j = lane; j < nt; j += 64) {
-        w.cnt[t0 + j] = 0;
-        w.off_tmp[t0 + j] = 0;
-      }
+      for (uint32_t j = lane; j < nt; j += 64) w.cnt[t0 + j] = 0;
       wave_sync();
       continue;
     }
-
-    // ---- flush: per-topic counts -> one reservation -> counting sort ----
-    uint32_t cl[WALK_CHUNK / 64];
-    uint32_t csum = 0;
-#pragma unroll
-    for (int k = 0; k < WALK_CHUNK / 64; ++k) {
-      const uint32_t j = lane * (WALK_CHUNK / 64) + k;   // consecutive per lane
-      cl[k] = (j < nt) ? L.cnt[j] : 0u;
-      csum += cl[k];
-    }
-    uint32_t ctotal;
-    uint32_t cb = wave_excl_scan(csum, lane, &ctotal);
-    unsigned long long base = 0;
-    if (lane == 0 && ctotal) base = atomicAdd(&w.stats->cursor, (unsigned long long)ctotal);
-    base = __shfl(base, 0, 64);
-    wave_sync();
-#pragma unroll
-    for (int k = 0; k < WALK_CHUNK / 64; ++k) {
-      const uint32_t j = lane * (WALK_CHUNK / 64) + k;
-      if (j < nt) {
-        w.off_tmp[t0 + j] = base + cb;
-        w.cnt[t0 + j] = cl[k];
-        L.cnt[j] = cb;
-      }
-      cb += cl[k];
-    }
-    wave_sync();
-    if (base + ctotal > w.ids_cap) {
-      if (lane == 0) atomicOr(&w.stats->overflow, 1u);
-    } else {
-      for (uint32_t i = lane; i < nstage; i += 64) {
-        const uint32_t tt = L.stage_t[i];
-        const uint32_t p = atomicAdd(&L.cnt[tt], 1u);
-        w.ids_tmp[base + p] = L.stage_fid[i];
-      }
-    }
+    if (nstage) flush_stage(L, nstage, t0, lane, w);
+    for (uint32_t j = lane; j < nt; j += 64) w.cnt[t0 + j] = L.cnt[j];
     wave_sync();
   }
   if (lane == 0 && visited) atomicAdd(&w.stats->visited, (unsigned long long)visited);
@@ -469,14 +485,13 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
     if ((tf & TF_WILDCARD) && mode == MODE_TRIE) {
       if (lane == 0) {
         w.cnt[t] = 0;
-        w.off_tmp[t] = 0;
         w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
       }
       continue;
     }
     const uint2 root = (tf & TF_WILDCARD) ? make_uint2(0, mk_meta(0, 0, 0, 0, 1))
                                           : make_uint2(0, mk_meta(0, 0, root_fl, 0, 0));
-    unsigned long long base = 0;
+    unsigned long long base = 0, pbase = 0;
     uint32_t count = 0;
     bool err = false, fits = true;
     for (int pass = 0; pass < 2 && !err; ++pass) {
@@ -519,9 +534,13 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
       wave_sync();
       if (pass == 0 && !err) {
         count = k;
-        if (lane == 0 && count) base = atomicAdd(&w.stats->cursor, (unsigned long long)count);
+        if (lane == 0 && count) {
+          base = atomicAdd(&w.stats->cursor, (unsigned long long)count);
+          pbase = atomicAdd(&w.stats->pieces, 1ull);
+        }
         base = __shfl(base, 0, 64);
-        fits = base + count <= w.ids_cap;
+        pbase = __shfl(pbase, 0, 64);
+        fits = base + count <= w.ids_cap && pbase < w.pieces_cap;
         if (!fits && lane == 0) atomicOr(&w.stats->overflow, 1u);
       }
     }
@@ -529,11 +548,10 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
       if (err) {
         atomicAdd(&w.stats->errors, 1u);
         w.cnt[t] = 0;
-        w.off_tmp[t] = 0;
         w.tfl[t] = (uint8_t)(tf | TF_HEAVY | TF_ERROR);
       } else {
         w.cnt[t] = count;
-        w.off_tmp[t] = base;
+        if (count && fits) w.pieces[pbase] = mk_piece(t, count | HEAVY_PIECE, base);
         w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
       }
     }
@@ -585,7 +603,7 @@ __global__ __launch_bounds__(1024) void k_scan_top(uint64_t* __restrict__ tile_s
 
 __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__ cnt, uint32_t n,
                                                     const uint64_t* __restrict__ tile_sums, uint32_t ntiles,
-                                                    uint64_t* __restrict__ row_ptr) {
+                                                    uint64_t* __restrict__ row_ptr, uint64_t* __restrict__ copy) {
   __shared__ uint64_t wsum[4];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t i0 = blockIdx.x * SCAN_TILE + threadIdx.x * 8;
@@ -608,28 +626,37 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
   pre += x - s;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    if (i0 + k < n) row_ptr[i0 + k] = pre;
+    if (i0 + k < n) {
+      row_ptr[i0 + k] = pre;
+      if (copy) copy[i0 + k] = pre;
+    }
     pre += v[k];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) row_ptr[n] = tile_sums[ntiles];
 }
 
-// chunk-ordered ids -> CSR rows (one lane per topic)
-__global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ off_tmp,
-                                                 const uint32_t* __restrict__ cnt,
+// pieces -> CSR rows.  cursor[t] starts at row_ptr[t]; each valid piece takes
+// its slot with one atomic (pieces of one topic may land in any order: a row
+// is a set).  Light pieces of topics re-run by k_heavy are ignored.
+__global__ __launch_bounds__(256) void k_compact(const uint4* __restrict__ pieces, const uint8_t* __restrict__ tfl,
                                                  const uint32_t* __restrict__ ids_tmp, uint32_t n,
                                                  const uint64_t* __restrict__ row_ptr,
-                                                 uint32_t* __restrict__ ids, uint64_t ids_cap,
-                                                 MatchStats* stats) {
+                                                 unsigned long long* __restrict__ cursor, uint32_t* __restrict__ ids,
+                                                 uint64_t ids_cap, MatchStats* stats) {
   if (stats->overflow) return;
   if (row_ptr[n] > ids_cap) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, 2u);
     return;
   }
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    const uint32_t c = cnt[t];
-    const uint64_t s = off_tmp[t], d = row_ptr[t];
-    for (uint32_t k = 0; k < c; ++k) ids[d + k] = ids_tmp[s + k];
+  const uint64_t np = stats->pieces;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < np; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4 pc = pieces[i];
+    const uint32_t t = pc.x, c = pc.y & ~HEAVY_PIECE;
+    const bool heavy = (pc.y & HEAVY_PIECE) != 0;
+    if ((tfl[t] & TF_HEAVY) && !heavy) continue;
+    const uint64_t s = (uint64_t)pc.z | ((uint64_t)pc.w << 32);
+    const uint64_t d = atomicAdd(&cursor[t], (unsigned long long)c);
+    for (uint32_t k2 = 0; k2 < c; ++k2) ids[d + k2] = ids_tmp[s + k2];
   }
 }
 
@@ -645,12 +672,12 @@ int walk_grid_blocks(uint32_t n) {
 size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
 static void scan_counts(const uint32_t* cnt, uint32_t n, uint64_t* tile_sums, uint64_t* row_ptr,
-                        hipStream_t s) {
+                        hipStream_t s, uint64_t* copy = nullptr) {
   const uint32_t ntiles = (uint32_t)scan_tiles(n);
   if (ntiles) hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(256), 0, s, cnt, n, tile_sums);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, tile_sums, ntiles);
-  if (ntiles) hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(256), 0, s, cnt, n, tile_sums, ntiles, row_ptr);
-  else hipLaunchKernelGGL(k_scan_apply, dim3(1), dim3(256), 0, s, cnt, n, tile_sums, ntiles, row_ptr);
+  hipLaunchKernelGGL(k_scan_apply, dim3(ntiles ? ntiles : 1), dim3(256), 0, s, cnt, n, tile_sums, ntiles, row_ptr,
+                     copy);
 }
 
 hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n,
@@ -667,9 +694,9 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64 * WALK_WAVES), 0, s, tab, off, n, mode, w);
   if (ev_walk) hipEventRecord(ev_walk[1], s);
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
-  scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);
-  hipLaunchKernelGGL(k_compact, dim3(min((n + 255) / 256, 4096u)), dim3(256), 0, s, w.off_tmp, w.cnt,
-                     w.ids_tmp, n, out.row_ptr, out.ids, out.ids_cap, w.stats);
+  scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s, w.off_tmp);
+  hipLaunchKernelGGL(k_compact, dim3(min((n + 255) / 256 + 1, 8192u)), dim3(256), 0, s, w.pieces, w.tfl, w.ids_tmp,
+                     n, out.row_ptr, (unsigned long long*)w.off_tmp, out.ids, out.ids_cap, w.stats);
   return hipGetLastError();
 }
 

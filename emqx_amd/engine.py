@@ -183,6 +183,9 @@ class GpuMatcher:
         return {"n_ids": a.value, "visited": b.value, "deferred_chunks": c.value, "overflow": d.value,
                 "errors": e.value}
 
+    def set_debug(self, flags: int):
+        self._check(self.lib.egm_set_debug(self.ctx, flags), "egm_set_debug")
+
     def set_timing(self, on: bool):
         self._check(self.lib.egm_set_timing(self.ctx, 1 if on else 0), "egm_set_timing")
 

@@ -137,6 +137,9 @@ int egm_last_stats(egm_ctx* ctx, uint64_t* n_ids, uint64_t* visited, uint32_t* n
 /* Enable per-kernel timing with HIP events on the launch stream (0/1) and read
    the accumulated walk-kernel time (ms) and launch count. */
 int egm_set_timing(egm_ctx* ctx, int enable);
+/* Test hooks: bit 0 routes every chunk through the overflow (heavy) kernel. */
+#define EGM_DEBUG_FORCE_HEAVY 1u
+int egm_set_debug(egm_ctx* ctx, uint32_t flags);
 int egm_get_timing(egm_ctx* ctx, double* walk_ms, uint64_t* walk_launches, double* fanout_ms,
                    uint64_t* fanout_launches);
 

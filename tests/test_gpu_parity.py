@@ -129,12 +129,19 @@ def test_heavy_path_wide_frontier(gm):
     topics = [b"/".join(b"k%d" % l for l in range(D)), b"k0/zz", b"/".join(b"k%d" % l for l in range(D - 1)) +
               b"/no"] + [b"p/q/r"] * 300
     res = gm.match_strings(topics, L.EGM_MODE_TRIE)
-    assert res.n_heavy > 0 and res.n_error == 0
+    assert res.n_error == 0
+    gm.set_debug(1)   # EGM_DEBUG_FORCE_HEAVY: the same batch through k_heavy
+    try:
+        hv = gm.match_strings(topics, L.EGM_MODE_TRIE)
+    finally:
+        gm.set_debug(0)
+    assert hv.n_heavy == len(topics) and hv.n_error == 0
+    assert sets_of(hv) == sets_of(res)
     got = sets_of(res)
     assert len(got[0]) == (1 << D) - 1 + 1 + 1   # all but the all-literal filter, + '#', 'k0/#'
     names = dict(enumerate(filters))
     for i, t in enumerate(topics[:3]):
-        assert [names[x] for x in got[i]] == sorted(R.trie_semantics(t, filters))
+        assert sorted(names[x] for x in got[i]) == sorted(R.trie_semantics(t, filters))
     rr = gm.match_strings(topics, L.EGM_MODE_ROUTES)
     assert sets_of(rr)[0] == sorted(got[0] + [0])   # + the exact filter k0/../k10
 
@@ -150,6 +157,24 @@ def test_config_c0_vs_cpp_oracle(gm, mode):
     assert np.array_equal(res.row_ptr, row)
     assert np.array_equal(canonical(res.row_ptr, res.ids), canonical(row, ids))
     assert res.visited > 0
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_config_c0_heavy_path_vs_cpp_oracle(gm, mode):
+    """The overflow kernel alone (every chunk deferred) is also bit-exact."""
+    f, t = synth.config("c0", n_topics=30_000)
+    gm.build(f.blob, f.off)
+    gm.set_debug(1)
+    try:
+        res = gm.match(t.blob, t.off, mode)
+    finally:
+        gm.set_debug(0)
+    assert res.n_heavy == t.n
+    o = OracleTrie(True, mode)
+    o.add(f.blob, f.off)
+    row, ids = o.match(t.blob, t.off, threads=8)
+    assert np.array_equal(res.row_ptr, row)
+    assert np.array_equal(canonical(res.row_ptr, res.ids), canonical(row, ids))
 
 
 def test_golden_fixture(gm):
