@@ -184,15 +184,19 @@ def main():
         else:
             exchange.step()
 
-    # warmup (also sizes the id buffer)
-    for _ in range(max(1, args.warmup)):
+    # size the id buffer (untimed), then warm up
+    for _ in range(4):
         step()
         torch.cuda.synchronize(dev)
         st = gm.last_stats()
-        if st["overflow"]:
-            cap = int(st["n_ids"] * 1.25) + 1024
-            d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
-            log(f"[rank {rank}] grew id buffer to {cap}")
+        if not st["overflow"]:
+            break
+        cap = int(st["n_ids"] * 1.25) + 1024
+        d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
+        log(f"[rank {rank}] grew id buffer to {cap}")
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
     st = gm.last_stats()
     assert st["overflow"] == 0 and st["errors"] == 0, st
 
