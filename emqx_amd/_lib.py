@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libemqx_gpu_match.so")
+LIB_PATH = os.environ.get("EGM_LIB") or os.path.join(_HERE, "libemqx_gpu_match.so")  # EGM_LIB: A/B tuning
 
 EGM_OK = 0
 EGM_E_INVAL = -1

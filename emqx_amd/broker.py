@@ -1,0 +1,183 @@
+"""Host mirror of the publish side of ``emqx_broker`` + ``emqx_shared_sub``.
+
+``publish_batch`` is the batched ``emqx_broker:publish/1`` (apps/emqx/src/emqx_broker.erl:200-209)
+for many messages: ``emqx_router:match_routes/1`` on the GPU, then the
+``dispatch/2`` subscriber expansion (:283-308) on the GPU fan-out kernel from
+a filter -> subscriber CSR, then per shared group one member picked by the
+configured strategy (emqx_shared_sub.erl:239-290) and remote node routes
+turned into forwards (:242-245).
+
+Delivery entries:
+  ("sub", filter, sub_id)                    local subscriber of filter
+  ("group", filter, group, member)           $share group, one member picked
+  ("node", filter, node)                     route to another node (forward)
+
+Subscriber sharding ({shard, Topic, I} bags beyond 1024 subscribers,
+emqx_broker.erl:149-157, emqx_broker_helper.erl:82-86) changes only the layout
+of the reference's ETS bags, never the delivery set; the fan-out CSR is the
+flattened union.
+"""
+from __future__ import annotations
+
+import random
+import zlib
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .router import Router
+from .topic import parse
+
+GROUP_BIT = 0x80000000
+SHARD_THRESHOLD = 1024        # ?SHARD, emqx_broker_helper.erl:54
+STRATEGIES = ("random", "round_robin", "sticky", "hash", "hash_clientid", "hash_topic")
+
+
+class Broker:
+    def __init__(self, router: Optional[Router] = None, device: int = 0, node: str = "local",
+                 shared_strategy: str = "random", seed: int = 0, shards: int = 32):
+        if shared_strategy not in STRATEGIES:
+            raise ValueError(shared_strategy)
+        self.router = router or Router(device=device, node=node)
+        self.node = node
+        self.strategy = shared_strategy
+        self.subscribers: Dict[bytes, List[int]] = {}            # filter -> local sub ids
+        self.shard_of: Dict[Tuple[bytes, int], int] = {}         # (filter, sub) -> shard (layout only)
+        self.shared: Dict[Tuple[bytes, bytes], List[int]] = {}   # (group, filter) -> members
+        self.group_ids: Dict[bytes, int] = {}
+        self.group_names: List[bytes] = []
+        self.clientid: Dict[int, bytes] = {}
+        self._rng = random.Random(seed)
+        self._rr: Dict[Tuple[bytes, bytes], int] = {}
+        self._sticky: Dict[Tuple[bytes, bytes], int] = {}
+        self._shards = shards
+        self._csr_dirty = True
+
+    # -- subscribe side (emqx_broker.erl:116-162, emqx_shared_sub.erl:108-109) --
+    def subscribe(self, topic: bytes, sub_id: int, opts: Optional[dict] = None, clientid: Optional[bytes] = None):
+        flt, o = parse(topic, opts)
+        if clientid is not None:
+            self.clientid[sub_id] = clientid
+        group = o.get("share")
+        if group is None:
+            subs = self.subscribers.setdefault(flt, [])
+            if sub_id in subs:
+                return "ok"
+            subs.append(sub_id)
+            if len(subs) > SHARD_THRESHOLD:
+                self.shard_of[(flt, sub_id)] = zlib.crc32(str(sub_id).encode()) % self._shards + 1
+            self.router.do_add_route(flt, self.node)
+        else:
+            mem = self.shared.setdefault((group, flt), [])
+            if sub_id in mem:
+                return "ok"
+            mem.append(sub_id)
+            if group not in self.group_ids:
+                self.group_ids[group] = len(self.group_names)
+                self.group_names.append(group)
+            self.router.do_add_route(flt, ("group", group))
+        self._csr_dirty = True
+        return "ok"
+
+    def unsubscribe(self, topic: bytes, sub_id: int, opts: Optional[dict] = None):
+        flt, o = parse(topic, opts)
+        group = o.get("share")
+        if group is None:
+            subs = self.subscribers.get(flt, [])
+            if sub_id in subs:
+                subs.remove(sub_id)
+                self.shard_of.pop((flt, sub_id), None)
+                if not subs:
+                    del self.subscribers[flt]
+                    self.router.do_delete_route(flt, self.node)
+        else:
+            mem = self.shared.get((group, flt), [])
+            if sub_id in mem:
+                mem.remove(sub_id)
+                if not mem:
+                    del self.shared[(group, flt)]
+                    self.router.do_delete_route(flt, ("group", group))
+        self._csr_dirty = True
+        return "ok"
+
+    # -- fan-out table ------------------------------------------------------------
+    def _upload_csr(self):
+        if not self._csr_dirty:
+            return
+        r = self.router
+        r.commit()
+        n = r._next
+        lists: List[List[int]] = [[] for _ in range(n)]
+        for flt, subs in self.subscribers.items():
+            lists[r.filter_id(flt)].extend(subs)
+        for (group, flt) in self.shared:
+            lists[r.filter_id(flt)].append(GROUP_BIT | self.group_ids[group])
+        row = np.zeros(n + 1, dtype=np.uint64)
+        row[1:] = np.cumsum([len(x) for x in lists]) if n else []
+        flat = np.fromiter((s for x in lists for s in x), dtype=np.uint32, count=int(row[-1]) if n else 0)
+        r.m.subs_build(row, flat)
+        self._csr_dirty = False
+
+    # -- publish side -------------------------------------------------------------------
+    def publish(self, topic: bytes, clientid: bytes = b"") -> List[tuple]:
+        return self.publish_batch([topic], [clientid])[0]
+
+    def publish_batch(self, topics: Sequence[bytes], clientids: Optional[Sequence[bytes]] = None) -> List[List[tuple]]:
+        self._upload_csr()
+        r = self.router
+        res = r.match_filters_batch(topics)
+        drow, dfid, dsub = r.m.fanout(res)
+        out = []
+        for k, t in enumerate(topics):
+            dl: List[tuple] = []
+            for j in range(int(drow[k]), int(drow[k + 1])):
+                f = r.filter_of(int(dfid[j]))
+                s = int(dsub[j])
+                if s & GROUP_BIT:
+                    g = self.group_names[s & ~GROUP_BIT]
+                    m = self._pick(g, f, t, clientids[k] if clientids else b"")
+                    if m is not None:
+                        dl.append(("group", f, g, m))
+                else:
+                    dl.append(("sub", f, s))
+            # routes to other nodes are forwarded, not expanded here
+            for fid in res.row(k).tolist():
+                f = r.filter_of(fid)
+                for d in r.routes[f]:
+                    if d != self.node and not (isinstance(d, tuple) and d[0] == "group"):
+                        dl.append(("node", f, d))
+            out.append(dl)
+        return out
+
+    def _pick(self, group: bytes, flt: bytes, source_topic: bytes, clientid: bytes) -> Optional[int]:
+        """``pick/6`` + ``do_pick_subscriber/6`` (emqx_shared_sub.erl:239-290).
+
+        phash2 (ERTS) is replaced by crc32: the member a hash strategy picks is
+        therefore not the reference's (parity is at (filter, group) level,
+        SURVEY §8c); each strategy keeps its reference behaviour otherwise.
+        """
+        mem = self.shared.get((group, flt))
+        if not mem:
+            return None
+        n = len(mem)
+        key = (group, flt)
+        s = self.strategy
+        if n == 1:
+            return mem[0]
+        if s == "random":
+            return mem[self._rng.randrange(n)]
+        if s == "round_robin":
+            i = self._rr.get(key)
+            i = self._rng.randrange(n) if i is None else (i + 1) % n
+            self._rr[key] = i
+            return mem[i]
+        if s == "sticky":
+            cur = self._sticky.get(key)
+            if cur in mem:
+                return cur
+            cur = mem[self._rng.randrange(n)]
+            self._sticky[key] = cur
+            return cur
+        if s in ("hash", "hash_clientid"):
+            return mem[zlib.crc32(clientid) % n]
+        return mem[zlib.crc32(source_topic) % n]   # hash_topic

@@ -6,8 +6,9 @@
 // it once per visited prefix (:192-206).  Here the same filter set is a
 // word-level trie flattened into three HBM arrays:
 //
-//   nodes[]  16 B  {plus_child, hash_fid, term_fid, meta}
-//   edges[]  64 B buckets of four 16 B slots {parent, word_id, child, child_flags}
+//   nodes[]  16 B  {plus_child, hash_fid, term_fid, flags}
+//   edges[]  128 B buckets of four 32 B slots {parent, word_id, child, flags,
+//            child's plus_child, hash_fid, term_fid, -}
 //   dict[]   32 B slots {hash64, word_id, len, inline bytes[16]}  (+ blob for long words)
 //
 // A literal transition is one bucket read keyed by (node, word_id); word ids
@@ -51,14 +52,20 @@ struct NodeRec {          // 16 B, one dwordx4 load
   uint32_t plus_child;    // node reached by '+', or NONE
   uint32_t hash_fid;      // filter id of "P/#", or NONE
   uint32_t term_fid;      // filter id of "P", or NONE
-  uint32_t meta;          // [0:4) flags of plus_child, [4:8) own flags
+  uint32_t flags;         // F_* bits of this node
 };
 
-struct EdgeSlot {         // 16 B
+// A literal edge carries a copy of its child's record, so a literal
+// transition is a single 128 B bucket read (four 32 B slots).
+struct EdgeSlot {         // 32 B
   uint32_t parent;        // NONE = empty, TOMB = deleted
   uint32_t wid;
   uint32_t child;
   uint32_t child_flags;
+  uint32_t child_plus;    // copy of nodes[child].plus_child
+  uint32_t child_hash;    // copy of nodes[child].hash_fid
+  uint32_t child_term;    // copy of nodes[child].term_fid
+  uint32_t pad;
 };
 
 struct DictSlot {         // 32 B
@@ -69,7 +76,7 @@ struct DictSlot {         // 32 B
 };
 
 static_assert(sizeof(NodeRec) == 16, "NodeRec");
-static_assert(sizeof(EdgeSlot) == 16, "EdgeSlot");
+static_assert(sizeof(EdgeSlot) == 32, "EdgeSlot");
 static_assert(sizeof(DictSlot) == 32, "DictSlot");
 
 // ---- hashing (identical on host and device) --------------------------------

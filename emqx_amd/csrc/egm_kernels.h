@@ -62,7 +62,10 @@ struct MatchOut {                 // CSR result (device)
 };
 
 // launch sizing shared with the host (egm_capi.cpp)
-constexpr int WALK_CHUNK = 128;   // topics per wave chunk
+#ifndef EGM_WALK_CHUNK
+#define EGM_WALK_CHUNK 64   // topics per wave chunk
+#endif
+constexpr int WALK_CHUNK = EGM_WALK_CHUNK;
 int walk_grid_blocks(uint32_t n_topics);
 size_t scan_tiles(uint32_t n);
 

@@ -29,13 +29,28 @@ namespace egm {
 constexpr int MODE_TRIE = 0;
 constexpr int MODE_ROUTES = 1;
 
-constexpr int WALK_WAVES = 4;        // waves per 256-thread block
-constexpr int WALK_STACK = 512;      // items per wave
-constexpr int WALK_STAGE = 1024;     // staged matches per wave chunk
-constexpr int WALK_WORDS = 1024;     // staged topic word ids per wave chunk
-constexpr int HEAVY_STACK = 8192;    // items (64 KB LDS) per heavy wave
+#ifndef EGM_WALK_WAVES
+#define EGM_WALK_WAVES 1   // waves per block (LDS granularity)
+#endif
+constexpr int WALK_WAVES = EGM_WALK_WAVES;
+#ifndef EGM_WALK_STACK
+#define EGM_WALK_STACK 384   // items per wave (20 B each)
+#endif
+constexpr int WALK_STACK = EGM_WALK_STACK;
+#ifndef EGM_WALK_STAGE
+#define EGM_WALK_STAGE 512   // staged matches per flush
+#endif
+constexpr int WALK_STAGE = EGM_WALK_STAGE;
+#ifndef EGM_WALK_WORDS
+#define EGM_WALK_WORDS 1024   // staged topic word ids per wave chunk
+#endif
+constexpr int WALK_WORDS = EGM_WALK_WORDS;
+constexpr int HEAVY_STACK = 6144;    // items (120 KB LDS) per heavy wave
 constexpr int TOK_BLOCK = 256;
-constexpr int TOK_LDS = 16384;
+#ifndef EGM_TOK_LDS
+#define EGM_TOK_LDS 32768   // staged topic bytes per tokenise block
+#endif
+constexpr int TOK_LDS = EGM_TOK_LDS;
 constexpr int SCAN_TILE = 2048;      // counts per scan tile (256 threads x 8)
 
 static_assert(WALK_CHUNK <= 256 && WALK_CHUNK % 64 == 0, "chunk");
@@ -103,50 +118,41 @@ __device__ uint32_t dict_probe(const DevTable& tab, uint64_t h, const uint8_t* p
 
 // -------------------------------------------------------------- tokenise ----
 // emqx_topic:words/1 (emqx_topic.erl:153-164) + wildcard/1 (:53-62) for a
-// batch: one lane per topic, the block's bytes staged in LDS by 4-byte loads.
+// batch: one lane per topic.  The block's bytes are staged in LDS with
+// coalesced 4-byte loads and scanned 4 bytes per LDS read; FNV-1a per word,
+// then the byte-exact dictionary probe.
 // Output: level count, TF_* flags and one word id per level at wid[off[t]+t+l].
-__global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint8_t* __restrict__ blob,
-                                                        const uint32_t* __restrict__ off, uint32_t n,
-                                                        uint32_t* __restrict__ wid, uint32_t* __restrict__ lv,
-                                                        uint8_t* __restrict__ tfl) {
-  __shared__ __attribute__((aligned(16))) uint32_t sw[TOK_LDS / 4];
-  const uint32_t t0 = blockIdx.x * TOK_BLOCK;
-  if (t0 >= n) return;
-  const uint32_t t1 = min(t0 + (uint32_t)TOK_BLOCK, n);
-  const uint32_t s = off[t0], e = off[t1];
-  const uint32_t sa = s & ~3u;
-  const bool staged = (e - sa) <= (uint32_t)TOK_LDS;
-  uint8_t* sb = (uint8_t*)sw;
-  if (staged) {
-    const uint32_t ew = e & ~3u;
-    const uint32_t nfull = (ew - sa) >> 2;
-    const uint32_t* src = (const uint32_t*)(blob + sa);
-    for (uint32_t i = threadIdx.x; i < nfull; i += TOK_BLOCK) sw[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < e - ew; i += TOK_BLOCK) sb[ew - sa + i] = blob[ew + i];
-  }
-  __syncthreads();
-  const uint32_t t = t0 + threadIdx.x;
-  if (t >= t1) return;
-  const uint32_t ts = off[t], len = off[t + 1] - ts;
-  const uint8_t* p = staged ? sb + (ts - sa) : blob + ts;
-  const uint32_t base = ts + t;
-  uint32_t l = 0, ws = 0;
-  uint8_t fl = (len > 0 && p[0] == '$') ? TF_DOLLAR : 0;
+// The topic's bytes start at byte `mis` of the aligned word array `wp`.
+__device__ __forceinline__ void tokenise_one(const DevTable& tab, const uint32_t* wp, uint32_t mis, uint32_t len,
+                                             uint32_t base, uint32_t* __restrict__ wid, uint32_t* lv_out,
+                                             uint8_t* fl_out) {
+  const uint8_t* p = (const uint8_t*)wp + mis;
+  uint32_t l = 0, ws = 0, cw = 0, cwi = 0xFFFFFFFFu;
+  uint32_t first = 0, wfirst = 0;
+  uint8_t fl = 0;
   uint64_t h = FNV_BASIS;
   for (uint32_t i = 0; i <= len; ++i) {
+    uint32_t c = '/';
     if (i < len) {
-      const uint8_t c = p[i];
+      const uint32_t idx = mis + i;
+      if ((idx >> 2) != cwi) {
+        cwi = idx >> 2;
+        cw = wp[cwi];
+      }
+      c = (cw >> (8 * (idx & 3u))) & 0xFFu;
+      if (i == 0) first = c;
+      if (i == ws) wfirst = c;
       if (c != '/') {
-        h = fnv_step(h, c);
+        h = fnv_step(h, (uint8_t)c);
         continue;
       }
     }
     const uint32_t wl = i - ws;
     uint32_t w;
-    if (wl == 1 && p[ws] == '+') {
+    if (wl == 1 && wfirst == '+') {
       w = WID_PLUS;
       fl |= TF_WILDCARD;
-    } else if (wl == 1 && p[ws] == '#') {
+    } else if (wl == 1 && wfirst == '#') {
       w = WID_HASH;
       fl |= TF_WILDCARD;
     } else {
@@ -157,26 +163,75 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
     ws = i + 1;
     h = FNV_BASIS;
   }
+  if (len > 0 && first == '$') fl |= TF_DOLLAR;
+  *lv_out = l;
+  *fl_out = fl;
+}
+
+__global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint8_t* __restrict__ blob,
+                                                        const uint32_t* __restrict__ off, uint32_t n,
+                                                        uint32_t* __restrict__ wid, uint32_t* __restrict__ lv,
+                                                        uint8_t* __restrict__ tfl) {
+  __shared__ __attribute__((aligned(16))) uint32_t sw[TOK_LDS / 4];
+  const uint32_t t0 = blockIdx.x * TOK_BLOCK;
+  if (t0 >= n) return;
+  const uint32_t t1 = min(t0 + (uint32_t)TOK_BLOCK, n);
+  const uint32_t s = off[t0], e = off[t1];
+  const uint32_t sa = s & ~3u;
+  const uint32_t ea = (e + 3u) & ~3u;   // blob is readable up to a multiple of 4 (ABI)
+  const bool staged = (ea - sa) <= (uint32_t)TOK_LDS;
+  if (staged) {
+    const uint32_t nw = (ea - sa) >> 2;
+    const uint32_t* src = (const uint32_t*)(blob + sa);
+    for (uint32_t i = threadIdx.x; i < nw; i += TOK_BLOCK) sw[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t t = t0 + threadIdx.x;
+  if (t >= t1) return;
+  const uint32_t ts = off[t], len = off[t + 1] - ts;
+  uint32_t l;
+  uint8_t fl;
+  if (staged) tokenise_one(tab, sw, ts - sa, len, ts + t, wid, &l, &fl);
+  else tokenise_one(tab, (const uint32_t*)(blob + (ts & ~3u)), ts & 3u, len, ts + t, wid, &l, &fl);
   lv[t] = l;
   tfl[t] = fl;
 }
 
 // ------------------------------------------------------------ NFA expand ----
-// Literal transition: one 64 B bucket of four {parent, wid, child, flags}
-// slots; slots fill in probe order, so the first empty slot ends the search.
-__device__ __forceinline__ uint32_t edge_probe(const DevTable& tab, uint32_t node, uint32_t w,
-                                               uint32_t* cfl) {
+// A work item is (node, meta) plus the node's record, so expanding it needs
+// no read of its own node: meta = level[0:17) | t[17:25) | flags[25:29) |
+// wc<<29 | exact<<30, rec = {plus_child, hash_fid, term_fid}.
+struct Item {
+  uint4 a;        // {node, meta, plus_child, hash_fid}
+  uint32_t term;  // term_fid
+};
+
+__device__ __forceinline__ Item mk_item(uint32_t node, uint32_t meta, uint32_t plus, uint32_t hash,
+                                        uint32_t term) {
+  Item it;
+  it.a = make_uint4(node, meta, plus, hash);
+  it.term = term;
+  return it;
+}
+
+// Literal transition: one 128 B bucket of four 32 B slots; a slot holds the
+// edge key and a copy of the child's record.  Slots fill in probe order, so
+// the first empty slot ends the search.
+__device__ __forceinline__ bool edge_probe(const DevTable& tab, uint32_t node, uint32_t w, uint4* lo_out,
+                                           uint4* hi_out) {
   uint32_t b = edge_bucket(node, w, tab.edge_mask);
   for (;;) {
     const EdgeSlot* bp = tab.edges + (size_t)b * EDGE_BUCKET;
 #pragma unroll
     for (int k = 0; k < EDGE_BUCKET; ++k) {
-      uint4 s = ld16(bp + k);
-      if (s.x == node && s.y == w) {
-        *cfl = s.w;
-        return s.z;
+      const uint4 lo = ld16(bp + k);
+      const uint4 hi = ld16((const uint8_t*)(bp + k) + 16);
+      if (lo.x == node && lo.y == w) {
+        *lo_out = lo;
+        *hi_out = hi;
+        return true;
       }
-      if (s.x == NONE) return NONE;
+      if (lo.x == NONE) return false;
     }
     b = (b + 1) & tab.edge_mask;
   }
@@ -184,7 +239,7 @@ __device__ __forceinline__ uint32_t edge_probe(const DevTable& tab, uint32_t nod
 
 struct Expand {
   uint32_t e0, e1;     // emitted filter ids ('P/#', 'P')
-  uint2 c0, c1;        // children (literal, '+')
+  Item c0, c1;         // children (literal, '+')
   bool h0, h1, hc0, hc1;
 };
 
@@ -200,52 +255,57 @@ struct Expand {
 //                                 lookup_topic(Prefix) -> e1 at D == 1
 // `exact` items walk a wildcard topic as a literal key (ROUTES mode only:
 // lookup_routes(Topic) of emqx_router.erl:129-134).
-__device__ __forceinline__ void expand(const DevTable& tab, int mode, uint2 it, uint32_t D,
+// Each child costs one random read: its bucket line or its node record.
+__device__ __forceinline__ void expand(const DevTable& tab, int mode, const Item& it, uint32_t D,
                                        uint32_t tflags, uint32_t w, Expand& x) {
-  const uint32_t node = it.x, meta = it.y;
+  const uint32_t node = it.a.x, meta = it.a.y;
   const uint32_t level = meta & 0x1FFFFu;
   const uint32_t tm = meta & (0xFFu << 17);
   const uint32_t fl = (meta >> 25) & 0xFu, wc = (meta >> 29) & 1u, ex = (meta >> 30) & 1u;
   const bool atend = level == D;
+  const uint32_t nmeta = (level + 1) | tm | (ex << 30);
   x.h0 = x.h1 = x.hc0 = x.hc1 = false;
+  x.e0 = it.a.w;
+  x.e1 = it.term;
   if (!ex) {
     const bool rootd = (level == 0) && (tflags & TF_DOLLAR);
-    const bool want_hash = (fl & F_HASH) && !rootd;
-    const bool want_term =
-        atend && (fl & F_TERM) && (mode == MODE_ROUTES || wc || (D == 1 && (tflags & TF_DOLLAR)));
+    x.h0 = (fl & F_HASH) && !rootd;
+    x.h1 = atend && (fl & F_TERM) && (mode == MODE_ROUTES || wc || (D == 1 && (tflags & TF_DOLLAR)));
     const bool want_plus = !atend && (fl & F_PLUS) && !rootd;
     const bool want_lit = !atend && (fl & F_LIT) && w < WID_MAX;
-    uint4 rec = make_uint4(NONE, NONE, NONE, 0);
-    if (want_hash || want_term || want_plus) rec = ld16(tab.nodes + node);
-    uint32_t cfl = 0, child = NONE;
-    if (want_lit) child = edge_probe(tab, node, w, &cfl);
-    x.e0 = rec.y;
-    x.h0 = want_hash;
-    x.e1 = rec.z;
-    x.h1 = want_term;
-    x.c0 = make_uint2(child, (level + 1) | tm | (cfl << 25) | (wc << 29));
-    x.hc0 = child != NONE;
-    x.c1 = make_uint2(rec.x, (level + 1) | tm | ((rec.w & 0xFu) << 25) | (1u << 29));
+    uint4 prec = make_uint4(NONE, NONE, NONE, 0), lo, hi;
+    if (want_plus) prec = ld16(tab.nodes + it.a.z);
+    const bool found = want_lit && edge_probe(tab, node, w, &lo, &hi);
+    x.hc0 = found;
+    if (found) x.c0 = mk_item(lo.z, nmeta | (lo.w << 25) | (wc << 29), hi.x, hi.y, hi.z);
     x.hc1 = want_plus;
+    x.c1 = mk_item(it.a.z, nmeta | (prec.w << 25) | (1u << 29), prec.x, prec.y, prec.z);
   } else {
-    const uint4 rec = ld16(tab.nodes + node);
-    if (atend) {
-      x.e1 = rec.z;
-      x.h1 = rec.z != NONE;
-      return;
-    }
-    uint32_t child = NONE, cfl = 0;
-    if (w == WID_PLUS) child = rec.x;
+    x.h1 = atend && (fl & F_TERM);
+    if (atend) return;
+    uint32_t child = NONE;
+    if (w == WID_PLUS) child = it.a.z;
     else if (w == WID_HASH) child = tab.hash_child[node];
-    else if (w < WID_MAX) child = edge_probe(tab, node, w, &cfl);
-    x.c0 = make_uint2(child, (level + 1) | tm | (1u << 30));
-    x.hc0 = child != NONE;
+    uint4 lo, hi;
+    if (child != NONE) {
+      const uint4 r = ld16(tab.nodes + child);
+      x.c0 = mk_item(child, nmeta | (r.w << 25), r.x, r.y, r.z);
+      x.hc0 = true;
+    } else if (w < WID_MAX && edge_probe(tab, node, w, &lo, &hi)) {
+      x.c0 = mk_item(lo.z, nmeta | (lo.w << 25), hi.x, hi.y, hi.z);
+      x.hc0 = true;
+    }
   }
+}
+
+__device__ __forceinline__ Item root_item(const uint4& r, uint32_t t, bool exact) {
+  return mk_item(0, mk_meta(0, t, r.w, 0, exact ? 1u : 0u), r.x, r.y, r.z);
 }
 
 // ------------------------------------------------------------------ walk ----
 struct alignas(16) WaveLds {
-  uint2 stack[WALK_STACK];
+  uint4 stack_a[WALK_STACK];
+  uint32_t stack_t[WALK_STACK];
   uint32_t stage_fid[WALK_STAGE];
   uint32_t words[WALK_WORDS];
   uint32_t tbase[WALK_CHUNK];   // word base: LDS index (staged) or wid index
@@ -312,7 +372,7 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
   WaveLds& L = lds_all[wave];
   const uint32_t nwaves = gridDim.x * WALK_WAVES;
   const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
-  const uint32_t root_fl = (tab.nodes[0].meta >> 4) & 0xFu;
+  const uint4 root = ld16(tab.nodes);
   uint64_t visited = 0;
 
   for (uint32_t c = blockIdx.x * WALK_WAVES + wave; c < nchunks; c += nwaves) {
@@ -370,20 +430,24 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
       if (sp < 64 && next < nt) {  // refill with new roots
         const uint32_t k = min(64u - sp, nt - next);
         bool has = false;
-        uint2 it = make_uint2(0, 0);
+        Item it = root_item(root, 0, false);
         if (lane < k) {
           const uint32_t j = next + lane;
           const uint32_t f = L.tinfo[j] >> 24;
           if (!(f & TF_WILDCARD)) {
             has = true;
-            it = make_uint2(0, mk_meta(0, j, root_fl, 0, 0));
+            it = root_item(root, j, false);
           } else if (mode == MODE_ROUTES) {
             has = true;
-            it = make_uint2(0, mk_meta(0, j, 0, 0, 1));
+            it = root_item(root, j, true);
           }
         }
         const uint64_t b = __ballot(has);
-        if (has) L.stack[sp + mbcnt(b)] = it;
+        if (has) {
+          const uint32_t p = sp + mbcnt(b);
+          L.stack_a[p] = it.a;
+          L.stack_t[p] = it.term;
+        }
         sp += popc(b);
         next += k;
         wave_sync();
@@ -395,8 +459,13 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
       const uint32_t take = min(64u, sp);
       const uint32_t bi = sp - take;
       const bool act = lane < take;
-      uint2 it = make_uint2(0, 0);
-      if (act) it = L.stack[bi + lane];
+      Item it;
+      it.a = make_uint4(0, 0, 0, 0);
+      it.term = NONE;
+      if (act) {
+        it.a = L.stack_a[bi + lane];
+        it.term = L.stack_t[bi + lane];
+      }
       sp = bi;
       wave_sync();
 
@@ -404,12 +473,15 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
       x.h0 = x.h1 = x.hc0 = x.hc1 = false;
       uint32_t t = 0;
       if (act) {
-        t = (it.y >> 17) & 0xFFu;
+        t = (it.a.y >> 17) & 0xFFu;
         const uint32_t ti = L.tinfo[t];
         const uint32_t D = ti & 0xFFFFFFu, tf = ti >> 24;
-        const uint32_t level = it.y & 0x1FFFFu;
+        const uint32_t level = it.a.y & 0x1FFFFu;
         uint32_t wd = WID_NONE;
-        if (level < D) wd = staged ? L.words[L.tbase[t] + level] : w.wid[L.tbase[t] + level];
+        if (level < D) {
+          if (staged) wd = L.words[L.tbase[t] + level];
+          else wd = __builtin_nontemporal_load(w.wid + L.tbase[t] + level);  // distinct op: no flat merge
+        }
         expand(tab, mode, it, D, tf, wd, x);
       }
       // children -> stack (checked first: an overflow abandons the chunk)
@@ -419,8 +491,16 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
         ovf = true;
         break;
       }
-      if (x.hc0) L.stack[sp + mbcnt(c0)] = x.c0;
-      if (x.hc1) L.stack[sp + m0 + mbcnt(c1)] = x.c1;
+      if (x.hc0) {
+        const uint32_t p = sp + mbcnt(c0);
+        L.stack_a[p] = x.c0.a;
+        L.stack_t[p] = x.c0.term;
+      }
+      if (x.hc1) {
+        const uint32_t p = sp + m0 + mbcnt(c1);
+        L.stack_a[p] = x.c1.a;
+        L.stack_t[p] = x.c1.term;
+      }
       sp += nc;
       // emits -> stage, flushed to global pieces whenever it would overflow
       const uint64_t b0 = __ballot(x.h0), b1 = __ballot(x.h1);
@@ -465,13 +545,15 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
 }
 
 // ----------------------------------------------------------------- heavy ----
-// Topics of deferred chunks: one wave per topic, 64 KB LDS stack, two passes
-// (count, then fill at a reserved offset) so the output needs no staging.
+// Topics of deferred chunks: one wave per topic, LDS stack of HEAVY_STACK
+// items, two passes (count, then fill at a reserved offset) so the output
+// needs no staging.
 __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __restrict__ off, uint32_t n,
                                               int mode, MatchWork w) {
-  __shared__ uint2 stk[HEAVY_STACK];
+  __shared__ uint4 stk_a[HEAVY_STACK];
+  __shared__ uint32_t stk_t[HEAVY_STACK];
   const uint32_t lane = threadIdx.x;
-  const uint32_t root_fl = (tab.nodes[0].meta >> 4) & 0xFu;
+  const uint4 rootr = ld16(tab.nodes);
   const uint32_t total = w.stats->n_deferred * (uint32_t)WALK_CHUNK;
   uint64_t visited = 0;
   for (;;) {
@@ -489,26 +571,33 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
       }
       continue;
     }
-    const uint2 root = (tf & TF_WILDCARD) ? make_uint2(0, mk_meta(0, 0, 0, 0, 1))
-                                          : make_uint2(0, mk_meta(0, 0, root_fl, 0, 0));
+    const Item root = root_item(rootr, 0, (tf & TF_WILDCARD) != 0);
     unsigned long long base = 0, pbase = 0;
     uint32_t count = 0;
     bool err = false, fits = true;
     for (int pass = 0; pass < 2 && !err; ++pass) {
       uint32_t sp = 1, k = 0;
-      if (lane == 0) stk[0] = root;
+      if (lane == 0) {
+        stk_a[0] = root.a;
+        stk_t[0] = root.term;
+      }
       wave_sync();
       while (sp) {
         const uint32_t take = min(64u, sp), bi = sp - take;
         const bool act = lane < take;
-        uint2 it = make_uint2(0, 0);
-        if (act) it = stk[bi + lane];
+        Item it;
+        it.a = make_uint4(0, 0, 0, 0);
+        it.term = NONE;
+        if (act) {
+          it.a = stk_a[bi + lane];
+          it.term = stk_t[bi + lane];
+        }
         sp = bi;
         wave_sync();
         Expand x;
         x.h0 = x.h1 = x.hc0 = x.hc1 = false;
         if (act) {
-          const uint32_t level = it.y & 0x1FFFFu;
+          const uint32_t level = it.a.y & 0x1FFFFu;
           const uint32_t wd = level < D ? w.wid[gb + level] : WID_NONE;
           expand(tab, mode, it, D, tf, wd, x);
         }
@@ -525,8 +614,16 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
           err = true;
           break;
         }
-        if (x.hc0) stk[sp + mbcnt(c0)] = x.c0;
-        if (x.hc1) stk[sp + m0 + mbcnt(c1)] = x.c1;
+        if (x.hc0) {
+          const uint32_t p = sp + mbcnt(c0);
+          stk_a[p] = x.c0.a;
+          stk_t[p] = x.c0.term;
+        }
+        if (x.hc1) {
+          const uint32_t p = sp + m0 + mbcnt(c1);
+          stk_a[p] = x.c1.a;
+          stk_t[p] = x.c1.term;
+        }
         sp += nc;
         if (pass == 0) visited += take;
         wave_sync();
@@ -648,15 +745,47 @@ __global__ __launch_bounds__(256) void k_compact(const uint4* __restrict__ piece
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, 2u);
     return;
   }
+  // one wave handles 64 consecutive pieces: every lane claims one piece's
+  // destination, then the wave copies the pieces one after another with
+  // coalesced 64-lane loads/stores, eight pieces' loads in flight at a time
   const uint64_t np = stats->pieces;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < np; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint4 pc = pieces[i];
-    const uint32_t t = pc.x, c = pc.y & ~HEAVY_PIECE;
-    const bool heavy = (pc.y & HEAVY_PIECE) != 0;
-    if ((tfl[t] & TF_HEAVY) && !heavy) continue;
-    const uint64_t s = (uint64_t)pc.z | ((uint64_t)pc.w << 32);
-    const uint64_t d = atomicAdd(&cursor[t], (unsigned long long)c);
-    for (uint32_t k2 = 0; k2 < c; ++k2) ids[d + k2] = ids_tmp[s + k2];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t b0 = wave * 64; b0 < np; b0 += nwaves * 64) {
+    const uint64_t i = b0 + lane;
+    uint32_t c = 0;
+    uint64_t s = 0, d = 0;
+    if (i < np) {
+      const uint4 pc = pieces[i];
+      const uint32_t t = pc.x;
+      const bool heavy = (pc.y & HEAVY_PIECE) != 0;
+      if (!((tfl[t] & TF_HEAVY) && !heavy)) {
+        c = pc.y & ~HEAVY_PIECE;
+        s = (uint64_t)pc.z | ((uint64_t)pc.w << 32);
+        d = atomicAdd(&cursor[t], (unsigned long long)c);
+      }
+    }
+#pragma unroll 1
+    for (int j0 = 0; j0 < 64; j0 += 8) {
+      uint32_t v[8], cj[8];
+      uint64_t dj[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        cj[u] = __shfl(c, j0 + u, 64);
+        const uint64_t sj = __shfl(s, j0 + u, 64);
+        dj[u] = __shfl(d, j0 + u, 64);
+        v[u] = lane < cj[u] ? ids_tmp[sj + lane] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (lane < cj[u]) ids[dj[u] + lane] = v[u];
+        if (cj[u] > 64u) {  // long pieces: the rest in 64-wide strides
+          const uint64_t sj = __shfl(s, j0 + u, 64);
+          for (uint32_t k = 64 + lane; k < cj[u]; k += 64) ids[dj[u] + k] = ids_tmp[sj + k];
+        }
+      }
+    }
   }
 }
 
@@ -664,7 +793,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint4* __restrict__ piece
 int walk_grid_blocks(uint32_t n) {
   const uint32_t chunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
   uint32_t blocks = (chunks + WALK_WAVES - 1) / WALK_WAVES;
-  const uint32_t cap = 256 * 8;  // grid-stride beyond ~8 blocks per CU
+  const uint32_t cap = 256 * 32 / WALK_WAVES;  // grid-stride beyond 32 waves per CU
   if (blocks > cap) blocks = cap;
   return blocks ? (int)blocks : 1;
 }

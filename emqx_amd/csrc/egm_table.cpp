@@ -79,7 +79,7 @@ void HostTable::clear() {
   edge_slot_.clear();
   free_nodes_.clear();
   n_live_nodes_ = 0;
-  edges.assign(16 * EDGE_BUCKET, EdgeSlot{NONE, 0, 0, 0});
+  edges.assign(16 * EDGE_BUCKET, EdgeSlot{NONE, 0, 0, 0, NONE, NONE, NONE, 0});
   n_edges_ = n_edge_tombs_ = 0;
   dict.assign(64, DictSlot{0, NONE, 0, {0}});
   dict_blob.clear();
@@ -138,18 +138,18 @@ uint32_t HostTable::own_flags(uint32_t n) const {
          (r.hash_fid != NONE ? F_HASH : 0u) | (r.term_fid != NONE ? F_TERM : 0u);
 }
 
-// Recompute n's flags and publish them where a walker picks them up: the
-// literal edge slot that reaches n, or the parent's record when n is its '+'.
+// Recompute n's flags and republish its record where a walker picks it up:
+// the literal edge slot that reaches n carries a copy (the '+' child and the
+// root are read from nodes[] itself).
 void HostTable::update_flags(uint32_t n) {
-  uint32_t f = own_flags(n);
-  nodes[n].meta = (nodes[n].meta & 0xFu) | (f << 4);
-  uint32_t p = parent_[n];
-  if (p == NONE) return;
-  if (via_[n] == WID_PLUS) {
-    nodes[p].meta = (nodes[p].meta & ~0xFu) | f;
-  } else if (via_[n] < WID_MAX) {
-    edges[edge_slot_[n]].child_flags = f;
-  }
+  NodeRec& r = nodes[n];
+  r.flags = own_flags(n);
+  if (parent_[n] == NONE || via_[n] >= WID_MAX) return;
+  EdgeSlot& s = edges[edge_slot_[n]];
+  s.child_flags = r.flags;
+  s.child_plus = r.plus_child;
+  s.child_hash = r.hash_fid;
+  s.child_term = r.term_fid;
 }
 
 // ---- dictionary ----
@@ -223,7 +223,8 @@ uint32_t HostTable::edge_insert(uint32_t parent, uint32_t wid, uint32_t child, u
       EdgeSlot& s = edges[(size_t)b * EDGE_BUCKET + k];
       if (s.parent == NONE || s.parent == TOMB) {
         if (s.parent == TOMB) --n_edge_tombs_;
-        s = EdgeSlot{parent, wid, child, cflags};
+        const NodeRec& r = nodes[child];
+        s = EdgeSlot{parent, wid, child, cflags, r.plus_child, r.hash_fid, r.term_fid, 0};
         ++n_edges_;
         return (uint32_t)(b * EDGE_BUCKET + k);
       }
@@ -235,7 +236,7 @@ uint32_t HostTable::edge_insert(uint32_t parent, uint32_t wid, uint32_t child, u
 void HostTable::edge_rehash(size_t n_buckets) {
   std::vector<EdgeSlot> old;
   old.swap(edges);
-  edges.assign(n_buckets * EDGE_BUCKET, EdgeSlot{NONE, 0, 0, 0});
+  edges.assign(n_buckets * EDGE_BUCKET, EdgeSlot{NONE, 0, 0, 0, NONE, NONE, NONE, 0});
   n_edges_ = n_edge_tombs_ = 0;
   for (const EdgeSlot& s : old) {
     if (s.parent == NONE || s.parent == TOMB) continue;
@@ -448,7 +449,7 @@ void HostTable::relayout() {
   while (nb * EDGE_BUCKET < (size_t)n_edges_ * 2) nb <<= 1;  // 25-50 % slot load
   std::vector<EdgeSlot> old;
   old.swap(edges);
-  edges.assign(nb * EDGE_BUCKET, EdgeSlot{NONE, 0, 0, 0});
+  edges.assign(nb * EDGE_BUCKET, EdgeSlot{NONE, 0, 0, 0, NONE, NONE, NONE, 0});
   n_edges_ = n_edge_tombs_ = 0;
   // insert in BFS order of the child so that bucket contents follow the levels
   std::vector<EdgeSlot> live;

@@ -259,7 +259,7 @@ class TableImage:
                                          shape=(n,)).copy()
 
         nodes = arr(v.nodes, v.n_nodes * 4, np.uint32).reshape(-1, 4)
-        edges = arr(v.edges, v.n_edge_slots * 4, np.uint32).reshape(-1, 4)
+        edges = arr(v.edges, v.n_edge_slots * 8, np.uint32).reshape(-1, 8)
         dict_ = arr(v.dict, v.n_dict_slots * 8, np.uint32).reshape(-1, 8)
         return {
             "nodes": nodes, "hash_child": arr(v.hash_child, v.n_nodes, np.uint32), "edges": edges,

@@ -151,4 +151,4 @@ def test_image_delete_all_frees_everything():
     a = im.arrays()
     assert a["n_filters"] == 0 and a["n_live_nodes"] == 1 and a["n_edges"] == 0
     root = a["nodes"][0]
-    assert list(root[:3]) == [L.NONE_ID] * 3 and (int(root[3]) >> 4) == 0
+    assert list(root[:3]) == [L.NONE_ID] * 3 and int(root[3]) == 0

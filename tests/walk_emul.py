@@ -3,10 +3,10 @@
 Used only to check, on a machine without a GPU, that the HBM image produced by
 the host table builder (egm_table.cpp, exposed through TableImage) encodes the
 filter set: tokenise -> byte-exact dictionary probe -> edge bucket probe ->
-frontier expansion, exactly as egm_kernels.hip does it.  Not a product path.
+frontier expansion, exactly as egm_kernels.hip does it (items carry their
+node's record; a literal edge slot carries a copy of its child's record).
+Not a product path.
 """
-import numpy as np
-
 NONE = 0xFFFFFFFF
 WID_NONE, WID_PLUS, WID_HASH, WID_MAX = 0xFFFFFFFF, 0xFFFFFFFD, 0xFFFFFFFC, 0xFFFFFFF0
 F_LIT, F_PLUS, F_HASH, F_TERM = 1, 2, 4, 8
@@ -35,16 +35,24 @@ class Emul:
             i = (i + 1) & a["dict_mask"]
 
     def edge(self, node, w):
+        """-> (child, record tuple (plus, hash, term, flags)) or (NONE, None)."""
         a = self.a
         b = self.img.edge_bucket(node, w, a["edge_mask"])
         while True:
             for k in range(4):
                 s = a["edges"][b * 4 + k]
                 if int(s[0]) == node and int(s[1]) == w:
-                    return int(s[2]), int(s[3])
+                    c = int(s[2])
+                    rec = (int(s[4]), int(s[5]), int(s[6]), int(s[3]))
+                    assert rec == self.rec(c), "edge slot's copy of the child record is stale"
+                    return c, rec
                 if int(s[0]) == NONE:
-                    return NONE, 0
+                    return NONE, None
             b = (b + 1) & a["edge_mask"]
+
+    def rec(self, node):
+        r = self.a["nodes"][node]
+        return int(r[0]), int(r[1]), int(r[2]), int(r[3])
 
     def match(self, topic: bytes, mode: int = 0):
         a = self.a
@@ -61,7 +69,6 @@ class Emul:
         dollar = topic[:1] == b"$"
         D = len(ws)
         out = []
-        nodes = a["nodes"]
         if wild:
             if mode == 0:
                 return out
@@ -69,7 +76,7 @@ class Emul:
             for l in range(D):
                 w = wids[l]
                 if w == WID_PLUS:
-                    node = int(nodes[node][0])
+                    node = self.rec(node)[0]
                 elif w == WID_HASH:
                     node = int(a["hash_child"][node])
                 elif w < WID_MAX:
@@ -78,26 +85,25 @@ class Emul:
                     node = NONE
                 if node == NONE:
                     return out
-            if int(nodes[node][2]) != NONE:
-                out.append(int(nodes[node][2]))
+            plus, hsh, term, fl = self.rec(node)
+            if fl & F_TERM:
+                out.append(term)
             return out
-        root_fl = (int(nodes[0][3]) >> 4) & 0xF
-        stack = [(0, 0, root_fl, 0)]
+        stack = [(0, 0, self.rec(0), 0)]
         while stack:
-            node, level, fl, wc = stack.pop()
-            rec = nodes[node]
+            node, level, (plus, hsh, term, fl), wc = stack.pop()
             atend = level == D
             rootd = level == 0 and dollar
             if (fl & F_HASH) and not rootd:
-                out.append(int(rec[1]))
+                out.append(hsh)
             if atend and (fl & F_TERM) and (mode == 1 or wc or (D == 1 and dollar)):
-                out.append(int(rec[2]))
+                out.append(term)
             if atend:
                 continue
             if (fl & F_LIT) and wids[level] < WID_MAX:
-                c, cf = self.edge(node, wids[level])
+                c, r = self.edge(node, wids[level])
                 if c != NONE:
-                    stack.append((c, level + 1, cf, wc))
+                    stack.append((c, level + 1, r, wc))
             if (fl & F_PLUS) and not rootd:
-                stack.append((int(rec[0]), level + 1, int(rec[3]) & 0xF, 1))
+                stack.append((plus, level + 1, self.rec(plus), 1))
         return out
