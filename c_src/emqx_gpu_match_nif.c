@@ -1,0 +1,207 @@
+/*
+ * emqx_gpu_match_nif.c — Erlang NIF shim over libemqx_gpu_match.so.
+ *
+ * Binds the C-ABI in include/emqx_gpu_match.h to the Erlang module
+ * erl/emqx_gpu_match.erl.  Written against the documented erl_nif API; it
+ * compiles only where an ERTS include directory exists (there is none in the
+ * build container: see INTEGRATION.md for the command line).
+ *
+ * Mapping to the reference (EMQ X 5.0-alpha.3):
+ *   open/1          -> egm_open            (one context per node, device ordinal)
+ *   build/2         -> egm_table_build     (bulk load of the route filters)
+ *   apply_delta/3   -> egm_table_apply_delta + egm_table_commit
+ *                      (emqx_trie:insert/1, delete/1 — apps/emqx/src/emqx_trie.erl:82-96)
+ *   match_batch/3   -> egm_match_batch     (emqx_trie:match/1 and the filter set of
+ *                      emqx_router:match_routes/1 — emqx_router.erl:129-141 — for a
+ *                      list of publish topics; returns [[FilterId]])
+ *
+ * Threading: match_batch and apply_delta run on dirty CPU schedulers
+ * (ERL_NIF_DIRTY_JOB_CPU_BOUND) — a batch takes well over 1 ms.  The library
+ * serialises calls per context.  Inputs (Erlang binaries) are borrowed only
+ * for the duration of the call: they are packed into one contiguous buffer
+ * here and the library copies them to device memory before returning.
+ * Errors: bad arguments -> enif_make_badarg (the reference's function_clause);
+ * library / device failures -> {error, Reason} so the caller can fall back to
+ * emqx_trie:match/1.
+ */
+#include <erl_nif.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/emqx_gpu_match.h"
+
+typedef struct {
+  egm_ctx* ctx;
+} egm_res_t;
+
+static ErlNifResourceType* EGM_RES;
+static ERL_NIF_TERM ATOM_OK, ATOM_ERROR;
+
+static void egm_res_dtor(ErlNifEnv* env, void* obj) {
+  (void)env;
+  egm_res_t* r = (egm_res_t*)obj;
+  if (r->ctx) egm_close(r->ctx);
+  r->ctx = NULL;
+}
+
+static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
+  (void)priv;
+  (void)info;
+  EGM_RES = enif_open_resource_type(env, NULL, "emqx_gpu_match_ctx", egm_res_dtor,
+                                    ERL_NIF_RT_CREATE | ERL_NIF_RT_TAKEOVER, NULL);
+  ATOM_OK = enif_make_atom(env, "ok");
+  ATOM_ERROR = enif_make_atom(env, "error");
+  return EGM_RES ? 0 : -1;
+}
+
+static ERL_NIF_TERM error_tuple(ErlNifEnv* env, egm_ctx* ctx, int rc) {
+  const char* msg = ctx ? egm_last_error(ctx) : "egm error";
+  return enif_make_tuple2(env, ATOM_ERROR,
+                          enif_make_tuple2(env, enif_make_int(env, rc), enif_make_string(env, msg, ERL_NIF_LATIN1)));
+}
+
+/* Pack a proper list of binaries into blob + offsets (caller frees). */
+static int pack_list(ErlNifEnv* env, ERL_NIF_TERM list, uint8_t** blob, uint32_t** off, uint32_t* n) {
+  unsigned len;
+  if (!enif_get_list_length(env, list, &len)) return 0;
+  uint32_t* o = (uint32_t*)malloc(((size_t)len + 1) * sizeof(uint32_t));
+  if (!o) return 0;
+  size_t total = 0;
+  ERL_NIF_TERM head, tail = list;
+  ErlNifBinary bin;
+  o[0] = 0;
+  for (unsigned i = 0; i < len; ++i) {
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_inspect_binary(env, head, &bin) ||
+        total + bin.size > 0xFFFFFFFFu) {
+      free(o);
+      return 0;
+    }
+    total += bin.size;
+    o[i + 1] = (uint32_t)total;
+  }
+  uint8_t* b = (uint8_t*)malloc(total + 16);
+  if (!b) {
+    free(o);
+    return 0;
+  }
+  tail = list;
+  for (unsigned i = 0; i < len; ++i) {
+    enif_get_list_cell(env, tail, &head, &tail);
+    enif_inspect_binary(env, head, &bin);
+    memcpy(b + o[i], bin.data, bin.size);
+  }
+  *blob = b;
+  *off = o;
+  *n = len;
+  return 1;
+}
+
+static int get_ctx(ErlNifEnv* env, ERL_NIF_TERM t, egm_res_t** r) {
+  return enif_get_resource(env, t, EGM_RES, (void**)r) && (*r)->ctx;
+}
+
+/* open(Device :: non_neg_integer()) -> {ok, Ctx} | {error, _} */
+static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  int dev;
+  if (argc != 1 || !enif_get_int(env, argv[0], &dev) || dev < 0) return enif_make_badarg(env);
+  egm_config cfg = {dev, 1, 0, 1000};
+  egm_ctx* ctx = NULL;
+  int rc = egm_open(&cfg, &ctx);
+  if (rc) return error_tuple(env, NULL, rc);
+  egm_res_t* r = (egm_res_t*)enif_alloc_resource(EGM_RES, sizeof(egm_res_t));
+  r->ctx = ctx;
+  ERL_NIF_TERM term = enif_make_resource(env, r);
+  enif_release_resource(r);
+  return enif_make_tuple2(env, ATOM_OK, term);
+}
+
+/* build(Ctx, [Filter :: binary()]) -> ok | {error, _}   (ids = list positions) */
+static ERL_NIF_TERM nif_build(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  egm_res_t* r;
+  uint8_t* blob;
+  uint32_t *off, n;
+  if (argc != 2 || !get_ctx(env, argv[0], &r) || !pack_list(env, argv[1], &blob, &off, &n))
+    return enif_make_badarg(env);
+  int rc = egm_table_build(r->ctx, blob, off, n, NULL);
+  free(blob);
+  free(off);
+  return rc ? error_tuple(env, r->ctx, rc) : ATOM_OK;
+}
+
+/* apply_delta(Ctx, [{Filter, Id}] inserts, [Filter] deletes) -> {ok, Epoch} | {error, _} */
+static ERL_NIF_TERM nif_apply_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  egm_res_t* r;
+  if (argc != 3 || !get_ctx(env, argv[0], &r)) return enif_make_badarg(env);
+  unsigned ni;
+  if (!enif_get_list_length(env, argv[1], &ni)) return enif_make_badarg(env);
+  ERL_NIF_TERM filters = enif_make_list(env, 0), head, tail = argv[1];
+  uint32_t* ids = (uint32_t*)malloc(((size_t)ni + 1) * sizeof(uint32_t));
+  for (unsigned i = 0; i < ni; ++i) {
+    const ERL_NIF_TERM* tup;
+    int arity;
+    unsigned id;
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_tuple(env, head, &arity, &tup) || arity != 2 ||
+        !enif_get_uint(env, tup[1], &id)) {
+      free(ids);
+      return enif_make_badarg(env);
+    }
+    ids[i] = id;
+    filters = enif_make_list_cell(env, tup[0], filters);
+  }
+  ERL_NIF_TERM rev;
+  enif_make_reverse_list(env, filters, &rev);
+  uint8_t *ib = NULL, *db = NULL;
+  uint32_t *io = NULL, *dof = NULL, nin = 0, nd = 0;
+  if (!pack_list(env, rev, &ib, &io, &nin) || !pack_list(env, argv[2], &db, &dof, &nd)) {
+    free(ids);
+    free(ib);
+    free(io);
+    return enif_make_badarg(env);
+  }
+  egm_delta ins = {ib, io, nin, ids}, del = {db, dof, nd, NULL};
+  uint64_t epoch = 0;
+  int rc = egm_table_apply_delta(r->ctx, &ins, &del);
+  if (!rc) rc = egm_table_commit(r->ctx, &epoch);
+  free(ids);
+  free(ib);
+  free(io);
+  free(db);
+  free(dof);
+  if (rc) return error_tuple(env, r->ctx, rc);
+  return enif_make_tuple2(env, ATOM_OK, enif_make_uint64(env, epoch));
+}
+
+/* match_batch(Ctx, [Topic :: binary()], Mode :: 0 | 1) -> {ok, [[Id]]} | {error, _} */
+static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  egm_res_t* r;
+  int mode;
+  uint8_t* blob;
+  uint32_t *off, n;
+  if (argc != 3 || !get_ctx(env, argv[0], &r) || !enif_get_int(env, argv[2], &mode) ||
+      (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES) || !pack_list(env, argv[1], &blob, &off, &n))
+    return enif_make_badarg(env);
+  egm_result* res = NULL;
+  int rc = egm_match_batch(r->ctx, blob, off, n, mode, &res);
+  free(blob);
+  free(off);
+  if (rc && !res) return error_tuple(env, r->ctx, rc);
+  ERL_NIF_TERM rows = enif_make_list(env, 0);
+  for (uint32_t i = n; i-- > 0;) {
+    ERL_NIF_TERM row = enif_make_list(env, 0);
+    for (uint64_t k = res->row_ptr[i + 1]; k-- > res->row_ptr[i];)
+      row = enif_make_list_cell(env, enif_make_uint(env, res->ids[k]), row);
+    rows = enif_make_list_cell(env, row, rows);
+  }
+  egm_result_free(res);
+  if (rc) return error_tuple(env, r->ctx, rc);
+  return enif_make_tuple2(env, ATOM_OK, rows);
+}
+
+static ErlNifFunc nif_funcs[] = {
+    {"open", 1, nif_open, 0},
+    {"build", 2, nif_build, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"apply_delta", 3, nif_apply_delta, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"match_batch", 3, nif_match_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+};
+
+ERL_NIF_INIT(emqx_gpu_match, nif_funcs, load, NULL, NULL, NULL)

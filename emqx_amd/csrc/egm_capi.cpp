@@ -79,8 +79,8 @@ struct egm_ctx {
   std::string err;
 
   // per-batch workspace
-  DevBuf wid, lv, tfl, off_tmp, cnt, ids_tmp, pieces, deferred, tile_sums, stats;
-  uint64_t pieces_cap = 0;
+  DevBuf wid, lv, tfl, cnt, ids_tmp, pieces, deferred, tile_sums, stats;
+  uint64_t pieces_cap = 0, ids_tmp_cap = 0;
   DevBuf in_blob, in_off, out_row, out_ids;
   uint32_t heavy_waves = 256;
   uint32_t debug = 0;
@@ -186,13 +186,13 @@ static int ensure_work(egm_ctx* c, uint32_t n, uint64_t blob_bytes, uint64_t ids
   if ((e = c->wid.ensure((blob_bytes + nn) * 4)) != hipSuccess) return c->hip_fail(e, "wid");
   if ((e = c->lv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "lv");
   if ((e = c->tfl.ensure(nn)) != hipSuccess) return c->hip_fail(e, "tfl");
-  if ((e = c->off_tmp.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "off_tmp");
   if ((e = c->cnt.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "cnt");
-  if ((e = c->ids_tmp.ensure((ids_cap + 1) * 4)) != hipSuccess) return c->hip_fail(e, "ids_tmp");
-  // a piece holds >= 1 id; typical batches use ~1.2 pieces per topic
-  uint64_t pcap = std::max<uint64_t>(nn * 2 + 4096, ids_cap / 4);
-  if (pcap > ids_cap + nn) pcap = ids_cap + nn;
-  if ((e = c->pieces.ensure(pcap * 16)) != hipSuccess) return c->hip_fail(e, "pieces");
+  // chunk-ordered ids and their pieces, plus the slack of per-wave slabs
+  const uint64_t tcap = ids_tmp_capacity(ids_cap, n);
+  if (tcap >= 0xFFFFFFF0ull) return c->fail(EGM_E_INVAL, "batch too large: > 4G matched ids (split it)");
+  if ((e = c->ids_tmp.ensure(tcap * 4)) != hipSuccess) return c->hip_fail(e, "ids_tmp");
+  c->ids_tmp_cap = c->ids_tmp.cap / 4;
+  if ((e = c->pieces.ensure(pieces_capacity(ids_cap, n) * 16)) != hipSuccess) return c->hip_fail(e, "pieces");
   c->pieces_cap = c->pieces.cap / 16;
   if ((e = c->deferred.ensure((n / WALK_CHUNK + 2) * 4)) != hipSuccess) return c->hip_fail(e, "deferred");
   if ((e = c->tile_sums.ensure((scan_tiles(n) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "tile_sums");
@@ -205,10 +205,10 @@ static MatchWork work_view(egm_ctx* c, uint64_t ids_cap) {
   w.wid = c->wid.as<uint32_t>();
   w.lv = c->lv.as<uint32_t>();
   w.tfl = c->tfl.as<uint8_t>();
-  w.off_tmp = c->off_tmp.as<uint64_t>();
   w.cnt = c->cnt.as<uint32_t>();
   w.ids_tmp = c->ids_tmp.as<uint32_t>();
-  w.ids_cap = ids_cap;
+  w.ids_cap = c->ids_tmp_cap;   // ids_tmp entries (the output capacity is MatchOut's)
+  (void)ids_cap;
   w.pieces = c->pieces.as<uint4>();
   w.pieces_cap = c->pieces_cap;
   w.deferred = c->deferred.as<uint32_t>();
@@ -402,7 +402,7 @@ int egm_last_stats(egm_ctx* c, uint64_t* n_ids, uint64_t* visited, uint32_t* n_d
   std::lock_guard<std::recursive_mutex> g(c->mu);
   int r = sync_last(c);
   if (r) return r;
-  if (n_ids) *n_ids = c->last.cursor;
+  if (n_ids) *n_ids = c->last.total_ids;
   if (visited) *visited = c->last.visited;
   if (n_def) *n_def = c->last.n_deferred;
   if (overflow) *overflow = c->last.overflow;
@@ -460,8 +460,7 @@ int egm_match_batch(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32
       hipSuccess)
     return c->hip_fail(e, "H2D offsets");
   std::shared_ptr<Epoch> ep = c->cur;
-  uint64_t cap = (uint64_t)n * 4 + 1024;
-  if (c->ids_tmp.cap / 4 > cap + 1) cap = c->ids_tmp.cap / 4 - 1;
+  uint64_t cap = std::max<uint64_t>((uint64_t)n * 4 + 1024, c->out_ids.cap / 4);
   for (int attempt = 0; attempt < 3; ++attempt) {
     int r = ensure_work(c, n, bytes, cap);
     if (r) return r;
@@ -473,10 +472,10 @@ int egm_match_batch(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32
     r = sync_last(c);
     if (r) return r;
     if (!c->last.overflow) break;
-    cap = c->last.cursor + 1024;
+    cap = c->last.total_ids + c->last.total_ids / 8 + 1024;   // exact total is known even on overflow
     if (attempt == 2) return c->fail(EGM_E_NOMEM, "ids capacity");
   }
-  const uint64_t nids = c->last.cursor;
+  const uint64_t nids = c->last.total_ids;
   // one allocation: struct + arrays (egm_result_free == free)
   size_t sz = sizeof(egm_result);
   size_t o_counts = sz;

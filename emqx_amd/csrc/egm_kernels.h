@@ -20,25 +20,32 @@ struct DevTable {                 // one epoch of the filter graph in HBM
 };
 
 struct MatchStats {               // device-side counters, zeroed per batch
-  unsigned long long cursor;      // ids reserved in ids_tmp
+  unsigned long long cursor;      // ids_tmp entries reserved (slabs, incl. slack)
   unsigned long long visited;     // NFA states expanded (light + heavy)
-  unsigned long long pieces;      // pieces reserved
+  unsigned long long pieces;      // pieces reserved (slabs, incl. slack)
+  unsigned long long total_ids;   // matched ids in the batch (= row_ptr[n])
   unsigned int n_deferred;        // chunks handed to the heavy kernel
   unsigned int heavy_next;        // heavy work counter
-  unsigned int overflow;          // ids_tmp / pieces capacity exceeded
+  unsigned int overflow;          // bit 0: ids_tmp/pieces full, bit 1: output ids full
   unsigned int errors;            // topics the heavy kernel could not finish
 };
 
 // A piece is one flush's run of a topic's ids in ids_tmp:
-// {topic, count | HEAVY_PIECE, offset lo, offset hi}.  CSR rows are assembled
-// from pieces; light-walk pieces of a topic later re-run by k_heavy are ignored.
+// {topic, count | HEAVY_PIECE, ids_tmp offset, offset inside the topic's row}.
+// CSR rows are assembled from pieces without atomics; light-walk pieces of a
+// topic later re-run by k_heavy are ignored; count 0 marks an unused slot.
 constexpr uint32_t HEAVY_PIECE = 0x80000000u;
+
+// Each wave reserves its output space in slabs (one device-scope atomic per
+// slab): a single shared counter bumped per flush serialises across the 8
+// XCDs at the memory side.
+constexpr uint32_t SLAB_IDS = 4096;
+constexpr uint32_t SLAB_PIECES = 256;
 
 struct MatchWork {                // per-batch device workspace
   uint32_t* wid;                  // [blob_bytes + n] word ids, topic t at off[t] + t
   uint32_t* lv;                   // [n] levels
   uint8_t* tfl;                   // [n] TF_* flags
-  uint64_t* off_tmp;              // [n] start of topic t's ids in ids_tmp
   uint32_t* cnt;                  // [n] number of ids of topic t
   uint32_t* ids_tmp;              // [ids_cap] chunk-ordered ids
   uint64_t ids_cap;
@@ -67,7 +74,17 @@ struct MatchOut {                 // CSR result (device)
 #endif
 constexpr int WALK_CHUNK = EGM_WALK_CHUNK;
 int walk_grid_blocks(uint32_t n_topics);
+int walk_waves_per_block();
 size_t scan_tiles(uint32_t n);
+// ids_tmp / pieces capacity a batch needs beyond its matched ids: slab tails
+inline uint64_t ids_tmp_capacity(uint64_t ids, uint32_t n) {
+  return ids + ids / 4 + (uint64_t)(walk_grid_blocks(n) * walk_waves_per_block() + 256) * SLAB_IDS;
+}
+inline uint64_t pieces_capacity(uint64_t ids, uint32_t n) {
+  uint64_t p = 2ull * n + 4096;
+  if (ids / 2 > p) p = ids / 2;
+  return p + (uint64_t)(walk_grid_blocks(n) * walk_waves_per_block() + 256) * SLAB_PIECES;
+}
 
 // Timing hooks: when ev != nullptr, ev[0]/ev[1] bracket the walk kernel.
 hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n,

@@ -315,13 +315,42 @@ struct alignas(16) WaveLds {
   uint8_t stage_t[WALK_STAGE];
 };
 
-__device__ __forceinline__ uint4 mk_piece(uint32_t t, uint32_t count, unsigned long long off) {
-  return make_uint4(t, count, (uint32_t)off, (uint32_t)(off >> 32));
+__device__ __forceinline__ uint4 mk_piece(uint32_t t, uint32_t count, uint32_t src, uint32_t row_off) {
+  return make_uint4(t, count, src, row_off);
 }
 
-// Write the stage out: one atomic reservation of ids and of pieces, per-topic
-// runs by counting sort in LDS, one piece per topic present.
-__device__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane, const MatchWork& w) {
+// Per-wave output slab (uniform across the wave).
+struct Slab {
+  unsigned long long cur, end;
+};
+
+// Take `need` entries from the wave's slab, reserving a new slab of at least
+// `grain` entries (one device-scope atomic) when the current one is short.
+// The unused tail of an abandoned pieces slab is marked empty (count 0).
+__device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, uint32_t grain,
+                                                        unsigned long long* counter, uint32_t lane,
+                                                        uint4* tail_fill, unsigned long long tail_cap) {
+  if (s.cur + need > s.end) {
+    if (tail_fill)
+      for (unsigned long long i = s.cur + lane; i < s.end && i < tail_cap; i += 64)
+        tail_fill[i] = make_uint4(NONE, 0, 0, 0);
+    const unsigned long long sz = need > grain ? need : grain;
+    unsigned long long b = 0;
+    if (lane == 0) b = atomicAdd(counter, sz);
+    b = __shfl(b, 0, 64);
+    s.cur = b;
+    s.end = b + sz;
+  }
+  const unsigned long long r = s.cur;
+  s.cur += need;
+  return r;
+}
+
+// Write the stage out: ids and pieces from the wave's slabs, per-topic runs by
+// counting sort in LDS, one piece per topic present carrying the topic's
+// running count as its offset inside the CSR row.
+__device__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane, const MatchWork& w,
+                            Slab& sid, Slab& spc) {
   constexpr int PER = WALK_CHUNK / 64;
   uint32_t fl[PER];
   uint32_t s = 0, np = 0;
@@ -334,19 +363,15 @@ __device__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t l
   uint32_t tot, ptot;
   uint32_t ex = wave_excl_scan(s, lane, &tot);
   uint32_t pex = wave_excl_scan(np, lane, &ptot);
-  unsigned long long base = 0, pbase = 0;
-  if (lane == 0) {
-    base = atomicAdd(&w.stats->cursor, (unsigned long long)tot);
-    pbase = atomicAdd(&w.stats->pieces, (unsigned long long)ptot);
-  }
-  base = __shfl(base, 0, 64);
-  pbase = __shfl(pbase, 0, 64);
+  const unsigned long long base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
+  const unsigned long long pbase =
+      slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
   const bool ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
   if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const uint32_t j = lane * PER + k;
-    if (fl[k] && ok) w.pieces[pbase + pex++] = mk_piece(t0 + j, fl[k], base + ex);
+    if (fl[k] && ok) w.pieces[pbase + pex++] = mk_piece(t0 + j, fl[k], (uint32_t)(base + ex), L.cnt[j]);
     L.fcnt[j] = ex;   // becomes the scatter cursor
     L.cnt[j] += fl[k];
     ex += fl[k];
@@ -374,6 +399,7 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
   const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
   const uint4 root = ld16(tab.nodes);
   uint64_t visited = 0;
+  Slab sid{0, 0}, spc{0, 0};
 
   for (uint32_t c = blockIdx.x * WALK_WAVES + wave; c < nchunks; c += nwaves) {
     const uint32_t t0 = c * WALK_CHUNK;
@@ -507,7 +533,7 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
       const uint32_t n0 = popc(b0), ne = n0 + popc(b1);
       if (nstage + ne > (uint32_t)WALK_STAGE) {
         wave_sync();
-        flush_stage(L, nstage, t0, lane, w);
+        flush_stage(L, nstage, t0, lane, w, sid, spc);
         nstage = 0;
       }
       if (x.h0) {
@@ -537,10 +563,12 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
       wave_sync();
       continue;
     }
-    if (nstage) flush_stage(L, nstage, t0, lane, w);
+    if (nstage) flush_stage(L, nstage, t0, lane, w, sid, spc);
     for (uint32_t j = lane; j < nt; j += 64) w.cnt[t0 + j] = L.cnt[j];
     wave_sync();
   }
+  for (unsigned long long i = spc.cur + lane; i < spc.end && i < w.pieces_cap; i += 64)
+    w.pieces[i] = make_uint4(NONE, 0, 0, 0);   // unused tail of the last pieces slab
   if (lane == 0 && visited) atomicAdd(&w.stats->visited, (unsigned long long)visited);
 }
 
@@ -648,7 +676,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
         w.tfl[t] = (uint8_t)(tf | TF_HEAVY | TF_ERROR);
       } else {
         w.cnt[t] = count;
-        if (count && fits) w.pieces[pbase] = mk_piece(t, count | HEAVY_PIECE, base);
+        if (count && fits) w.pieces[pbase] = mk_piece(t, count | HEAVY_PIECE, (uint32_t)base, 0);
         w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
       }
     }
@@ -732,60 +760,38 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
   if (blockIdx.x == 0 && threadIdx.x == 0) row_ptr[n] = tile_sums[ntiles];
 }
 
-// pieces -> CSR rows.  cursor[t] starts at row_ptr[t]; each valid piece takes
-// its slot with one atomic (pieces of one topic may land in any order: a row
-// is a set).  Light pieces of topics re-run by k_heavy are ignored.
+// pieces -> CSR rows, no atomics: a piece knows its offset inside the row.
+// One lane per piece, four independent loads in flight per lane.  Light
+// pieces of topics re-run by k_heavy and unused slab slots are skipped.
 __global__ __launch_bounds__(256) void k_compact(const uint4* __restrict__ pieces, const uint8_t* __restrict__ tfl,
                                                  const uint32_t* __restrict__ ids_tmp, uint32_t n,
-                                                 const uint64_t* __restrict__ row_ptr,
-                                                 unsigned long long* __restrict__ cursor, uint32_t* __restrict__ ids,
-                                                 uint64_t ids_cap, MatchStats* stats) {
+                                                 const uint64_t* __restrict__ row_ptr, uint32_t* __restrict__ ids,
+                                                 uint64_t ids_cap, uint64_t pieces_cap, MatchStats* stats) {
+  const uint64_t total = row_ptr[n];
+  if (blockIdx.x == 0 && threadIdx.x == 0) stats->total_ids = total;
   if (stats->overflow) return;
-  if (row_ptr[n] > ids_cap) {
+  if (total > ids_cap) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, 2u);
     return;
   }
-  // one wave handles 64 consecutive pieces: every lane claims one piece's
-  // destination, then the wave copies the pieces one after another with
-  // coalesced 64-lane loads/stores, eight pieces' loads in flight at a time
-  const uint64_t np = stats->pieces;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  for (uint64_t b0 = wave * 64; b0 < np; b0 += nwaves * 64) {
-    const uint64_t i = b0 + lane;
-    uint32_t c = 0;
-    uint64_t s = 0, d = 0;
-    if (i < np) {
-      const uint4 pc = pieces[i];
-      const uint32_t t = pc.x;
-      const bool heavy = (pc.y & HEAVY_PIECE) != 0;
-      if (!((tfl[t] & TF_HEAVY) && !heavy)) {
-        c = pc.y & ~HEAVY_PIECE;
-        s = (uint64_t)pc.z | ((uint64_t)pc.w << 32);
-        d = atomicAdd(&cursor[t], (unsigned long long)c);
-      }
+  const uint64_t np = min((uint64_t)stats->pieces, pieces_cap);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < np; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4 pc = pieces[i];
+    const uint32_t c = pc.y & ~HEAVY_PIECE;
+    if (c == 0) continue;
+    const uint32_t t = pc.x;
+    if ((tfl[t] & TF_HEAVY) && !(pc.y & HEAVY_PIECE)) continue;
+    const uint32_t* src = ids_tmp + pc.z;
+    uint32_t* dst = ids + row_ptr[t] + pc.w;
+    uint32_t k = 0;
+    for (; k + 4 <= c; k += 4) {
+      const uint32_t a0 = src[k], a1 = src[k + 1], a2 = src[k + 2], a3 = src[k + 3];
+      dst[k] = a0;
+      dst[k + 1] = a1;
+      dst[k + 2] = a2;
+      dst[k + 3] = a3;
     }
-#pragma unroll 1
-    for (int j0 = 0; j0 < 64; j0 += 8) {
-      uint32_t v[8], cj[8];
-      uint64_t dj[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        cj[u] = __shfl(c, j0 + u, 64);
-        const uint64_t sj = __shfl(s, j0 + u, 64);
-        dj[u] = __shfl(d, j0 + u, 64);
-        v[u] = lane < cj[u] ? ids_tmp[sj + lane] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (lane < cj[u]) ids[dj[u] + lane] = v[u];
-        if (cj[u] > 64u) {  // long pieces: the rest in 64-wide strides
-          const uint64_t sj = __shfl(s, j0 + u, 64);
-          for (uint32_t k = 64 + lane; k < cj[u]; k += 64) ids[dj[u] + k] = ids_tmp[sj + k];
-        }
-      }
-    }
+    for (; k < c; ++k) dst[k] = src[k];
   }
 }
 
@@ -797,6 +803,8 @@ int walk_grid_blocks(uint32_t n) {
   if (blocks > cap) blocks = cap;
   return blocks ? (int)blocks : 1;
 }
+
+int walk_waves_per_block() { return WALK_WAVES; }
 
 size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
@@ -823,9 +831,9 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64 * WALK_WAVES), 0, s, tab, off, n, mode, w);
   if (ev_walk) hipEventRecord(ev_walk[1], s);
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
-  scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s, w.off_tmp);
-  hipLaunchKernelGGL(k_compact, dim3(min((n + 255) / 256 + 1, 8192u)), dim3(256), 0, s, w.pieces, w.tfl, w.ids_tmp,
-                     n, out.row_ptr, (unsigned long long*)w.off_tmp, out.ids, out.ids_cap, w.stats);
+  scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);
+  hipLaunchKernelGGL(k_compact, dim3(8192), dim3(256), 0, s, w.pieces, w.tfl, w.ids_tmp, n, out.row_ptr, out.ids,
+                     out.ids_cap, w.pieces_cap, w.stats);
   return hipGetLastError();
 }
 

@@ -1,0 +1,89 @@
+%%--------------------------------------------------------------------
+%% emqx_gpu_match — Erlang side of the MI355X route lookup (NIF wrapper).
+%%
+%% A drop-in behind emqx_router:match_routes/1 and emqx_trie:match/1
+%% (EMQ X 5.0-alpha.3: apps/emqx/src/emqx_router.erl:129-141,
+%% apps/emqx/src/emqx_trie.erl:100-114).  Filters are identified by dense
+%% integer ids assigned here in insertion order; the id -> filter binary map
+%% lives in an ETS set so match results translate back to the [binary()] the
+%% reference returns.  Every NIF failure returns {error, _} and the callers
+%% below fall back to the reference implementation, so semantics never change.
+%%
+%% Not compiled in this repository's CI (no ERTS in the build image); see
+%% INTEGRATION.md for the build line and for the batching process that turns
+%% per-message publish calls into GPU batches.
+%%--------------------------------------------------------------------
+-module(emqx_gpu_match).
+
+-export([open/1, build/2, apply_delta/3, match_batch/3]).
+-export([init/0, insert/1, delete/1, match/1, match_routes/1]).
+
+-on_load(load_nif/0).
+
+-define(TAB, emqx_gpu_match_ids).        %% Id -> Filter and {filter, Filter} -> Id
+-define(MODE_TRIE, 0).
+-define(MODE_ROUTES, 1).
+
+load_nif() ->
+    Dir = case code:priv_dir(emqx) of
+              {error, _} -> "priv";
+              P -> P
+          end,
+    erlang:load_nif(filename:join(Dir, "emqx_gpu_match_nif"), 0).
+
+%% NIF stubs (replaced on load)
+open(_Device) -> erlang:nif_error(nif_not_loaded).
+build(_Ctx, _Filters) -> erlang:nif_error(nif_not_loaded).
+apply_delta(_Ctx, _Inserts, _Deletes) -> erlang:nif_error(nif_not_loaded).
+match_batch(_Ctx, _Topics, _Mode) -> erlang:nif_error(nif_not_loaded).
+
+%% ---------------------------------------------------------------------
+%% emqx_trie-shaped API
+%% ---------------------------------------------------------------------
+
+init() ->
+    _ = ets:new(?TAB, [named_table, public, set, {read_concurrency, true}]),
+    {ok, Ctx} = open(0),
+    persistent_term:put(?MODULE, Ctx),
+    ets:insert(?TAB, {next_id, 0}),
+    ok.
+
+ctx() -> persistent_term:get(?MODULE).
+
+%% emqx_trie:insert/1 — idempotent (emqx_trie.erl:82-87)
+insert(Filter) when is_binary(Filter) ->
+    case ets:lookup(?TAB, {filter, Filter}) of
+        [_] -> ok;
+        [] ->
+            Id = ets:update_counter(?TAB, next_id, 1) - 1,
+            ets:insert(?TAB, [{Id, Filter}, {{filter, Filter}, Id}]),
+            {ok, _Epoch} = apply_delta(ctx(), [{Filter, Id}], []),
+            ok
+    end.
+
+%% emqx_trie:delete/1 — no-op when absent (emqx_trie.erl:91-96)
+delete(Filter) when is_binary(Filter) ->
+    case ets:lookup(?TAB, {filter, Filter}) of
+        [] -> ok;
+        [{_, Id}] ->
+            {ok, _Epoch} = apply_delta(ctx(), [], [Filter]),
+            ets:delete(?TAB, Id),
+            ets:delete(?TAB, {filter, Filter}),
+            ok
+    end.
+
+%% emqx_trie:match/1 — one topic; production callers go through the batcher
+match(Topic) when is_binary(Topic) ->
+    case match_batch(ctx(), [Topic], ?MODE_TRIE) of
+        {ok, [Ids]} -> [ets:lookup_element(?TAB, Id, 2) || Id <- Ids];
+        {error, _} -> emqx_trie:match(Topic)
+    end.
+
+%% The filter set of emqx_router:match_routes/1 (exact ∪ wildcard); the
+%% router expands each filter to its #route{} entries with lookup_routes/1.
+match_routes(Topic) when is_binary(Topic) ->
+    case match_batch(ctx(), [Topic], ?MODE_ROUTES) of
+        {ok, [Ids]} ->
+            lists:append([emqx_router:lookup_routes(ets:lookup_element(?TAB, Id, 2)) || Id <- Ids]);
+        {error, _} -> emqx_router:match_routes(Topic)
+    end.
