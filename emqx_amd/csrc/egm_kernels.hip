@@ -41,6 +41,10 @@ constexpr int WALK_STACK = EGM_WALK_STACK;
 #define EGM_WALK_STAGE 512   // staged matches per flush
 #endif
 constexpr int WALK_STAGE = EGM_WALK_STAGE;
+#ifndef EGM_WALK_IPL
+#define EGM_WALK_IPL 1   // work items per lane per iteration
+#endif
+constexpr int WALK_IPL = EGM_WALK_IPL;
 #ifndef EGM_WALK_WORDS
 #define EGM_WALK_WORDS 1024   // staged topic word ids per wave chunk
 #endif
@@ -88,6 +92,23 @@ __device__ __forceinline__ uint32_t mk_meta(uint32_t level, uint32_t t, uint32_t
 
 __device__ __forceinline__ uint4 ld16(const void* p) { return *(const uint4*)p; }
 
+// EGM_FOR_U(stmts): run stmts once per work item of a lane with a constant
+// index u (WALK_IPL <= 2).  A macro, not a lambda: arrays of per-item state
+// indexed by constants then stay in registers (a lambda capturing them by
+// reference made LLVM keep them in scratch).
+#define EGM_FOR_U(...)                                 \
+  do {                                                 \
+    {                                                  \
+      constexpr int u = 0;                             \
+      __VA_ARGS__                                      \
+    }                                                  \
+    if constexpr (WALK_IPL > 1) {                      \
+      constexpr int u = WALK_IPL > 1 ? 1 : 0;          \
+      __VA_ARGS__                                      \
+    }                                                  \
+  } while (0)
+static_assert(WALK_IPL == 1 || WALK_IPL == 2, "WALK_IPL");
+
 // ------------------------------------------------------------ dictionary ----
 __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t k) {
   uint32_t w = (k < 8) ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
@@ -99,12 +120,12 @@ __device__ uint32_t dict_probe(const DevTable& tab, uint64_t h, const uint8_t* p
   uint32_t i = (uint32_t)h & tab.dict_mask;
   for (;;) {
     const uint8_t* sp = (const uint8_t*)(tab.dict + i);
-    uint4 a = ld16(sp);  // {hash lo, hash hi, wid, len}
+    const uint4 a = ld16(sp);       // {hash lo, hash hi, wid, len}
+    const uint4 b = ld16(sp + 16);  // inline bytes: same 32 B slot, same round trip
     if (a.z == NONE) return WID_NONE;
     if (a.x == (uint32_t)h && a.y == (uint32_t)(h >> 32) && a.w == len) {
       bool eq = true;
       if (len <= 16) {
-        uint4 b = ld16(sp + 16);
         for (uint32_t k = 0; k < len; ++k) eq &= byte_of(b, k) == p[k];
       } else {
         const uint8_t* q = tab.dict_blob + tab.dict_off[a.z];
@@ -349,7 +370,8 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
 // Write the stage out: ids and pieces from the wave's slabs, per-topic runs by
 // counting sort in LDS, one piece per topic present carrying the topic's
 // running count as its offset inside the CSR row.
-__device__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane, const MatchWork& w,
+__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane,
+                                            const MatchWork& w,
                             Slab& sid, Slab& spc) {
   constexpr int PER = WALK_CHUNK / 64;
   uint32_t fl[PER];
@@ -390,6 +412,104 @@ __device__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t l
   wave_sync();
 }
 
+// Two-phase item processing: issue() starts every global read an item needs
+// (the '+' child's record and the first two slots of the literal bucket),
+// finish() consumes them.  A wave issues the reads of all its items before it
+// waits on any, so each lane keeps WALK_IPL dependent chains in flight.
+struct Pend {
+  Item it;
+  uint32_t D, tf, w, b;
+  bool act, lit, plus;
+  uint4 prec, l0, h0, l1, h1;
+};
+
+__device__ __forceinline__ void issue(const DevTable& tab, Pend& p) {
+  const uint32_t meta = p.it.a.y;
+  const uint32_t level = meta & 0x1FFFFu, fl = (meta >> 25) & 0xFu, ex = (meta >> 30) & 1u;
+  const bool atend = level == p.D;
+  const bool rootd = (level == 0) && (p.tf & TF_DOLLAR);
+  p.plus = p.act && !ex && !atend && (fl & F_PLUS) && !rootd;
+  p.lit = p.act && !ex && !atend && (fl & F_LIT) && p.w < WID_MAX;
+  if (p.plus) p.prec = ld16(tab.nodes + p.it.a.z);
+  if (p.lit) {
+    p.b = edge_bucket(p.it.a.x, p.w, tab.edge_mask);
+    const uint8_t* bp = (const uint8_t*)(tab.edges + (size_t)p.b * EDGE_BUCKET);
+    p.l0 = ld16(bp);
+    p.h0 = ld16(bp + 16);
+    p.l1 = ld16(bp + 32);
+    p.h1 = ld16(bp + 48);
+  }
+}
+
+// continue a bucket probe at slot k0 of bucket b (rare: first two slots busy)
+__device__ __forceinline__ bool edge_probe_from(const DevTable& tab, uint32_t b, int k0, uint32_t node, uint32_t w,
+                                                uint4* lo_out,
+                                uint4* hi_out) {
+  for (;;) {
+    const EdgeSlot* bp = tab.edges + (size_t)b * EDGE_BUCKET;
+    for (int k = k0; k < EDGE_BUCKET; ++k) {
+      const uint4 lo = ld16(bp + k);
+      const uint4 hi = ld16((const uint8_t*)(bp + k) + 16);
+      if (lo.x == node && lo.y == w) {
+        *lo_out = lo;
+        *hi_out = hi;
+        return true;
+      }
+      if (lo.x == NONE) return false;
+    }
+    k0 = 0;
+    b = (b + 1) & tab.edge_mask;
+  }
+}
+
+__device__ __forceinline__ void finish(const DevTable& tab, int mode, Pend& p, Expand& x) {
+  x.h0 = x.h1 = x.hc0 = x.hc1 = false;
+  if (!p.act) return;
+  const Item& it = p.it;
+  const uint32_t meta = it.a.y;
+  if ((meta >> 30) & 1u) {  // exact walk of a wildcard topic (ROUTES mode): rare
+    expand(tab, mode, it, p.D, p.tf, p.w, x);
+    return;
+  }
+  const uint32_t level = meta & 0x1FFFFu, tm = meta & (0xFFu << 17);
+  const uint32_t fl = (meta >> 25) & 0xFu, wc = (meta >> 29) & 1u;
+  const bool atend = level == p.D;
+  const bool rootd = (level == 0) && (p.tf & TF_DOLLAR);
+  const uint32_t nmeta = (level + 1) | tm;
+  x.e0 = it.a.w;
+  x.e1 = it.term;
+  x.h0 = (fl & F_HASH) && !rootd;
+  x.h1 = atend && (fl & F_TERM) && (mode == MODE_ROUTES || wc || (p.D == 1 && (p.tf & TF_DOLLAR)));
+  if (p.lit) {
+    // pick the matching slot's fields with masks, not a select of the two
+    // loaded slots: LLVM folds the latter into a phi of addresses into the
+    // per-item array and then keeps that array in scratch
+    const uint32_t node = it.a.x;
+    const bool m0 = p.l0.x == node && p.l0.y == p.w;
+    const bool e0 = p.l0.x == NONE;
+    const bool m1 = !m0 && !e0 && p.l1.x == node && p.l1.y == p.w;
+    const bool e1 = p.l1.x == NONE;
+    const uint32_t s1 = m1 ? 0xFFFFFFFFu : 0u;
+    uint32_t cz = (p.l0.z & ~s1) | (p.l1.z & s1), cw = (p.l0.w & ~s1) | (p.l1.w & s1);
+    uint32_t hx = (p.h0.x & ~s1) | (p.h1.x & s1), hy = (p.h0.y & ~s1) | (p.h1.y & s1);
+    uint32_t hz = (p.h0.z & ~s1) | (p.h1.z & s1);
+    bool found = m0 || m1;
+    if (!m0 && !e0 && !m1 && !e1) {   // both first slots busy with other keys: keep probing
+      uint4 lo, hi;
+      found = edge_probe_from(tab, p.b, 2, node, p.w, &lo, &hi);
+      cz = lo.z;
+      cw = lo.w;
+      hx = hi.x;
+      hy = hi.y;
+      hz = hi.z;
+    }
+    x.hc0 = found;
+    x.c0 = mk_item(cz, nmeta | (cw << 25) | (wc << 29), hx, hy, hz);
+  }
+  x.hc1 = p.plus;
+  if (p.plus) x.c1 = mk_item(it.a.z, nmeta | (p.prec.w << 25) | (1u << 29), p.prec.x, p.prec.y, p.prec.z);
+}
+
 __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const uint32_t* __restrict__ off,
                                                           uint32_t n, int mode, MatchWork w) {
   __shared__ WaveLds lds_all[WALK_WAVES];
@@ -400,13 +520,14 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
   const uint4 root = ld16(tab.nodes);
   uint64_t visited = 0;
   Slab sid{0, 0}, spc{0, 0};
+  constexpr uint32_t POP = 64u * WALK_IPL;
 
   for (uint32_t c = blockIdx.x * WALK_WAVES + wave; c < nchunks; c += nwaves) {
     const uint32_t t0 = c * WALK_CHUNK;
     const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
 
-    // ---- topic info + word staging (word bases are any disjoint layout) ----
-    uint32_t dsum = 0;
+    // ---- topic info; words staged as [topic][level] with a chunk-wide stride ----
+    uint32_t dmax = 0;
     uint32_t dl[WALK_CHUNK / 64];
 #pragma unroll
     for (int k = 0; k < WALK_CHUNK / 64; ++k) {
@@ -417,34 +538,33 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
         f = w.tfl[t0 + j];
       }
       dl[k] = D;
-      dsum += D;
+      dmax = max(dmax, D);
       L.tinfo[j] = D | (f << 24);
       L.cnt[j] = 0;
       L.fcnt[j] = 0;
     }
-    uint32_t wtotal;
-    uint32_t wb = wave_excl_scan(dsum, lane, &wtotal);
-    const bool staged = wtotal <= (uint32_t)WALK_WORDS;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, d, 64));
+    const uint32_t ws = dmax;   // stride of words[t][level]
+    const bool staged = (uint64_t)ws * WALK_CHUNK <= (uint64_t)WALK_WORDS;
 #pragma unroll
     for (int k = 0; k < WALK_CHUNK / 64; ++k) {
       const uint32_t j = lane + 64 * k;
       if (j < nt) {
         const uint32_t gb = off[t0 + j] + t0 + j;
+        L.tbase[j] = staged ? j * ws : gb;
         if (staged) {
-          L.tbase[j] = wb;
           const uint32_t* src = w.wid + gb;
+          uint32_t* dst = L.words + j * ws;
           uint32_t i = 0;
           for (; i + 4 <= dl[k]; i += 4) {
             uint32_t a0 = src[i], a1 = src[i + 1], a2 = src[i + 2], a3 = src[i + 3];
-            L.words[wb + i] = a0;
-            L.words[wb + i + 1] = a1;
-            L.words[wb + i + 2] = a2;
-            L.words[wb + i + 3] = a3;
+            dst[i] = a0;
+            dst[i + 1] = a1;
+            dst[i + 2] = a2;
+            dst[i + 3] = a3;
           }
-          for (; i < dl[k]; ++i) L.words[wb + i] = src[i];
-          wb += dl[k];
-        } else {
-          L.tbase[j] = gb;
+          for (; i < dl[k]; ++i) dst[i] = src[i];
         }
       }
     }
@@ -453,28 +573,31 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
     uint32_t next = 0, sp = 0, nstage = 0;
     bool ovf = (w.debug & DEBUG_FORCE_HEAVY) != 0;
     for (; !ovf;) {
-      if (sp < 64 && next < nt) {  // refill with new roots
-        const uint32_t k = min(64u - sp, nt - next);
-        bool has = false;
-        Item it = root_item(root, 0, false);
-        if (lane < k) {
-          const uint32_t j = next + lane;
-          const uint32_t f = L.tinfo[j] >> 24;
-          if (!(f & TF_WILDCARD)) {
-            has = true;
-            it = root_item(root, j, false);
-          } else if (mode == MODE_ROUTES) {
-            has = true;
-            it = root_item(root, j, true);
+      if (sp < POP && next < nt) {  // refill with new roots
+        const uint32_t k = min(POP - sp, nt - next);
+EGM_FOR_U(
+          const uint32_t r = u * 64 + lane;
+          bool has = false;
+          Item it = root_item(root, 0, false);
+          if (r < k) {
+            const uint32_t j = next + r;
+            const uint32_t f = L.tinfo[j] >> 24;
+            if (!(f & TF_WILDCARD)) {
+              has = true;
+              it = root_item(root, j, false);
+            } else if (mode == MODE_ROUTES) {
+              has = true;
+              it = root_item(root, j, true);
+            }
           }
-        }
-        const uint64_t b = __ballot(has);
-        if (has) {
-          const uint32_t p = sp + mbcnt(b);
-          L.stack_a[p] = it.a;
-          L.stack_t[p] = it.term;
-        }
-        sp += popc(b);
+          const uint64_t b = __ballot(has);
+          if (has) {
+            const uint32_t p = sp + mbcnt(b);
+            L.stack_a[p] = it.a;
+            L.stack_t[p] = it.term;
+          }
+          sp += popc(b);
+        );
         next += k;
         wave_sync();
       }
@@ -482,73 +605,92 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
         if (next >= nt) break;
         continue;
       }
-      const uint32_t take = min(64u, sp);
+      const uint32_t take = min(POP, sp);
       const uint32_t bi = sp - take;
-      const bool act = lane < take;
-      Item it;
-      it.a = make_uint4(0, 0, 0, 0);
-      it.term = NONE;
-      if (act) {
-        it.a = L.stack_a[bi + lane];
-        it.term = L.stack_t[bi + lane];
-      }
+      Pend p[WALK_IPL];
+      uint32_t tt[WALK_IPL];
+EGM_FOR_U(
+        const uint32_t r = u * 64 + lane;
+        p[u].act = r < take;
+        p[u].it.a = make_uint4(0, 0, 0, 0);
+        p[u].it.term = NONE;
+        if (p[u].act) {
+          p[u].it.a = L.stack_a[bi + r];
+          p[u].it.term = L.stack_t[bi + r];
+        }
+      );
       sp = bi;
       wave_sync();
-
-      Expand x;
-      x.h0 = x.h1 = x.hc0 = x.hc1 = false;
-      uint32_t t = 0;
-      if (act) {
-        t = (it.a.y >> 17) & 0xFFu;
-        const uint32_t ti = L.tinfo[t];
-        const uint32_t D = ti & 0xFFFFFFu, tf = ti >> 24;
-        const uint32_t level = it.a.y & 0x1FFFFu;
-        uint32_t wd = WID_NONE;
-        if (level < D) {
-          if (staged) wd = L.words[L.tbase[t] + level];
-          else wd = __builtin_nontemporal_load(w.wid + L.tbase[t] + level);  // distinct op: no flat merge
+EGM_FOR_U(
+        tt[u] = (p[u].it.a.y >> 17) & 0xFFu;
+        p[u].D = p[u].tf = 0;
+        p[u].w = WID_NONE;
+        if (p[u].act) {
+          const uint32_t ti = L.tinfo[tt[u]];
+          p[u].D = ti & 0xFFFFFFu;
+          p[u].tf = ti >> 24;
+          const uint32_t level = p[u].it.a.y & 0x1FFFFu;
+          if (level < p[u].D) {
+            if (staged) p[u].w = L.words[tt[u] * ws + level];
+            else p[u].w = __builtin_nontemporal_load(w.wid + L.tbase[tt[u]] + level);  // distinct op: no flat merge
+          }
         }
-        expand(tab, mode, it, D, tf, wd, x);
-      }
-      // children -> stack (checked first: an overflow abandons the chunk)
-      const uint64_t c0 = __ballot(x.hc0), c1 = __ballot(x.hc1);
-      const uint32_t m0 = popc(c0), nc = m0 + popc(c1);
+      );
+      EGM_FOR_U(issue(tab, p[u]););
+      Expand x[WALK_IPL];
+      EGM_FOR_U(
+        finish(tab, mode, p[u], x[u]);
+      );
+
+      // children -> stack (all counted first: an overflow abandons the chunk)
+      uint64_t c0b[WALK_IPL], c1b[WALK_IPL];
+      uint32_t nc = 0;
+EGM_FOR_U(
+        c0b[u] = __ballot(x[u].hc0);
+        c1b[u] = __ballot(x[u].hc1);
+        nc += popc(c0b[u]) + popc(c1b[u]);
+      );
       if (sp + nc > (uint32_t)WALK_STACK) {
         ovf = true;
         break;
       }
-      if (x.hc0) {
-        const uint32_t p = sp + mbcnt(c0);
-        L.stack_a[p] = x.c0.a;
-        L.stack_t[p] = x.c0.term;
-      }
-      if (x.hc1) {
-        const uint32_t p = sp + m0 + mbcnt(c1);
-        L.stack_a[p] = x.c1.a;
-        L.stack_t[p] = x.c1.term;
-      }
-      sp += nc;
+EGM_FOR_U(
+        const uint32_t m0 = popc(c0b[u]);
+        if (x[u].hc0) {
+          const uint32_t q = sp + mbcnt(c0b[u]);
+          L.stack_a[q] = x[u].c0.a;
+          L.stack_t[q] = x[u].c0.term;
+        }
+        if (x[u].hc1) {
+          const uint32_t q = sp + m0 + mbcnt(c1b[u]);
+          L.stack_a[q] = x[u].c1.a;
+          L.stack_t[q] = x[u].c1.term;
+        }
+        sp += m0 + popc(c1b[u]);
+      );
       // emits -> stage, flushed to global pieces whenever it would overflow
-      const uint64_t b0 = __ballot(x.h0), b1 = __ballot(x.h1);
-      const uint32_t n0 = popc(b0), ne = n0 + popc(b1);
-      if (nstage + ne > (uint32_t)WALK_STAGE) {
-        wave_sync();
-        flush_stage(L, nstage, t0, lane, w, sid, spc);
-        nstage = 0;
-      }
-      if (x.h0) {
-        const uint32_t p = nstage + mbcnt(b0);
-        L.stage_fid[p] = x.e0;
-        L.stage_t[p] = (uint8_t)t;
-        atomicAdd(&L.fcnt[t], 1u);
-      }
-      if (x.h1) {
-        const uint32_t p = nstage + n0 + mbcnt(b1);
-        L.stage_fid[p] = x.e1;
-        L.stage_t[p] = (uint8_t)t;
-        atomicAdd(&L.fcnt[t], 1u);
-      }
-      nstage += ne;
+EGM_FOR_U(
+        const uint64_t b0 = __ballot(x[u].h0), b1 = __ballot(x[u].h1);
+        const uint32_t n0 = popc(b0), ne = n0 + popc(b1);
+        if (nstage + ne > (uint32_t)WALK_STAGE) {
+          wave_sync();
+          flush_stage(L, nstage, t0, lane, w, sid, spc);
+          nstage = 0;
+        }
+        if (x[u].h0) {
+          const uint32_t q = nstage + mbcnt(b0);
+          L.stage_fid[q] = x[u].e0;
+          L.stage_t[q] = (uint8_t)tt[u];
+          atomicAdd(&L.fcnt[tt[u]], 1u);
+        }
+        if (x[u].h1) {
+          const uint32_t q = nstage + n0 + mbcnt(b1);
+          L.stage_fid[q] = x[u].e1;
+          L.stage_t[q] = (uint8_t)tt[u];
+          atomicAdd(&L.fcnt[tt[u]], 1u);
+        }
+        nstage += ne;
+      );
       visited += take;
       wave_sync();
     }
