@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--match", default="routes", choices=["routes", "trie"])
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--x-presort", action="store_true",
+                    help="EXPERIMENT ONLY: sort the batch on the host before upload (not a valid bench line)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -131,6 +133,12 @@ def main():
     tseed = seed + (7919 * rank if args.mode == "replicate" else 0)
     t = synth.topics(nt, f, c["dmin"], c["dmax"], seed=tseed)
     log(f"[rank {rank}] generated {f.n} filters, {t.n} topics in {time.time() - t0:.1f}s")
+    if args.x_presort:
+        tl = t.to_list()
+        order = np.array(sorted(range(len(tl)), key=tl.__getitem__), dtype=np.int64)
+        del tl
+        t = t.subset(order)
+        log(f"[rank {rank}] EXPERIMENT: batch pre-sorted on the host")
 
     gm = GpuMatcher(local, max_batch=nt)
     t0 = time.time()
@@ -216,6 +224,7 @@ def main():
         elapsed = float(e.item())
     tim = gm.get_timing()
     st = gm.last_stats()
+    wc = gm.walk_counters()
     gm.set_timing(False)
 
     units_per_step = n * world if (args.mode == "replicate" or world == 1) else n
@@ -250,7 +259,8 @@ def main():
                          "kernel": "k_walk", "kernel_ms": walk_ms, "bytes_per_launch": walk_bytes,
                          "path_frac": path_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "stats": {"ids_per_step": n_ids, "visited_per_step": visited, "levels_per_step": sum_d,
-                      "deferred_chunks": st["deferred_chunks"]},
+                      "deferred_chunks": st["deferred_chunks"], "walk_iters": wc["iters"],
+                      "walk_popped": wc["popped"], "walk_lane_occupancy": wc["lane_occupancy"]},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -396,6 +396,17 @@ int egm_match_device(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, con
   return EGM_OK;
 }
 
+int egm_last_walk_counters(egm_ctx* c, uint64_t* iters, uint64_t* popped, uint32_t* items_per_lane) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  int r = sync_last(c);
+  if (r) return r;
+  if (iters) *iters = c->last.iters;
+  if (popped) *popped = c->last.popped;
+  if (items_per_lane) *items_per_lane = (uint32_t)walk_items_per_lane();
+  return EGM_OK;
+}
+
 int egm_last_stats(egm_ctx* c, uint64_t* n_ids, uint64_t* visited, uint32_t* n_def, uint32_t* overflow,
                    uint32_t* n_error) {
   if (!c) return EGM_E_INVAL;

@@ -34,19 +34,19 @@ constexpr int MODE_ROUTES = 1;
 #endif
 constexpr int WALK_WAVES = EGM_WALK_WAVES;
 #ifndef EGM_WALK_STACK
-#define EGM_WALK_STACK 384   // items per wave (20 B each)
+#define EGM_WALK_STACK 384   // items per wave (16 B each)
 #endif
 constexpr int WALK_STACK = EGM_WALK_STACK;
 #ifndef EGM_WALK_STAGE
-#define EGM_WALK_STAGE 512   // staged matches per flush
+#define EGM_WALK_STAGE 384   // staged matches per flush (7 B each)
 #endif
 constexpr int WALK_STAGE = EGM_WALK_STAGE;
 #ifndef EGM_WALK_IPL
-#define EGM_WALK_IPL 1   // work items per lane per iteration
+#define EGM_WALK_IPL 1   // work items per lane per iteration (2 doubles the stack growth per iteration)
 #endif
 constexpr int WALK_IPL = EGM_WALK_IPL;
 #ifndef EGM_WALK_WORDS
-#define EGM_WALK_WORDS 1024   // staged topic word ids per wave chunk
+#define EGM_WALK_WORDS 512   // staged topic word ids per wave chunk
 #endif
 constexpr int WALK_WORDS = EGM_WALK_WORDS;
 constexpr int HEAVY_STACK = 6144;    // items (120 KB LDS) per heavy wave
@@ -324,16 +324,34 @@ __device__ __forceinline__ Item root_item(const uint4& r, uint32_t t, bool exact
 }
 
 // ------------------------------------------------------------------ walk ----
+// A work item is 16 B (one ds_read_b128): {node, meta, plus_child, word}
+//   meta = level[0:17) | t[17:24) | flags[24:28) | wc << 28
+//   word = the topic's word id at `level`
+// A state is finished when it is created, from the record that created it
+// (the literal edge slot carries its child's record, the '+' child's record
+// is one 16 B read): its 'match_#' emit and, at the topic's last level, its
+// lookup_topic emit are staged at once, and only a state that still has a
+// literal or '+' transition to take is pushed.  So every popped item is at a
+// level < D and costs exactly the reads of its own transitions, issued
+// together for all the items a wave pops.
+constexpr uint32_t ML_BITS = 17;
+constexpr uint32_t MT_SHIFT = 17;
+constexpr uint32_t MF_SHIFT = 24;
+constexpr uint32_t MW_SHIFT = 28;
+constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
+constexpr uint32_t T_BITS = WALK_CHUNK <= 64 ? 6 : 7;
+static_assert(WALK_CHUNK <= 128, "t field is 7 bits");
+
 struct alignas(16) WaveLds {
-  uint4 stack_a[WALK_STACK];
-  uint32_t stack_t[WALK_STACK];
+  uint4 stack[WALK_STACK];
   uint32_t stage_fid[WALK_STAGE];
+  uint16_t stage_rank[WALK_STAGE];
+  uint8_t stage_t[WALK_STAGE];
   uint32_t words[WALK_WORDS];
+  uint32_t tinfo[WALK_CHUNK];   // D | tflags << 24
   uint32_t tbase[WALK_CHUNK];   // word base: LDS index (staged) or wid index
-  uint32_t tinfo[WALK_CHUNK];   // levels | flags << 24
   uint32_t cnt[WALK_CHUNK];     // ids per topic, whole chunk
   uint32_t fcnt[WALK_CHUNK];    // ids per topic in the current stage
-  uint8_t stage_t[WALK_STAGE];
 };
 
 __device__ __forceinline__ uint4 mk_piece(uint32_t t, uint32_t count, uint32_t src, uint32_t row_off) {
@@ -367,12 +385,31 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
   return r;
 }
 
-// Write the stage out: ids and pieces from the wave's slabs, per-topic runs by
-// counting sort in LDS, one piece per topic present carrying the topic's
-// running count as its offset inside the CSR row.
+// Write the stage out.  Entries are ranked within their topic by a
+// conflict-free multi-split (lanes holding the same topic find each other
+// with T_BITS ballots; one LDS add per topic per 64 entries), then scattered
+// into the wave's ids slab grouped by topic, one piece per topic present
+// carrying the topic's running count as its offset inside the CSR row.
 __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane,
-                                            const MatchWork& w,
-                            Slab& sid, Slab& spc) {
+                                            const MatchWork& w, Slab& sid, Slab& spc) {
+  for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const bool act = i < nstage;
+    const uint32_t tt = act ? L.stage_t[i] : 0u;
+    uint64_t m = __ballot(act);
+#pragma unroll
+    for (uint32_t b = 0; b < T_BITS; ++b) {
+      const bool bit = (tt >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    const uint32_t leader = act ? (uint32_t)__builtin_ctzll(m) : lane;
+    uint32_t old = 0;
+    if (act && lane == leader) old = atomicAdd(&L.fcnt[tt], popc(m));
+    old = __shfl(old, (int)leader, 64);
+    if (act) L.stage_rank[i] = (uint16_t)(old + mbcnt(m));
+  }
+  wave_sync();
   constexpr int PER = WALK_CHUNK / 64;
   uint32_t fl[PER];
   uint32_t s = 0, np = 0;
@@ -394,17 +431,14 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
   for (int k = 0; k < PER; ++k) {
     const uint32_t j = lane * PER + k;
     if (fl[k] && ok) w.pieces[pbase + pex++] = mk_piece(t0 + j, fl[k], (uint32_t)(base + ex), L.cnt[j]);
-    L.fcnt[j] = ex;   // becomes the scatter cursor
+    L.fcnt[j] = ex;   // the topic's start inside this flush
     L.cnt[j] += fl[k];
     ex += fl[k];
   }
   wave_sync();
   if (ok) {
-    for (uint32_t i = lane; i < nstage; i += 64) {
-      const uint32_t tt = L.stage_t[i];
-      const uint32_t p = atomicAdd(&L.fcnt[tt], 1u);
-      w.ids_tmp[base + p] = L.stage_fid[i];
-    }
+    for (uint32_t i = lane; i < nstage; i += 64)
+      w.ids_tmp[base + L.fcnt[L.stage_t[i]] + L.stage_rank[i]] = L.stage_fid[i];
   }
   wave_sync();
 #pragma unroll
@@ -412,39 +446,10 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
   wave_sync();
 }
 
-// Two-phase item processing: issue() starts every global read an item needs
-// (the '+' child's record and the first two slots of the literal bucket),
-// finish() consumes them.  A wave issues the reads of all its items before it
-// waits on any, so each lane keeps WALK_IPL dependent chains in flight.
-struct Pend {
-  Item it;
-  uint32_t D, tf, w, b;
-  bool act, lit, plus;
-  uint4 prec, l0, h0, l1, h1;
-};
-
-__device__ __forceinline__ void issue(const DevTable& tab, Pend& p) {
-  const uint32_t meta = p.it.a.y;
-  const uint32_t level = meta & 0x1FFFFu, fl = (meta >> 25) & 0xFu, ex = (meta >> 30) & 1u;
-  const bool atend = level == p.D;
-  const bool rootd = (level == 0) && (p.tf & TF_DOLLAR);
-  p.plus = p.act && !ex && !atend && (fl & F_PLUS) && !rootd;
-  p.lit = p.act && !ex && !atend && (fl & F_LIT) && p.w < WID_MAX;
-  if (p.plus) p.prec = ld16(tab.nodes + p.it.a.z);
-  if (p.lit) {
-    p.b = edge_bucket(p.it.a.x, p.w, tab.edge_mask);
-    const uint8_t* bp = (const uint8_t*)(tab.edges + (size_t)p.b * EDGE_BUCKET);
-    p.l0 = ld16(bp);
-    p.h0 = ld16(bp + 16);
-    p.l1 = ld16(bp + 32);
-    p.h1 = ld16(bp + 48);
-  }
-}
-
-// continue a bucket probe at slot k0 of bucket b (rare: first two slots busy)
+// Slot search continued at slot k0 of bucket b (rare: both first slots hold
+// other keys).
 __device__ __forceinline__ bool edge_probe_from(const DevTable& tab, uint32_t b, int k0, uint32_t node, uint32_t w,
-                                                uint4* lo_out,
-                                uint4* hi_out) {
+                                                uint4* lo_out, uint4* hi_out) {
   for (;;) {
     const EdgeSlot* bp = tab.edges + (size_t)b * EDGE_BUCKET;
     for (int k = k0; k < EDGE_BUCKET; ++k) {
@@ -462,52 +467,135 @@ __device__ __forceinline__ bool edge_probe_from(const DevTable& tab, uint32_t b,
   }
 }
 
-__device__ __forceinline__ void finish(const DevTable& tab, int mode, Pend& p, Expand& x) {
-  x.h0 = x.h1 = x.hc0 = x.hc1 = false;
+// One popped item between issuing its reads and consuming them.
+struct Pend {
+  uint4 it;                 // the item
+  uint32_t b, ti, nw;       // bucket, its topic's info, the word at level + 1
+  bool act, lit, plus;
+  uint4 prec, l0, h0, l1, h1;
+};
+
+// Up to four emits and two pushes per popped item.
+struct Out {
+  uint32_t f0, f1, f2, f3;  // literal child: '#', terminal; '+' child: '#', terminal
+  bool e0, e1, e2, e3;
+  uint4 c0, c1;             // children to push
+  bool p0, p1;
+  uint32_t created;         // states created (instrumentation: SURVEY §8d V_t)
+};
+
+__device__ __forceinline__ uint32_t word_at(const WaveLds& L, const MatchWork& w, bool staged, uint32_t tt,
+                                            uint32_t level) {
+  if (staged) return L.words[min(L.tbase[tt] + level, (uint32_t)WALK_WORDS - 1)];
+  return w.wid[L.tbase[tt] + level];
+}
+
+// Branch-free on purpose: every lane issues its loads unconditionally (an
+// idle lane reads node 0 / bucket 0, lines every wave keeps hot).  A load
+// inside an `if` makes LLVM merge its result at the end of the block, and
+// the copy it inserts there waits for the load — the second item's reads
+// would then only be issued after the first item's had returned.
+__device__ __forceinline__ void issue(const DevTable& tab, const WaveLds& L, bool staged, uint32_t ws, Pend& p) {
+  const uint32_t meta = p.it.y;
+  const uint32_t fl = (meta >> MF_SHIFT) & 0xFu;
+  p.plus = p.act && (fl & F_PLUS);
+  p.lit = p.act && (fl & F_LIT) && p.it.w < WID_MAX;
+  p.b = edge_bucket(p.it.x, p.it.w, tab.edge_mask);
+  p.prec = ld16(tab.nodes + (p.plus ? p.it.z : 0u));
+  const uint8_t* bp = (const uint8_t*)(tab.edges + (size_t)(p.lit ? p.b : 0u) * EDGE_BUCKET);
+  p.l0 = ld16(bp);
+  p.h0 = ld16(bp + 16);
+  p.l1 = ld16(bp + 32);
+  p.h1 = ld16(bp + 48);
+  // LDS reads overlapping the global ones: the topic's info and, when the
+  // words are staged, the next level's word (clamped; used only if level+1 < D)
+  const uint32_t tt = (meta >> MT_SHIFT) & 0x7Fu, level = meta & LEVEL_MAX;
+  p.ti = L.tinfo[tt];
+  p.nw = L.words[min(tt * ws + level + 1, (uint32_t)WALK_WORDS - 1)];
+  (void)staged;
+}
+
+__device__ __forceinline__ void finish(const DevTable& tab, int mode, const WaveLds& L, const MatchWork& w,
+                                       bool staged, Pend& p, Out& o) {
+  o.e0 = o.e1 = o.e2 = o.e3 = o.p0 = o.p1 = false;
+  o.created = 0;
   if (!p.act) return;
-  const Item& it = p.it;
-  const uint32_t meta = it.a.y;
-  if ((meta >> 30) & 1u) {  // exact walk of a wildcard topic (ROUTES mode): rare
-    expand(tab, mode, it, p.D, p.tf, p.w, x);
-    return;
-  }
-  const uint32_t level = meta & 0x1FFFFu, tm = meta & (0xFFu << 17);
-  const uint32_t fl = (meta >> 25) & 0xFu, wc = (meta >> 29) & 1u;
-  const bool atend = level == p.D;
-  const bool rootd = (level == 0) && (p.tf & TF_DOLLAR);
-  const uint32_t nmeta = (level + 1) | tm;
-  x.e0 = it.a.w;
-  x.e1 = it.term;
-  x.h0 = (fl & F_HASH) && !rootd;
-  x.h1 = atend && (fl & F_TERM) && (mode == MODE_ROUTES || wc || (p.D == 1 && (p.tf & TF_DOLLAR)));
+  const uint32_t meta = p.it.y;
+  const uint32_t level = meta & LEVEL_MAX, tt = (meta >> MT_SHIFT) & 0x7Fu;
+  const uint32_t wc = (meta >> MW_SHIFT) & 1u;
+  const uint32_t D = p.ti & 0xFFFFFFu, tf = p.ti >> 24;
+  const uint32_t nl = level + 1;
+  const bool leaf = nl == D;
+  uint32_t nw = p.nw;
+  if (!staged) nw = leaf ? WID_NONE : w.wid[L.tbase[tt] + nl];
+  const uint32_t base_meta = nl | (tt << MT_SHIFT);
   if (p.lit) {
     // pick the matching slot's fields with masks, not a select of the two
     // loaded slots: LLVM folds the latter into a phi of addresses into the
     // per-item array and then keeps that array in scratch
-    const uint32_t node = it.a.x;
-    const bool m0 = p.l0.x == node && p.l0.y == p.w;
-    const bool e0 = p.l0.x == NONE;
-    const bool m1 = !m0 && !e0 && p.l1.x == node && p.l1.y == p.w;
-    const bool e1 = p.l1.x == NONE;
+    const uint32_t node = p.it.x;
+    const bool m0 = p.l0.x == node && p.l0.y == p.it.w;
+    const bool z0 = p.l0.x == NONE;
+    const bool m1 = !m0 && !z0 && p.l1.x == node && p.l1.y == p.it.w;
+    const bool z1 = p.l1.x == NONE;
     const uint32_t s1 = m1 ? 0xFFFFFFFFu : 0u;
     uint32_t cz = (p.l0.z & ~s1) | (p.l1.z & s1), cw = (p.l0.w & ~s1) | (p.l1.w & s1);
     uint32_t hx = (p.h0.x & ~s1) | (p.h1.x & s1), hy = (p.h0.y & ~s1) | (p.h1.y & s1);
     uint32_t hz = (p.h0.z & ~s1) | (p.h1.z & s1);
     bool found = m0 || m1;
-    if (!m0 && !e0 && !m1 && !e1) {   // both first slots busy with other keys: keep probing
+    if (!m0 && !z0 && !m1 && !z1) {   // both first slots hold other keys: keep probing
       uint4 lo, hi;
-      found = edge_probe_from(tab, p.b, 2, node, p.w, &lo, &hi);
+      found = edge_probe_from(tab, p.b, 2, node, p.it.w, &lo, &hi);
       cz = lo.z;
       cw = lo.w;
       hx = hi.x;
       hy = hi.y;
       hz = hi.z;
     }
-    x.hc0 = found;
-    x.c0 = mk_item(cz, nmeta | (cw << 25) | (wc << 29), hx, hy, hz);
+    if (found) {
+      o.created += 1;
+      o.e0 = (cw & F_HASH) != 0;
+      o.f0 = hy;
+      o.e1 = leaf && (cw & F_TERM) && (mode == MODE_ROUTES || wc || (D == 1 && (tf & TF_DOLLAR)));
+      o.f1 = hz;
+      o.p0 = !leaf && (cw & (F_LIT | F_PLUS));
+      o.c0 = make_uint4(cz, base_meta | (cw << MF_SHIFT) | (wc << MW_SHIFT), hx, nw);
+    }
   }
-  x.hc1 = p.plus;
-  if (p.plus) x.c1 = mk_item(it.a.z, nmeta | (p.prec.w << 25) | (1u << 29), p.prec.x, p.prec.y, p.prec.z);
+  if (p.plus) {
+    const uint32_t pf = p.prec.w;
+    o.created += 1;
+    o.e2 = (pf & F_HASH) != 0;
+    o.f2 = p.prec.y;
+    o.e3 = leaf && (pf & F_TERM);
+    o.f3 = p.prec.z;
+    o.p1 = !leaf && (pf & (F_LIT | F_PLUS));
+    o.c1 = make_uint4(p.it.z, base_meta | (pf << MF_SHIFT) | (1u << MW_SHIFT), p.prec.x, nw);
+  }
+}
+
+// lookup_routes(Topic) of a wildcard topic in ROUTES mode (emqx_router.erl:
+// 129-134): the topic's words walked as a literal key, '+'/'#' words taking
+// the '+'/'#' edges.  Rare (MQTT publishes never carry wildcards): one lane,
+// one dependent read per level.
+__device__ bool exact_walk(const DevTable& tab, const WaveLds& L, const MatchWork& w, bool staged, uint32_t j,
+                           uint32_t D, uint32_t* fid) {
+  uint32_t node = 0;
+  for (uint32_t l = 0; l < D; ++l) {
+    const uint32_t wd = word_at(L, w, staged, j, l);
+    uint32_t child = NONE;
+    if (wd == WID_PLUS) child = tab.nodes[node].plus_child;
+    else if (wd == WID_HASH) child = tab.hash_child[node];
+    else if (wd < WID_MAX) {
+      uint4 lo, hi;
+      if (edge_probe_from(tab, edge_bucket(node, wd, tab.edge_mask), 0, node, wd, &lo, &hi)) child = lo.z;
+    }
+    if (child == NONE) return false;
+    node = child;
+  }
+  const NodeRec r = tab.nodes[node];
+  *fid = r.term_fid;
+  return (r.flags & F_TERM) != 0;
 }
 
 __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const uint32_t* __restrict__ off,
@@ -518,7 +606,8 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
   const uint32_t nwaves = gridDim.x * WALK_WAVES;
   const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
   const uint4 root = ld16(tab.nodes);
-  uint64_t visited = 0;
+  uint32_t created = 0;
+  unsigned long long iters = 0, popped = 0;
   Slab sid{0, 0}, spc{0, 0};
   constexpr uint32_t POP = 64u * WALK_IPL;
 
@@ -573,30 +662,42 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
     uint32_t next = 0, sp = 0, nstage = 0;
     bool ovf = (w.debug & DEBUG_FORCE_HEAVY) != 0;
     for (; !ovf;) {
-      if (sp < POP && next < nt) {  // refill with new roots
+      if (sp < POP && next < nt) {  // admit new topics: emit their root '#', push their roots
         const uint32_t k = min(POP - sp, nt - next);
+        if (nstage + POP > (uint32_t)WALK_STAGE) {
+          flush_stage(L, nstage, t0, lane, w, sid, spc);
+          nstage = 0;
+        }
 EGM_FOR_U(
           const uint32_t r = u * 64 + lane;
-          bool has = false;
-          Item it = root_item(root, 0, false);
+          bool has = false, em = false;
+          uint32_t fid = NONE;
+          uint4 it = make_uint4(0, 0, 0, 0);
+          const uint32_t j = next + r;
           if (r < k) {
-            const uint32_t j = next + r;
-            const uint32_t f = L.tinfo[j] >> 24;
-            if (!(f & TF_WILDCARD)) {
-              has = true;
-              it = root_item(root, j, false);
-            } else if (mode == MODE_ROUTES) {
-              has = true;
-              it = root_item(root, j, true);
+            const uint32_t ti = L.tinfo[j], D = ti & 0xFFFFFFu, tf = ti >> 24;
+            if (tf & TF_WILDCARD) {
+              if (mode == MODE_ROUTES) em = exact_walk(tab, L, w, staged, j, D, &fid);
+            } else if (D <= LEVEL_MAX) {
+              const bool dollar = (tf & TF_DOLLAR) != 0;
+              em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
+              fid = root.y;
+              created += 1;
+              const uint32_t fl = root.w & (F_LIT | (dollar ? 0u : F_PLUS));
+              has = (fl & (F_LIT | F_PLUS)) != 0;
+              it = make_uint4(0, (j << MT_SHIFT) | (fl << MF_SHIFT), root.x, word_at(L, w, staged, j, 0));
             }
           }
           const uint64_t b = __ballot(has);
-          if (has) {
-            const uint32_t p = sp + mbcnt(b);
-            L.stack_a[p] = it.a;
-            L.stack_t[p] = it.term;
-          }
+          if (has) L.stack[sp + mbcnt(b)] = it;
           sp += popc(b);
+          const uint64_t be = __ballot(em);
+          if (em) {
+            const uint32_t q = nstage + mbcnt(be);
+            L.stage_fid[q] = fid;
+            L.stage_t[q] = (uint8_t)j;
+          }
+          nstage += popc(be);
         );
         next += k;
         wave_sync();
@@ -608,90 +709,71 @@ EGM_FOR_U(
       const uint32_t take = min(POP, sp);
       const uint32_t bi = sp - take;
       Pend p[WALK_IPL];
-      uint32_t tt[WALK_IPL];
 EGM_FOR_U(
         const uint32_t r = u * 64 + lane;
         p[u].act = r < take;
-        p[u].it.a = make_uint4(0, 0, 0, 0);
-        p[u].it.term = NONE;
-        if (p[u].act) {
-          p[u].it.a = L.stack_a[bi + r];
-          p[u].it.term = L.stack_t[bi + r];
-        }
+        p[u].it = L.stack[min(bi + r, (uint32_t)WALK_STACK - 1)];   // unconditional: see issue()
       );
       sp = bi;
-      wave_sync();
-EGM_FOR_U(
-        tt[u] = (p[u].it.a.y >> 17) & 0xFFu;
-        p[u].D = p[u].tf = 0;
-        p[u].w = WID_NONE;
-        if (p[u].act) {
-          const uint32_t ti = L.tinfo[tt[u]];
-          p[u].D = ti & 0xFFFFFFu;
-          p[u].tf = ti >> 24;
-          const uint32_t level = p[u].it.a.y & 0x1FFFFu;
-          if (level < p[u].D) {
-            if (staged) p[u].w = L.words[tt[u] * ws + level];
-            else p[u].w = __builtin_nontemporal_load(w.wid + L.tbase[tt[u]] + level);  // distinct op: no flat merge
-          }
-        }
-      );
-      EGM_FOR_U(issue(tab, p[u]););
-      Expand x[WALK_IPL];
-      EGM_FOR_U(
-        finish(tab, mode, p[u], x[u]);
-      );
+      iters += 1;
+      popped += take;
+      EGM_FOR_U(issue(tab, L, staged, ws, p[u]););
+      Out o[WALK_IPL];
+      EGM_FOR_U(finish(tab, mode, L, w, staged, p[u], o[u]); created += o[u].created;);
 
       // children -> stack (all counted first: an overflow abandons the chunk)
       uint64_t c0b[WALK_IPL], c1b[WALK_IPL];
       uint32_t nc = 0;
 EGM_FOR_U(
-        c0b[u] = __ballot(x[u].hc0);
-        c1b[u] = __ballot(x[u].hc1);
+        c0b[u] = __ballot(o[u].p0);
+        c1b[u] = __ballot(o[u].p1);
         nc += popc(c0b[u]) + popc(c1b[u]);
       );
       if (sp + nc > (uint32_t)WALK_STACK) {
         ovf = true;
         break;
       }
+      wave_sync();   // the pops above read the slots the pushes below may overwrite
 EGM_FOR_U(
         const uint32_t m0 = popc(c0b[u]);
-        if (x[u].hc0) {
-          const uint32_t q = sp + mbcnt(c0b[u]);
-          L.stack_a[q] = x[u].c0.a;
-          L.stack_t[q] = x[u].c0.term;
-        }
-        if (x[u].hc1) {
-          const uint32_t q = sp + m0 + mbcnt(c1b[u]);
-          L.stack_a[q] = x[u].c1.a;
-          L.stack_t[q] = x[u].c1.term;
-        }
+        if (o[u].p0) L.stack[sp + mbcnt(c0b[u])] = o[u].c0;
+        if (o[u].p1) L.stack[sp + m0 + mbcnt(c1b[u])] = o[u].c1;
         sp += m0 + popc(c1b[u]);
       );
       // emits -> stage, flushed to global pieces whenever it would overflow
 EGM_FOR_U(
-        const uint64_t b0 = __ballot(x[u].h0), b1 = __ballot(x[u].h1);
-        const uint32_t n0 = popc(b0), ne = n0 + popc(b1);
+        const uint64_t b0 = __ballot(o[u].e0), b1 = __ballot(o[u].e1);
+        const uint64_t b2 = __ballot(o[u].e2), b3 = __ballot(o[u].e3);
+        const uint32_t n0 = popc(b0), n1 = popc(b1), n2 = popc(b2);
+        const uint32_t ne = n0 + n1 + n2 + popc(b3);
         if (nstage + ne > (uint32_t)WALK_STAGE) {
           wave_sync();
           flush_stage(L, nstage, t0, lane, w, sid, spc);
           nstage = 0;
         }
-        if (x[u].h0) {
+        const uint8_t tt = (uint8_t)((p[u].it.y >> MT_SHIFT) & 0x7Fu);
+        if (o[u].e0) {
           const uint32_t q = nstage + mbcnt(b0);
-          L.stage_fid[q] = x[u].e0;
-          L.stage_t[q] = (uint8_t)tt[u];
-          atomicAdd(&L.fcnt[tt[u]], 1u);
+          L.stage_fid[q] = o[u].f0;
+          L.stage_t[q] = tt;
         }
-        if (x[u].h1) {
+        if (o[u].e1) {
           const uint32_t q = nstage + n0 + mbcnt(b1);
-          L.stage_fid[q] = x[u].e1;
-          L.stage_t[q] = (uint8_t)tt[u];
-          atomicAdd(&L.fcnt[tt[u]], 1u);
+          L.stage_fid[q] = o[u].f1;
+          L.stage_t[q] = tt;
+        }
+        if (o[u].e2) {
+          const uint32_t q = nstage + n0 + n1 + mbcnt(b2);
+          L.stage_fid[q] = o[u].f2;
+          L.stage_t[q] = tt;
+        }
+        if (o[u].e3) {
+          const uint32_t q = nstage + n0 + n1 + n2 + mbcnt(b3);
+          L.stage_fid[q] = o[u].f3;
+          L.stage_t[q] = tt;
         }
         nstage += ne;
       );
-      visited += take;
       wave_sync();
     }
     wave_sync();
@@ -702,6 +784,7 @@ EGM_FOR_U(
         w.deferred[d] = c;
       }
       for (uint32_t j = lane; j < nt; j += 64) w.cnt[t0 + j] = 0;
+      nstage = 0;
       wave_sync();
       continue;
     }
@@ -711,7 +794,14 @@ EGM_FOR_U(
   }
   for (unsigned long long i = spc.cur + lane; i < spc.end && i < w.pieces_cap; i += 64)
     w.pieces[i] = make_uint4(NONE, 0, 0, 0);   // unused tail of the last pieces slab
-  if (lane == 0 && visited) atomicAdd(&w.stats->visited, (unsigned long long)visited);
+  unsigned long long v = created;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  if (lane == 0) {
+    if (v) atomicAdd(&w.stats->visited, v);
+    atomicAdd(&w.stats->iters, iters);
+    atomicAdd(&w.stats->popped, popped);
+  }
 }
 
 // ----------------------------------------------------------------- heavy ----
@@ -947,6 +1037,7 @@ int walk_grid_blocks(uint32_t n) {
 }
 
 int walk_waves_per_block() { return WALK_WAVES; }
+int walk_items_per_lane() { return WALK_IPL; }
 
 size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 

@@ -183,6 +183,13 @@ class GpuMatcher:
         return {"n_ids": a.value, "visited": b.value, "deferred_chunks": c.value, "overflow": d.value,
                 "errors": e.value}
 
+    def walk_counters(self) -> dict:
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint32()
+        self._check(self.lib.egm_last_walk_counters(self.ctx, C.byref(a), C.byref(b), C.byref(c)),
+                    "egm_last_walk_counters")
+        occ = b.value / max(1, a.value * 64 * c.value)
+        return {"iters": a.value, "popped": b.value, "items_per_lane": c.value, "lane_occupancy": occ}
+
     def set_debug(self, flags: int):
         self._check(self.lib.egm_set_debug(self.ctx, flags), "egm_set_debug")
 
