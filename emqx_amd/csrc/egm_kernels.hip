@@ -52,9 +52,13 @@ constexpr int WALK_WORDS = EGM_WALK_WORDS;
 constexpr int HEAVY_STACK = 6144;    // items (120 KB LDS) per heavy wave
 constexpr int TOK_BLOCK = 256;
 #ifndef EGM_TOK_LDS
-#define EGM_TOK_LDS 32768   // staged topic bytes per tokenise block
+#define EGM_TOK_LDS 24576   // staged topic bytes per tokenise block
 #endif
 constexpr int TOK_LDS = EGM_TOK_LDS;
+#ifndef EGM_TOK_WORDS
+#define EGM_TOK_WORDS 3072   // words per tokenise block (9 B of LDS each)
+#endif
+constexpr int TOK_WORDS = EGM_TOK_WORDS;
 constexpr int SCAN_TILE = 2048;      // counts per scan tile (256 threads x 8)
 
 static_assert(WALK_CHUNK <= 256 && WALK_CHUNK % 64 == 0, "chunk");
@@ -87,7 +91,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
 // item = (node, meta); meta = level[0:17) | t[17:25) | flags[25:29) | wc<<29 | exact<<30
 __device__ __forceinline__ uint32_t mk_meta(uint32_t level, uint32_t t, uint32_t fl, uint32_t wc,
                                             uint32_t ex) {
-  return level | (t << 17) | (fl << 25) | (wc << 29) | (ex << 30);
+  return level | (t << 17) | ((fl & F_BASIC) << 25) | (wc << 29) | (ex << 30);
 }
 
 __device__ __forceinline__ uint4 ld16(const void* p) { return *(const uint4*)p; }
@@ -189,33 +193,196 @@ __device__ __forceinline__ void tokenise_one(const DevTable& tab, const uint32_t
   *fl_out = fl;
 }
 
+__device__ __forceinline__ uint32_t lds_byte(const uint32_t* sw, uint32_t i) {
+  return (sw[i >> 2] >> (8 * (i & 3u))) & 0xFFu;
+}
+
+// Mask (bit 7 of each byte) of the bytes of v equal to '/'.
+__device__ __forceinline__ uint32_t slash_mask(uint32_t v) {
+  const uint32_t x = v ^ 0x2F2F2F2Fu;
+  return (x - 0x01010101u) & ~x & 0x80808080u;
+}
+
+// Keep the bytes [lo, hi) of a 4-byte word (0 <= lo <= hi <= 4) in a byte mask.
+__device__ __forceinline__ uint32_t byte_range(uint32_t lo, uint32_t hi) {
+  const uint32_t a = lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo));
+  const uint32_t b = hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u);
+  return a & b;
+}
+
+// Resolve a dictionary probe whose first slot {a, b} is already loaded; the
+// candidate's bytes are in LDS at st.  Continues with the next slots (rare).
+__device__ __forceinline__ uint32_t dict_resolve(const DevTable& tab, uint64_t h, uint4 a, uint4 b,
+                                                 const uint32_t* sw, uint32_t st, uint32_t len) {
+  uint32_t i = (uint32_t)h & tab.dict_mask;
+  for (;;) {
+    if (a.z == NONE) return WID_NONE;
+    if (a.x == (uint32_t)h && a.y == (uint32_t)(h >> 32) && a.w == len) {
+      bool eq = true;
+      if (len <= 16) {
+        for (uint32_t k = 0; k < len; ++k) eq &= byte_of(b, k) == lds_byte(sw, st + k);
+      } else {
+        const uint8_t* q = tab.dict_blob + tab.dict_off[a.z];
+        for (uint32_t k = 0; k < len; ++k) eq &= q[k] == lds_byte(sw, st + k);
+      }
+      if (eq) return a.z;
+    }
+    i = (i + 1) & tab.dict_mask;
+    const uint8_t* sp = (const uint8_t*)(tab.dict + i);
+    a = ld16(sp);
+    b = ld16(sp + 16);
+  }
+}
+
+// emqx_topic:words/1 (emqx_topic.erl:153-164) + wildcard/1 (:53-62) for a
+// block of TOK_BLOCK topics, in three passes over the block's bytes staged in
+// LDS so that no lane waits on another's divergent work:
+//   1. lane per topic: count '/' four bytes at a time -> levels, '$' flag;
+//      block scan -> each topic's first word slot
+//   2. lane per topic: record every word's (start, length, output index)
+//   3. lane per word, two words per lane in flight: FNV-1a of its bytes, the
+//      '+'/'#' words, the byte-exact dictionary probe -> wid[off[t] + t + l]
+// Blocks whose bytes or words do not fit LDS take the lane-per-topic path.
 __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint8_t* __restrict__ blob,
                                                         const uint32_t* __restrict__ off, uint32_t n,
                                                         uint32_t* __restrict__ wid, uint32_t* __restrict__ lv,
                                                         uint8_t* __restrict__ tfl) {
   __shared__ __attribute__((aligned(16))) uint32_t sw[TOK_LDS / 4];
+  __shared__ uint32_t wpos[TOK_WORDS];   // start | len << 16 (LDS byte index)
+  __shared__ uint32_t wdst[TOK_WORDS];   // index into wid[]
+  __shared__ uint8_t wtop[TOK_WORDS];    // topic within the block
+  __shared__ uint32_t tbase[TOK_BLOCK];
+  __shared__ uint32_t tflag[TOK_BLOCK];
+  __shared__ uint32_t wsum[TOK_BLOCK / 64];
   const uint32_t t0 = blockIdx.x * TOK_BLOCK;
   if (t0 >= n) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t t1 = min(t0 + (uint32_t)TOK_BLOCK, n);
   const uint32_t s = off[t0], e = off[t1];
   const uint32_t sa = s & ~3u;
   const uint32_t ea = (e + 3u) & ~3u;   // blob is readable up to a multiple of 4 (ABI)
-  const bool staged = (ea - sa) <= (uint32_t)TOK_LDS;
-  if (staged) {
+  const bool staged = (ea - sa) <= (uint32_t)TOK_LDS && (ea - sa) < 32768u;
+  const uint32_t t = t0 + tid;
+  if (!staged) {   // long topics: lane per topic straight from global memory
+    if (t < t1) {
+      const uint32_t ts = off[t], len = off[t + 1] - ts;
+      uint32_t l;
+      uint8_t fl;
+      tokenise_one(tab, (const uint32_t*)(blob + (ts & ~3u)), ts & 3u, len, ts + t, wid, &l, &fl);
+      lv[t] = l;
+      tfl[t] = fl;
+    }
+    return;
+  }
+  {
     const uint32_t nw = (ea - sa) >> 2;
     const uint32_t* src = (const uint32_t*)(blob + sa);
-    for (uint32_t i = threadIdx.x; i < nw; i += TOK_BLOCK) sw[i] = src[i];
+    for (uint32_t i = tid; i < nw; i += TOK_BLOCK) sw[i] = src[i];
   }
   __syncthreads();
-  const uint32_t t = t0 + threadIdx.x;
-  if (t >= t1) return;
-  const uint32_t ts = off[t], len = off[t + 1] - ts;
-  uint32_t l;
-  uint8_t fl;
-  if (staged) tokenise_one(tab, sw, ts - sa, len, ts + t, wid, &l, &fl);
-  else tokenise_one(tab, (const uint32_t*)(blob + (ts & ~3u)), ts & 3u, len, ts + t, wid, &l, &fl);
-  lv[t] = l;
-  tfl[t] = fl;
+
+  // ---- pass 1: levels per topic ----
+  uint32_t ts = 0, len = 0, D = 0, fl = 0;
+  if (t < t1) {
+    ts = off[t] - sa;
+    len = off[t + 1] - off[t];
+    uint32_t c = 0;
+    for (uint32_t q = ts & ~3u; q < ts + len; q += 4) {
+      const uint32_t lo = q < ts ? ts - q : 0u, hi = min(4u, ts + len - q);
+      c += popc((uint64_t)(slash_mask(sw[q >> 2]) & byte_range(lo, hi)));
+    }
+    D = c + 1;
+    if (len > 0 && lds_byte(sw, ts) == '$') fl |= TF_DOLLAR;
+  }
+  uint32_t wtot;
+  uint32_t ex = wave_excl_scan(D, lane, &wtot);
+  if (lane == 0) wsum[wv] = wtot;
+  __syncthreads();
+  uint32_t W = 0;
+#pragma unroll
+  for (int k = 0; k < TOK_BLOCK / 64; ++k) {
+    if ((uint32_t)k < wv) ex += wsum[k];
+    W += wsum[k];
+  }
+  if (W > (uint32_t)TOK_WORDS) {   // too many words for LDS: lane per topic
+    if (t < t1) {
+      uint32_t l;
+      uint8_t f;
+      tokenise_one(tab, sw, ts, len, off[t] + t, wid, &l, &f);
+      lv[t] = l;
+      tfl[t] = f;
+    }
+    return;
+  }
+  tflag[tid] = fl;
+
+  // ---- pass 2: word boundaries ----
+  if (t < t1) {
+    const uint32_t g = off[t] + t;   // wid index of the topic's first word
+    uint32_t l = 0, ws = ts;
+    for (uint32_t q = ts & ~3u; q < ts + len; q += 4) {
+      const uint32_t lo = q < ts ? ts - q : 0u, hi = min(4u, ts + len - q);
+      uint32_t m = slash_mask(sw[q >> 2]) & byte_range(lo, hi);
+      while (m) {
+        const uint32_t p = q + (__builtin_ctz(m) >> 3);
+        m &= m - 1;
+        wpos[ex + l] = ws | ((p - ws) << 16);
+        wdst[ex + l] = g + l;
+        wtop[ex + l] = (uint8_t)tid;
+        ++l;
+        ws = p + 1;
+      }
+    }
+    wpos[ex + l] = ws | ((ts + len - ws) << 16);
+    wdst[ex + l] = g + l;
+    wtop[ex + l] = (uint8_t)tid;
+    lv[t] = D;
+  }
+  __syncthreads();
+
+  // ---- pass 3: hash + dictionary probe, lane per word ----
+  for (uint32_t i0 = tid; i0 < W; i0 += 2 * TOK_BLOCK) {
+    uint32_t st[2], wl[2], res[2];
+    uint64_t h[2];
+    bool act[2], spec[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t i = i0 + u * TOK_BLOCK;
+      act[u] = i < W;
+      const uint32_t pw = act[u] ? wpos[i] : 0u;
+      st[u] = pw & 0xFFFFu;
+      wl[u] = pw >> 16;
+      uint64_t x = FNV_BASIS;
+      for (uint32_t k = 0; k < wl[u]; ++k) x = fnv_step(x, (uint8_t)lds_byte(sw, st[u] + k));
+      h[u] = word_hash_finish(x, wl[u]);
+      spec[u] = false;
+      res[u] = WID_NONE;
+      if (wl[u] == 1) {
+        const uint32_t c = lds_byte(sw, st[u]);
+        if (c == '+' || c == '#') {
+          spec[u] = true;
+          res[u] = c == '+' ? WID_PLUS : WID_HASH;
+        }
+      }
+    }
+    uint4 a[2], b[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {   // both first-slot reads in flight (unconditional: see issue())
+      const uint8_t* sp = (const uint8_t*)(tab.dict + ((act[u] && !spec[u]) ? ((uint32_t)h[u] & tab.dict_mask) : 0u));
+      a[u] = ld16(sp);
+      b[u] = ld16(sp + 16);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!act[u]) continue;
+      const uint32_t i = i0 + u * TOK_BLOCK;
+      if (spec[u]) atomicOr(&tflag[wtop[i]], (uint32_t)TF_WILDCARD);
+      else res[u] = dict_resolve(tab, h[u], a[u], b[u], sw, st[u], wl[u]);
+      wid[wdst[i]] = res[u];
+    }
+  }
+  __syncthreads();
+  if (t < t1) tfl[t] = (uint8_t)tflag[tid];
 }
 
 // ------------------------------------------------------------ NFA expand ----
@@ -298,9 +465,9 @@ __device__ __forceinline__ void expand(const DevTable& tab, int mode, const Item
     if (want_plus) prec = ld16(tab.nodes + it.a.z);
     const bool found = want_lit && edge_probe(tab, node, w, &lo, &hi);
     x.hc0 = found;
-    if (found) x.c0 = mk_item(lo.z, nmeta | (lo.w << 25) | (wc << 29), hi.x, hi.y, hi.z);
+    if (found) x.c0 = mk_item(lo.z, nmeta | ((lo.w & F_BASIC) << 25) | (wc << 29), hi.x, hi.y, hi.z);
     x.hc1 = want_plus;
-    x.c1 = mk_item(it.a.z, nmeta | (prec.w << 25) | (1u << 29), prec.x, prec.y, prec.z);
+    x.c1 = mk_item(it.a.z, nmeta | ((prec.w & F_BASIC) << 25) | (1u << 29), prec.x, prec.y, prec.z);
   } else {
     x.h1 = atend && (fl & F_TERM);
     if (atend) return;
@@ -310,10 +477,10 @@ __device__ __forceinline__ void expand(const DevTable& tab, int mode, const Item
     uint4 lo, hi;
     if (child != NONE) {
       const uint4 r = ld16(tab.nodes + child);
-      x.c0 = mk_item(child, nmeta | (r.w << 25), r.x, r.y, r.z);
+      x.c0 = mk_item(child, nmeta | ((r.w & F_BASIC) << 25), r.x, r.y, r.z);
       x.hc0 = true;
     } else if (w < WID_MAX && edge_probe(tab, node, w, &lo, &hi)) {
-      x.c0 = mk_item(lo.z, nmeta | (lo.w << 25), hi.x, hi.y, hi.z);
+      x.c0 = mk_item(lo.z, nmeta | ((lo.w & F_BASIC) << 25), hi.x, hi.y, hi.z);
       x.hc0 = true;
     }
   }
@@ -529,6 +696,9 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Wave
   uint32_t nw = p.nw;
   if (!staged) nw = leaf ? WID_NONE : w.wid[L.tbase[tt] + nl];
   const uint32_t base_meta = nl | (tt << MT_SHIFT);
+  // the literal probe of a child is only worth a read if its signature has
+  // the next word's bit (egm_common.h)
+  const uint32_t nsig = nw < WID_MAX ? sig_bit(nw) : 0u;
   if (p.lit) {
     // pick the matching slot's fields with masks, not a select of the two
     // loaded slots: LLVM folds the latter into a phi of addresses into the
@@ -558,8 +728,9 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Wave
       o.f0 = hy;
       o.e1 = leaf && (cw & F_TERM) && (mode == MODE_ROUTES || wc || (D == 1 && (tf & TF_DOLLAR)));
       o.f1 = hz;
-      o.p0 = !leaf && (cw & (F_LIT | F_PLUS));
-      o.c0 = make_uint4(cz, base_meta | (cw << MF_SHIFT) | (wc << MW_SHIFT), hx, nw);
+      const uint32_t go = (cw & F_PLUS) | ((cw & nsig) ? (cw & F_LIT) : 0u);
+      o.p0 = !leaf && go;
+      o.c0 = make_uint4(cz, base_meta | (go << MF_SHIFT) | (wc << MW_SHIFT), hx, nw);
     }
   }
   if (p.plus) {
@@ -569,8 +740,9 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Wave
     o.f2 = p.prec.y;
     o.e3 = leaf && (pf & F_TERM);
     o.f3 = p.prec.z;
-    o.p1 = !leaf && (pf & (F_LIT | F_PLUS));
-    o.c1 = make_uint4(p.it.z, base_meta | (pf << MF_SHIFT) | (1u << MW_SHIFT), p.prec.x, nw);
+    const uint32_t go = (pf & F_PLUS) | ((pf & nsig) ? (pf & F_LIT) : 0u);
+    o.p1 = !leaf && go;
+    o.c1 = make_uint4(p.it.z, base_meta | (go << MF_SHIFT) | (1u << MW_SHIFT), p.prec.x, nw);
   }
 }
 
@@ -683,9 +855,11 @@ EGM_FOR_U(
               em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
               fid = root.y;
               created += 1;
-              const uint32_t fl = root.w & (F_LIT | (dollar ? 0u : F_PLUS));
-              has = (fl & (F_LIT | F_PLUS)) != 0;
-              it = make_uint4(0, (j << MT_SHIFT) | (fl << MF_SHIFT), root.x, word_at(L, w, staged, j, 0));
+              const uint32_t w0 = word_at(L, w, staged, j, 0);
+              const uint32_t s0 = w0 < WID_MAX ? sig_bit(w0) : 0u;
+              const uint32_t fl = (dollar ? 0u : (root.w & F_PLUS)) | ((root.w & s0) ? (root.w & F_LIT) : 0u);
+              has = fl != 0;
+              it = make_uint4(0, (j << MT_SHIFT) | (fl << MF_SHIFT), root.x, w0);
             }
           }
           const uint64_t b = __ballot(has);

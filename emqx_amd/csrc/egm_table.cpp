@@ -76,6 +76,7 @@ void HostTable::clear() {
   via_.clear();
   ref_.clear();
   lit_count_.clear();
+  sig_.clear();
   edge_slot_.clear();
   free_nodes_.clear();
   n_live_nodes_ = 0;
@@ -109,6 +110,7 @@ uint32_t HostTable::new_node(uint32_t parent, uint32_t via) {
     via_.push_back(NONE);
     ref_.push_back(0);
     lit_count_.push_back(0);
+    sig_.push_back(0);
     edge_slot_.push_back(NONE);
   }
   nodes[n] = NodeRec{NONE, NONE, NONE, 0};
@@ -117,6 +119,7 @@ uint32_t HostTable::new_node(uint32_t parent, uint32_t via) {
   via_[n] = via;
   ref_[n] = 0;
   lit_count_[n] = 0;
+  sig_[n] = 0;
   edge_slot_[n] = NONE;
   ++n_live_nodes_;
   return n;
@@ -134,7 +137,7 @@ void HostTable::free_node(uint32_t n) {
 
 uint32_t HostTable::own_flags(uint32_t n) const {
   const NodeRec& r = nodes[n];
-  return (lit_count_[n] ? F_LIT : 0u) | (r.plus_child != NONE ? F_PLUS : 0u) |
+  return (lit_count_[n] ? F_LIT | sig_[n] : 0u) | (r.plus_child != NONE ? F_PLUS : 0u) |
          (r.hash_fid != NONE ? F_HASH : 0u) | (r.term_fid != NONE ? F_TERM : 0u);
 }
 
@@ -312,6 +315,7 @@ int HostTable::insert(const uint8_t* p, uint32_t len, uint32_t fid, uint32_t* ou
         s = edge_insert(cur, wid, c, 0);
         edge_slot_[c] = s;
         ++lit_count_[cur];
+        sig_[cur] |= sig_bit(wid);
         update_flags(cur);
       } else {
         c = edges[s].child;
@@ -435,6 +439,8 @@ void HostTable::relayout() {
     nref[i] = ref_[o];
     nlit[i] = lit_count_[o];
   }
+  std::vector<uint32_t>().swap(sig_);
+  sig_.assign(L, 0);
   nodes.swap(nn);
   hash_child.swap(nhc);
   parent_.swap(npar);
@@ -461,7 +467,11 @@ void HostTable::relayout() {
     s.child = newid[s.child];
   }
   std::sort(live.begin(), live.end(), [](const EdgeSlot& a, const EdgeSlot& b) { return a.child < b.child; });
-  for (const EdgeSlot& s : live) edge_slot_[s.child] = edge_insert(s.parent, s.wid, s.child, s.child_flags);
+  // exact literal-child signatures, then every record and slot copy refreshed
+  for (const EdgeSlot& s : live) sig_[s.parent] |= sig_bit(s.wid);
+  for (uint32_t n = 0; n < L; ++n) nodes[n].flags = own_flags(n);
+  for (const EdgeSlot& s : live)
+    edge_slot_[s.child] = edge_insert(s.parent, s.wid, s.child, nodes[s.child].flags);
 }
 
 }  // namespace egm

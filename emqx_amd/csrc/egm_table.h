@@ -74,7 +74,7 @@ class HostTable {
 
  private:
   // host-only per-node bookkeeping
-  std::vector<uint32_t> parent_, via_, ref_, lit_count_, edge_slot_;
+  std::vector<uint32_t> parent_, via_, ref_, lit_count_, edge_slot_, sig_;
   std::vector<uint32_t> free_nodes_;
   uint32_t n_live_nodes_ = 0;
   uint64_t n_edges_ = 0, n_edge_tombs_ = 0;
