@@ -56,14 +56,14 @@ def build_lib(verbose=False, force=False) -> str:
     hip_src = os.path.join(CSRC, "egm_kernels.hip")
     o = os.path.join(BUILD, "egm_kernels.o")
     if force or _stale(o, [hip_src] + HEADERS):
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall",
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result", "-Wno-unused-value",
               "-c", hip_src, "-o", o], verbose)
     objs.append(o)
     for name in ("egm_table.cpp", "egm_capi.cpp"):
         src = os.path.join(CSRC, name)
         o = os.path.join(BUILD, name.replace(".cpp", ".o"))
         if force or _stale(o, [src] + HEADERS):
-            _run(["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__",
+            _run(["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result", "-Wno-unused-value", "-D__HIP_PLATFORM_AMD__",
                   f"-I{ROCM}/include", "-c", src, "-o", o], verbose)
         objs.append(o)
     if force or _stale(LIB, objs + [os.path.abspath(__file__)]):

@@ -34,11 +34,11 @@ constexpr int MODE_ROUTES = 1;
 #endif
 constexpr int WALK_WAVES = EGM_WALK_WAVES;
 #ifndef EGM_WALK_STACK
-#define EGM_WALK_STACK 384   // items per wave (16 B each)
+#define EGM_WALK_STACK 320   // items per wave (16 B each)
 #endif
 constexpr int WALK_STACK = EGM_WALK_STACK;
 #ifndef EGM_WALK_STAGE
-#define EGM_WALK_STAGE 384   // staged matches per flush (7 B each)
+#define EGM_WALK_STAGE 320   // staged matches per flush (7 B each)
 #endif
 constexpr int WALK_STAGE = EGM_WALK_STAGE;
 #ifndef EGM_WALK_IPL
@@ -46,7 +46,7 @@ constexpr int WALK_STAGE = EGM_WALK_STAGE;
 #endif
 constexpr int WALK_IPL = EGM_WALK_IPL;
 #ifndef EGM_WALK_WORDS
-#define EGM_WALK_WORDS 512   // staged topic word ids per wave chunk
+#define EGM_WALK_WORDS 448   // staged topic word ids per wave chunk
 #endif
 constexpr int WALK_WORDS = EGM_WALK_WORDS;
 constexpr int HEAVY_STACK = 6144;    // items (120 KB LDS) per heavy wave
@@ -507,7 +507,7 @@ constexpr uint32_t MF_SHIFT = 24;
 constexpr uint32_t MW_SHIFT = 28;
 constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 constexpr uint32_t T_BITS = WALK_CHUNK <= 64 ? 6 : 7;
-static_assert(WALK_CHUNK <= 128, "t field is 7 bits");
+static_assert(WALK_CHUNK == 64, "one topic per lane in the chunk prologue");
 
 struct alignas(16) WaveLds {
   uint4 stack[WALK_STACK];
@@ -651,10 +651,8 @@ struct Out {
   uint32_t created;         // states created (instrumentation: SURVEY §8d V_t)
 };
 
-__device__ __forceinline__ uint32_t word_at(const WaveLds& L, const MatchWork& w, bool staged, uint32_t tt,
-                                            uint32_t level) {
-  if (staged) return L.words[min(L.tbase[tt] + level, (uint32_t)WALK_WORDS - 1)];
-  return w.wid[L.tbase[tt] + level];
+__device__ __forceinline__ uint32_t word_at(const WaveLds& L, uint32_t tt, uint32_t level) {
+  return L.words[min(L.tbase[tt] + level, (uint32_t)WALK_WORDS - 1)];
 }
 
 // Branch-free on purpose: every lane issues its loads unconditionally (an
@@ -662,7 +660,7 @@ __device__ __forceinline__ uint32_t word_at(const WaveLds& L, const MatchWork& w
 // inside an `if` makes LLVM merge its result at the end of the block, and
 // the copy it inserts there waits for the load — the second item's reads
 // would then only be issued after the first item's had returned.
-__device__ __forceinline__ void issue(const DevTable& tab, const WaveLds& L, bool staged, uint32_t ws, Pend& p) {
+__device__ __forceinline__ void issue(const DevTable& tab, const WaveLds& L, Pend& p) {
   const uint32_t meta = p.it.y;
   const uint32_t fl = (meta >> MF_SHIFT) & 0xFu;
   p.plus = p.act && (fl & F_PLUS);
@@ -674,16 +672,14 @@ __device__ __forceinline__ void issue(const DevTable& tab, const WaveLds& L, boo
   p.h0 = ld16(bp + 16);
   p.l1 = ld16(bp + 32);
   p.h1 = ld16(bp + 48);
-  // LDS reads overlapping the global ones: the topic's info and, when the
-  // words are staged, the next level's word (clamped; used only if level+1 < D)
+  // LDS reads overlapping the global ones: the topic's info and the next
+  // level's word (clamped; used only if level + 1 < D)
   const uint32_t tt = (meta >> MT_SHIFT) & 0x7Fu, level = meta & LEVEL_MAX;
   p.ti = L.tinfo[tt];
-  p.nw = L.words[min(tt * ws + level + 1, (uint32_t)WALK_WORDS - 1)];
-  (void)staged;
+  p.nw = word_at(L, tt, level + 1);
 }
 
-__device__ __forceinline__ void finish(const DevTable& tab, int mode, const WaveLds& L, const MatchWork& w,
-                                       bool staged, Pend& p, Out& o) {
+__device__ __forceinline__ void finish(const DevTable& tab, int mode, Pend& p, Out& o) {
   o.e0 = o.e1 = o.e2 = o.e3 = o.p0 = o.p1 = false;
   o.created = 0;
   if (!p.act) return;
@@ -693,8 +689,7 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Wave
   const uint32_t D = p.ti & 0xFFFFFFu, tf = p.ti >> 24;
   const uint32_t nl = level + 1;
   const bool leaf = nl == D;
-  uint32_t nw = p.nw;
-  if (!staged) nw = leaf ? WID_NONE : w.wid[L.tbase[tt] + nl];
+  const uint32_t nw = p.nw;
   const uint32_t base_meta = nl | (tt << MT_SHIFT);
   // the literal probe of a child is only worth a read if its signature has
   // the next word's bit (egm_common.h)
@@ -750,11 +745,10 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Wave
 // 129-134): the topic's words walked as a literal key, '+'/'#' words taking
 // the '+'/'#' edges.  Rare (MQTT publishes never carry wildcards): one lane,
 // one dependent read per level.
-__device__ bool exact_walk(const DevTable& tab, const WaveLds& L, const MatchWork& w, bool staged, uint32_t j,
-                           uint32_t D, uint32_t* fid) {
+__device__ bool exact_walk(const DevTable& tab, const WaveLds& L, uint32_t j, uint32_t D, uint32_t* fid) {
   uint32_t node = 0;
   for (uint32_t l = 0; l < D; ++l) {
-    const uint32_t wd = word_at(L, w, staged, j, l);
+    const uint32_t wd = word_at(L, j, l);
     uint32_t child = NONE;
     if (wd == WID_PLUS) child = tab.nodes[node].plus_child;
     else if (wd == WID_HASH) child = tab.hash_child[node];
@@ -783,173 +777,209 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
   Slab sid{0, 0}, spc{0, 0};
   constexpr uint32_t POP = 64u * WALK_IPL;
 
+#ifdef EGM_XCD_MAP
+  // blocks are dealt round-robin to the 8 XCDs: give XCD x the contiguous
+  // x-th eighth of the chunks, so neighbouring topics share one L2
+  const uint32_t xcd = blockIdx.x & 7u, nslot = gridDim.x >> 3;
+  const uint32_t c_lo = (uint32_t)((uint64_t)nchunks * xcd / 8), c_hi = (uint32_t)((uint64_t)nchunks * (xcd + 1) / 8);
+  for (uint32_t c = c_lo + (blockIdx.x >> 3) * WALK_WAVES + wave; c < c_hi; c += nslot * WALK_WAVES) {
+#else
   for (uint32_t c = blockIdx.x * WALK_WAVES + wave; c < nchunks; c += nwaves) {
+#endif
     const uint32_t t0 = c * WALK_CHUNK;
     const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
 
-    // ---- topic info; words staged as [topic][level] with a chunk-wide stride ----
+    // ---- topic info (lane j: topic t0 + j) ----
     uint32_t dmax = 0;
-    uint32_t dl[WALK_CHUNK / 64];
-#pragma unroll
-    for (int k = 0; k < WALK_CHUNK / 64; ++k) {
-      const uint32_t j = lane + 64 * k;
+    {
       uint32_t D = 0, f = 0;
-      if (j < nt) {
-        D = w.lv[t0 + j];
-        f = w.tfl[t0 + j];
+      if (lane < nt) {
+        D = w.lv[t0 + lane];
+        f = w.tfl[t0 + lane];
       }
-      dl[k] = D;
-      dmax = max(dmax, D);
-      L.tinfo[j] = D | (f << 24);
-      L.cnt[j] = 0;
-      L.fcnt[j] = 0;
+      dmax = D;
+      L.tinfo[lane] = D | (f << 24);
+      L.cnt[lane] = 0;
+      L.fcnt[lane] = 0;
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, d, 64));
-    const uint32_t ws = dmax;   // stride of words[t][level]
-    const bool staged = (uint64_t)ws * WALK_CHUNK <= (uint64_t)WALK_WORDS;
-#pragma unroll
-    for (int k = 0; k < WALK_CHUNK / 64; ++k) {
-      const uint32_t j = lane + 64 * k;
-      if (j < nt) {
-        const uint32_t gb = off[t0 + j] + t0 + j;
-        L.tbase[j] = staged ? j * ws : gb;
-        if (staged) {
-          const uint32_t* src = w.wid + gb;
-          uint32_t* dst = L.words + j * ws;
-          uint32_t i = 0;
-          for (; i + 4 <= dl[k]; i += 4) {
-            uint32_t a0 = src[i], a1 = src[i + 1], a2 = src[i + 2], a3 = src[i + 3];
-            dst[i] = a0;
-            dst[i + 1] = a1;
-            dst[i + 2] = a2;
-            dst[i + 3] = a3;
-          }
-          for (; i < dl[k]; ++i) dst[i] = src[i];
-        }
+    // Words are always staged in LDS as [topic][level] (finish() must not
+    // load from global memory, see issue()): a chunk of deep topics is walked
+    // as sub-chunks of S topics with S * dmax <= WALK_WORDS.  Topics deeper
+    // than WALK_WORDS levels go to the heavy kernel.
+    uint32_t S = WALK_CHUNK;
+    while (S > 1 && S * dmax > (uint32_t)WALK_WORDS) S >>= 1;
+    uint32_t sp = 0, nstage = 0;
+    bool ovf = (w.debug & DEBUG_FORCE_HEAVY) != 0 || dmax > (uint32_t)WALK_WORDS;
+    wave_sync();
+    for (uint32_t sub = 0; sub < nt && !ovf; sub += S) {
+    const uint32_t end = min(sub + S, nt);
+    if (lane < end - sub) {
+      const uint32_t j = sub + lane, D = L.tinfo[j] & 0xFFFFFFu;
+      const uint32_t* src = w.wid + off[t0 + j] + t0 + j;
+      uint32_t* dst = L.words + lane * dmax;
+      L.tbase[j] = lane * dmax;
+      uint32_t i = 0;
+      for (; i + 4 <= D; i += 4) {
+        uint32_t a0 = src[i], a1 = src[i + 1], a2 = src[i + 2], a3 = src[i + 3];
+        dst[i] = a0;
+        dst[i + 1] = a1;
+        dst[i + 2] = a2;
+        dst[i + 3] = a3;
       }
+      for (; i < D; ++i) dst[i] = src[i];
     }
     wave_sync();
+    uint32_t next = sub;
 
-    uint32_t next = 0, sp = 0, nstage = 0;
-    bool ovf = (w.debug & DEBUG_FORCE_HEAVY) != 0;
-    for (; !ovf;) {
-      if (sp < POP && next < nt) {  // admit new topics: emit their root '#', push their roots
-        const uint32_t k = min(POP - sp, nt - next);
-        if (nstage + POP > (uint32_t)WALK_STAGE) {
-          flush_stage(L, nstage, t0, lane, w, sid, spc);
-          nstage = 0;
-        }
-EGM_FOR_U(
-          const uint32_t r = u * 64 + lane;
-          bool has = false, em = false;
-          uint32_t fid = NONE;
-          uint4 it = make_uint4(0, 0, 0, 0);
-          const uint32_t j = next + r;
-          if (r < k) {
-            const uint32_t ti = L.tinfo[j], D = ti & 0xFFFFFFu, tf = ti >> 24;
-            if (tf & TF_WILDCARD) {
-              if (mode == MODE_ROUTES) em = exact_walk(tab, L, w, staged, j, D, &fid);
-            } else if (D <= LEVEL_MAX) {
-              const bool dollar = (tf & TF_DOLLAR) != 0;
-              em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
-              fid = root.y;
-              created += 1;
-              const uint32_t w0 = word_at(L, w, staged, j, 0);
-              const uint32_t s0 = w0 < WID_MAX ? sig_bit(w0) : 0u;
-              const uint32_t fl = (dollar ? 0u : (root.w & F_PLUS)) | ((root.w & s0) ? (root.w & F_LIT) : 0u);
-              has = fl != 0;
-              it = make_uint4(0, (j << MT_SHIFT) | (fl << MF_SHIFT), root.x, w0);
-            }
-          }
-          const uint64_t b = __ballot(has);
-          if (has) L.stack[sp + mbcnt(b)] = it;
-          sp += popc(b);
-          const uint64_t be = __ballot(em);
-          if (em) {
-            const uint32_t q = nstage + mbcnt(be);
-            L.stage_fid[q] = fid;
-            L.stage_t[q] = (uint8_t)j;
-          }
-          nstage += popc(be);
-        );
-        next += k;
-        wave_sync();
-      }
+// Admit new topics while the stack is short: emit their root '#', push their
+// roots (wildcard topics in ROUTES mode: one exact lookup, no push).
+#define WALK_REFILL()                                                                                  \
+    if (sp < 64u && next < end) {                                                                      \
+      const uint32_t k = min(64u - sp, end - next);                                                    \
+      if (nstage + 64u > (uint32_t)WALK_STAGE) {                                                       \
+        flush_stage(L, nstage, t0, lane, w, sid, spc);                                                 \
+        nstage = 0;                                                                                    \
+      }                                                                                                \
+      bool has = false, em = false;                                                                    \
+      uint32_t fid = NONE;                                                                             \
+      uint4 it = make_uint4(0, 0, 0, 0);                                                               \
+      const uint32_t j = next + lane;                                                                  \
+      if (lane < k) {                                                                                  \
+        const uint32_t ti = L.tinfo[j], D = ti & 0xFFFFFFu, tf = ti >> 24;                             \
+        if (tf & TF_WILDCARD) {                                                                        \
+          if (mode == MODE_ROUTES) em = exact_walk(tab, L, j, D, &fid);                     \
+        } else if (D <= LEVEL_MAX) {                                                                   \
+          const bool dollar = (tf & TF_DOLLAR) != 0;                                                   \
+          em = (root.w & F_HASH) && !dollar; /* filter '#': never for a '$' topic */                   \
+          fid = root.y;                                                                                \
+          created += 1;                                                                                \
+          const uint32_t w0 = word_at(L, j, 0);                                             \
+          const uint32_t s0 = w0 < WID_MAX ? sig_bit(w0) : 0u;                                         \
+          const uint32_t fl = (dollar ? 0u : (root.w & F_PLUS)) | ((root.w & s0) ? (root.w & F_LIT) : 0u); \
+          has = fl != 0;                                                                               \
+          it = make_uint4(0, (j << MT_SHIFT) | (fl << MF_SHIFT), root.x, w0);                          \
+        }                                                                                              \
+      }                                                                                                \
+      const uint64_t b = __ballot(has);                                                                \
+      if (has) L.stack[sp + mbcnt(b)] = it;                                                            \
+      sp += popc(b);                                                                                   \
+      const uint64_t be = __ballot(em);                                                                \
+      if (em) {                                                                                        \
+        const uint32_t q = nstage + mbcnt(be);                                                         \
+        L.stage_fid[q] = fid;                                                                          \
+        L.stage_t[q] = (uint8_t)j;                                                                     \
+      }                                                                                                \
+      nstage += popc(be);                                                                              \
+      next += k;                                                                                       \
+      wave_sync();                                                                                     \
+    }
+
+// Pop up to 64 items (one per lane) and issue all their reads.
+#define WALK_POP(P, TAKE)                                                                              \
+    {                                                                                                  \
+      const uint32_t take_ = min(64u, sp), bi_ = sp - take_;                                           \
+      P.act = lane < take_;                                                                            \
+      P.it = L.stack[min(bi_ + lane, (uint32_t)WALK_STACK - 1)]; /* unconditional: see issue() */     \
+      sp = bi_;                                                                                        \
+      TAKE = take_;                                                                                    \
+      iters += take_ ? 1u : 0u;                                                                        \
+      popped += take_;                                                                                 \
+      issue(tab, L, P);                                                                    \
+    }
+
+// Consume a popped batch's reads: children -> stack (counted first: an
+// overflow abandons the chunk), emits -> stage (flushed when full).
+#define WALK_RETIRE(P)                                                                                 \
+    {                                                                                                  \
+      Out o;                                                                                           \
+      finish(tab, mode, P, o);                                                           \
+      created += o.created;                                                                            \
+      const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);                                       \
+      const uint32_t m0 = popc(c0b), nc = m0 + popc(c1b);                                              \
+      if (sp + nc > (uint32_t)WALK_STACK) {                                                            \
+        ovf = true;                                                                                    \
+      } else {                                                                                         \
+        if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;                                                     \
+        if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;                                                \
+        sp += nc;                                                                                      \
+        const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1);                                       \
+        const uint64_t b2 = __ballot(o.e2), b3 = __ballot(o.e3);                                       \
+        const uint32_t n0 = popc(b0), n1 = popc(b1), n2 = popc(b2);                                    \
+        const uint32_t ne = n0 + n1 + n2 + popc(b3);                                                   \
+        if (nstage + ne > (uint32_t)WALK_STAGE) {                                                      \
+          wave_sync();                                                                                 \
+          flush_stage(L, nstage, t0, lane, w, sid, spc);                                               \
+          nstage = 0;                                                                                  \
+        }                                                                                              \
+        const uint8_t tt = (uint8_t)((P.it.y >> MT_SHIFT) & 0x7Fu);                                    \
+        if (o.e0) {                                                                                    \
+          const uint32_t q = nstage + mbcnt(b0);                                                       \
+          L.stage_fid[q] = o.f0;                                                                       \
+          L.stage_t[q] = tt;                                                                           \
+        }                                                                                              \
+        if (o.e1) {                                                                                    \
+          const uint32_t q = nstage + n0 + mbcnt(b1);                                                  \
+          L.stage_fid[q] = o.f1;                                                                       \
+          L.stage_t[q] = tt;                                                                           \
+        }                                                                                              \
+        if (o.e2) {                                                                                    \
+          const uint32_t q = nstage + n0 + n1 + mbcnt(b2);                                             \
+          L.stage_fid[q] = o.f2;                                                                       \
+          L.stage_t[q] = tt;                                                                           \
+        }                                                                                              \
+        if (o.e3) {                                                                                    \
+          const uint32_t q = nstage + n0 + n1 + n2 + mbcnt(b3);                                        \
+          L.stage_fid[q] = o.f3;                                                                       \
+          L.stage_t[q] = tt;                                                                           \
+        }                                                                                              \
+        nstage += ne;                                                                                  \
+      }                                                                                                \
+      wave_sync();                                                                                     \
+    }
+
+#ifdef EGM_WALK_PIPE
+    // Software pipeline over two batches A and B: the reads of the next batch
+    // are issued before the current one is retired.  (Measured: LLVM copies
+    // the loop-carried load results and waits for them right after issue, so
+    // this buys nothing today; kept for the A/B harness.)
+    Pend pa, pb;
+    uint32_t ta = 0, tb = 0;
+    if (!ovf) {
+      WALK_REFILL();
+      WALK_POP(pa, ta);
+    }
+    while (!ovf) {
+      WALK_REFILL();
+      WALK_POP(pb, tb);
+      wave_sync();
+      if (ta) WALK_RETIRE(pa);
+      if (ovf || (!tb && sp == 0 && next >= end)) break;
+      WALK_REFILL();
+      WALK_POP(pa, ta);
+      wave_sync();
+      if (tb) WALK_RETIRE(pb);
+      if (ovf || (!ta && sp == 0 && next >= end)) break;
+    }
+#else
+    while (!ovf) {
+      WALK_REFILL();
       if (sp == 0) {
-        if (next >= nt) break;
+        if (next >= end) break;
         continue;
       }
-      const uint32_t take = min(POP, sp);
-      const uint32_t bi = sp - take;
-      Pend p[WALK_IPL];
-EGM_FOR_U(
-        const uint32_t r = u * 64 + lane;
-        p[u].act = r < take;
-        p[u].it = L.stack[min(bi + r, (uint32_t)WALK_STACK - 1)];   // unconditional: see issue()
-      );
-      sp = bi;
-      iters += 1;
-      popped += take;
-      EGM_FOR_U(issue(tab, L, staged, ws, p[u]););
-      Out o[WALK_IPL];
-      EGM_FOR_U(finish(tab, mode, L, w, staged, p[u], o[u]); created += o[u].created;);
-
-      // children -> stack (all counted first: an overflow abandons the chunk)
-      uint64_t c0b[WALK_IPL], c1b[WALK_IPL];
-      uint32_t nc = 0;
-EGM_FOR_U(
-        c0b[u] = __ballot(o[u].p0);
-        c1b[u] = __ballot(o[u].p1);
-        nc += popc(c0b[u]) + popc(c1b[u]);
-      );
-      if (sp + nc > (uint32_t)WALK_STACK) {
-        ovf = true;
-        break;
-      }
-      wave_sync();   // the pops above read the slots the pushes below may overwrite
-EGM_FOR_U(
-        const uint32_t m0 = popc(c0b[u]);
-        if (o[u].p0) L.stack[sp + mbcnt(c0b[u])] = o[u].c0;
-        if (o[u].p1) L.stack[sp + m0 + mbcnt(c1b[u])] = o[u].c1;
-        sp += m0 + popc(c1b[u]);
-      );
-      // emits -> stage, flushed to global pieces whenever it would overflow
-EGM_FOR_U(
-        const uint64_t b0 = __ballot(o[u].e0), b1 = __ballot(o[u].e1);
-        const uint64_t b2 = __ballot(o[u].e2), b3 = __ballot(o[u].e3);
-        const uint32_t n0 = popc(b0), n1 = popc(b1), n2 = popc(b2);
-        const uint32_t ne = n0 + n1 + n2 + popc(b3);
-        if (nstage + ne > (uint32_t)WALK_STAGE) {
-          wave_sync();
-          flush_stage(L, nstage, t0, lane, w, sid, spc);
-          nstage = 0;
-        }
-        const uint8_t tt = (uint8_t)((p[u].it.y >> MT_SHIFT) & 0x7Fu);
-        if (o[u].e0) {
-          const uint32_t q = nstage + mbcnt(b0);
-          L.stage_fid[q] = o[u].f0;
-          L.stage_t[q] = tt;
-        }
-        if (o[u].e1) {
-          const uint32_t q = nstage + n0 + mbcnt(b1);
-          L.stage_fid[q] = o[u].f1;
-          L.stage_t[q] = tt;
-        }
-        if (o[u].e2) {
-          const uint32_t q = nstage + n0 + n1 + mbcnt(b2);
-          L.stage_fid[q] = o[u].f2;
-          L.stage_t[q] = tt;
-        }
-        if (o[u].e3) {
-          const uint32_t q = nstage + n0 + n1 + n2 + mbcnt(b3);
-          L.stage_fid[q] = o[u].f3;
-          L.stage_t[q] = tt;
-        }
-        nstage += ne;
-      );
+      Pend pa;
+      uint32_t ta;
+      WALK_POP(pa, ta);
       wave_sync();
+      WALK_RETIRE(pa);
     }
+#endif
+    }  // sub-chunks
+#undef WALK_REFILL
+#undef WALK_POP
+#undef WALK_RETIRE
     wave_sync();
 
     if (ovf) {  // frontier exceeded the LDS stack: hand the chunk to k_heavy
@@ -1167,12 +1197,23 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
 }
 
 // pieces -> CSR rows, no atomics: a piece knows its offset inside the row.
-// One lane per piece, four independent loads in flight per lane.  Light
-// pieces of topics re-run by k_heavy and unused slab slots are skipped.
-__global__ __launch_bounds__(256) void k_compact(const uint4* __restrict__ pieces, const uint8_t* __restrict__ tfl,
-                                                 const uint32_t* __restrict__ ids_tmp, uint32_t n,
-                                                 const uint64_t* __restrict__ row_ptr, uint32_t* __restrict__ ids,
-                                                 uint64_t ids_cap, uint64_t pieces_cap, MatchStats* stats) {
+// One wave per window of 64 pieces: lane k loads piece k and its row start,
+// a wave scan lays the window's ids out as one run [0, tot), and the lanes
+// copy that run with consecutive lanes on consecutive ids (a binary search
+// over the window's 64 scan values finds each id's piece).  The pieces of one
+// flush have contiguous sources and topics of one chunk, so the reads and the
+// row_ptr loads coalesce.  Light pieces of topics re-run by k_heavy and unused
+// slab slots (count 0) are skipped.
+constexpr int COMPACT_WAVES = 4;
+__global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __restrict__ pieces,
+                                                                const uint8_t* __restrict__ tfl,
+                                                                const uint32_t* __restrict__ ids_tmp, uint32_t n,
+                                                                const uint64_t* __restrict__ row_ptr,
+                                                                uint32_t* __restrict__ ids, uint64_t ids_cap,
+                                                                uint64_t pieces_cap, MatchStats* stats) {
+  __shared__ uint32_t s_scan[COMPACT_WAVES][64];
+  __shared__ uint32_t s_src[COMPACT_WAVES][64];
+  __shared__ uint64_t s_dst[COMPACT_WAVES][64];
   const uint64_t total = row_ptr[n];
   if (blockIdx.x == 0 && threadIdx.x == 0) stats->total_ids = total;
   if (stats->overflow) return;
@@ -1180,24 +1221,38 @@ __global__ __launch_bounds__(256) void k_compact(const uint4* __restrict__ piece
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, 2u);
     return;
   }
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t np = min((uint64_t)stats->pieces, pieces_cap);
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < np; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint4 pc = pieces[i];
-    const uint32_t c = pc.y & ~HEAVY_PIECE;
-    if (c == 0) continue;
-    const uint32_t t = pc.x;
-    if ((tfl[t] & TF_HEAVY) && !(pc.y & HEAVY_PIECE)) continue;
-    const uint32_t* src = ids_tmp + pc.z;
-    uint32_t* dst = ids + row_ptr[t] + pc.w;
-    uint32_t k = 0;
-    for (; k + 4 <= c; k += 4) {
-      const uint32_t a0 = src[k], a1 = src[k + 1], a2 = src[k + 2], a3 = src[k + 3];
-      dst[k] = a0;
-      dst[k + 1] = a1;
-      dst[k + 2] = a2;
-      dst[k + 3] = a3;
+  const uint64_t stride = (uint64_t)gridDim.x * COMPACT_WAVES * 64;
+  for (uint64_t w0 = ((uint64_t)blockIdx.x * COMPACT_WAVES + wave) * 64; w0 < np; w0 += stride) {
+    const uint64_t i = w0 + lane;
+    uint32_t c = 0, src = 0;
+    uint64_t dst = 0;
+    if (i < np) {
+      const uint4 pc = pieces[i];
+      c = pc.y & ~HEAVY_PIECE;
+      if (c && !((tfl[pc.x] & TF_HEAVY) && !(pc.y & HEAVY_PIECE))) {
+        src = pc.z;
+        dst = row_ptr[pc.x] + pc.w;
+      } else {
+        c = 0;
+      }
     }
-    for (; k < c; ++k) dst[k] = src[k];
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan(c, lane, &tot);
+    s_scan[wave][lane] = ex;
+    s_src[wave][lane] = src;
+    s_dst[wave][lane] = dst;
+    wave_sync();
+    for (uint32_t q = lane; q < tot; q += 64) {
+      uint32_t k = 0;
+#pragma unroll
+      for (uint32_t step = 32; step >= 1; step >>= 1)
+        if (s_scan[wave][k + step] <= q) k += step;
+      const uint32_t o = q - s_scan[wave][k];
+      ids[s_dst[wave][k] + o] = ids_tmp[s_src[wave][k] + o];
+    }
+    wave_sync();
   }
 }
 
@@ -1207,6 +1262,7 @@ int walk_grid_blocks(uint32_t n) {
   uint32_t blocks = (chunks + WALK_WAVES - 1) / WALK_WAVES;
   const uint32_t cap = 256 * 32 / WALK_WAVES;  // grid-stride beyond 32 waves per CU
   if (blocks > cap) blocks = cap;
+  blocks = (blocks + 7) & ~7u;                 // a multiple of the 8 XCDs (EGM_XCD_MAP)
   return blocks ? (int)blocks : 1;
 }
 
@@ -1239,7 +1295,7 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   if (ev_walk) hipEventRecord(ev_walk[1], s);
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
   scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);
-  hipLaunchKernelGGL(k_compact, dim3(8192), dim3(256), 0, s, w.pieces, w.tfl, w.ids_tmp, n, out.row_ptr, out.ids,
+  hipLaunchKernelGGL(k_compact, dim3(8192), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.tfl, w.ids_tmp, n, out.row_ptr, out.ids,
                      out.ids_cap, w.pieces_cap, w.stats);
   return hipGetLastError();
 }
