@@ -101,15 +101,26 @@ EGM_HD uint64_t mix64(uint64_t x) {   // murmur3 fmix64
   return x;
 }
 
-EGM_HD uint64_t fnv_step(uint64_t h, uint8_t b) { return (h ^ b) * FNV_PRIME; }
+// Word hash: 4-byte little-endian chunks, each folded in with one 64-bit
+// multiply (a quarter of byte-wise FNV-1a's serial multiplies); the tail chunk
+// is zero-padded and the length is mixed in last, so "ab" != "ab\0".
+EGM_HD uint64_t hash_chunk(uint64_t h, uint32_t c) { return (h ^ c) * FNV_PRIME; }
 
-EGM_HD uint64_t word_hash_finish(uint64_t fnv, uint32_t len) {
-  return mix64(fnv ^ ((uint64_t)len << 56));
+EGM_HD uint64_t word_hash_finish(uint64_t h, uint32_t len) {
+  return mix64(h ^ ((uint64_t)len << 56));
 }
 
 EGM_HD uint64_t word_hash(const uint8_t* p, uint32_t len) {
   uint64_t h = FNV_BASIS;
-  for (uint32_t i = 0; i < len; ++i) h = fnv_step(h, p[i]);
+  uint32_t i = 0;
+  for (; i + 4 <= len; i += 4)
+    h = hash_chunk(h, (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16) |
+                          ((uint32_t)p[i + 3] << 24));
+  if (i < len) {
+    uint32_t c = 0;
+    for (uint32_t k = 0; i + k < len; ++k) c |= (uint32_t)p[i + k] << (8 * k);
+    h = hash_chunk(h, c);
+  }
   return word_hash_finish(h, len);
 }
 

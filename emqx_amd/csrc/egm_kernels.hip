@@ -96,6 +96,15 @@ __device__ __forceinline__ uint32_t mk_meta(uint32_t level, uint32_t t, uint32_t
 
 __device__ __forceinline__ uint4 ld16(const void* p) { return *(const uint4*)p; }
 
+// An empty piece {NONE, 0, 0, 0}, materialised where it is stored: as a plain
+// constant LLVM hoists it out of every loop and pins four VGPRs for the whole
+// walk kernel.
+__device__ __forceinline__ uint4 empty_piece() {
+  uint32_t x = NONE, z = 0;
+  asm volatile("" : "+v"(x), "+v"(z));
+  return make_uint4(x, z, z, z);
+}
+
 // EGM_FOR_U(stmts): run stmts once per work item of a lane with a constant
 // index u (WALK_IPL <= 2).  A macro, not a lambda: arrays of per-item state
 // indexed by constants then stay in registers (a lambda capturing them by
@@ -152,49 +161,50 @@ __device__ __forceinline__ void tokenise_one(const DevTable& tab, const uint32_t
                                              uint32_t base, uint32_t* __restrict__ wid, uint32_t* lv_out,
                                              uint8_t* fl_out) {
   const uint8_t* p = (const uint8_t*)wp + mis;
-  uint32_t l = 0, ws = 0, cw = 0, cwi = 0xFFFFFFFFu;
-  uint32_t first = 0, wfirst = 0;
+  uint32_t l = 0, ws = 0;
   uint8_t fl = 0;
-  uint64_t h = FNV_BASIS;
   for (uint32_t i = 0; i <= len; ++i) {
-    uint32_t c = '/';
-    if (i < len) {
-      const uint32_t idx = mis + i;
-      if ((idx >> 2) != cwi) {
-        cwi = idx >> 2;
-        cw = wp[cwi];
-      }
-      c = (cw >> (8 * (idx & 3u))) & 0xFFu;
-      if (i == 0) first = c;
-      if (i == ws) wfirst = c;
-      if (c != '/') {
-        h = fnv_step(h, (uint8_t)c);
-        continue;
-      }
-    }
+    if (i < len && p[i] != '/') continue;
     const uint32_t wl = i - ws;
     uint32_t w;
-    if (wl == 1 && wfirst == '+') {
+    if (wl == 1 && p[ws] == '+') {
       w = WID_PLUS;
       fl |= TF_WILDCARD;
-    } else if (wl == 1 && wfirst == '#') {
+    } else if (wl == 1 && p[ws] == '#') {
       w = WID_HASH;
       fl |= TF_WILDCARD;
     } else {
-      w = dict_probe(tab, word_hash_finish(h, wl), p + ws, wl);
+      w = dict_probe(tab, word_hash(p + ws, wl), p + ws, wl);
     }
     wid[base + l] = w;
     ++l;
     ws = i + 1;
-    h = FNV_BASIS;
   }
-  if (len > 0 && first == '$') fl |= TF_DOLLAR;
+  if (len > 0 && p[0] == '$') fl |= TF_DOLLAR;
   *lv_out = l;
   *fl_out = fl;
 }
 
 __device__ __forceinline__ uint32_t lds_byte(const uint32_t* sw, uint32_t i) {
   return (sw[i >> 2] >> (8 * (i & 3u))) & 0xFFu;
+}
+
+// The 4 bytes at LDS byte offset i (any alignment; reads up to one word past).
+__device__ __forceinline__ uint32_t lds_word(const uint32_t* sw, uint32_t i) {
+  const uint32_t lo = sw[i >> 2], hi = sw[(i >> 2) + 1];
+  return __builtin_amdgcn_alignbyte(hi, lo, i & 3u);
+}
+
+// Low n bytes of a word (n <= 4).
+__device__ __forceinline__ uint32_t low_bytes(uint32_t v, uint32_t n) {
+  return n >= 4 ? v : (v & ((1u << (8 * n)) - 1u));
+}
+
+// word_hash (egm_common.h) of the wl bytes at LDS offset st.
+__device__ __forceinline__ uint64_t lds_word_hash(const uint32_t* sw, uint32_t st, uint32_t wl) {
+  uint64_t h = FNV_BASIS;
+  for (uint32_t k = 0; k < wl; k += 4) h = hash_chunk(h, low_bytes(lds_word(sw, st + k), wl - k));
+  return word_hash_finish(h, wl);
 }
 
 // Mask (bit 7 of each byte) of the bytes of v equal to '/'.
@@ -220,7 +230,10 @@ __device__ __forceinline__ uint32_t dict_resolve(const DevTable& tab, uint64_t h
     if (a.x == (uint32_t)h && a.y == (uint32_t)(h >> 32) && a.w == len) {
       bool eq = true;
       if (len <= 16) {
-        for (uint32_t k = 0; k < len; ++k) eq &= byte_of(b, k) == lds_byte(sw, st + k);
+        const uint32_t bw[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k += 4)
+          if (k < len) eq &= low_bytes(lds_word(sw, st + k), len - k) == low_bytes(bw[k >> 2], len - k);
       } else {
         const uint8_t* q = tab.dict_blob + tab.dict_off[a.z];
         for (uint32_t k = 0; k < len; ++k) eq &= q[k] == lds_byte(sw, st + k);
@@ -247,7 +260,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
                                                         const uint32_t* __restrict__ off, uint32_t n,
                                                         uint32_t* __restrict__ wid, uint32_t* __restrict__ lv,
                                                         uint8_t* __restrict__ tfl) {
-  __shared__ __attribute__((aligned(16))) uint32_t sw[TOK_LDS / 4];
+  __shared__ __attribute__((aligned(16))) uint32_t sw[TOK_LDS / 4 + 1];   // +1: lds_word reads one word past
   __shared__ uint32_t wpos[TOK_WORDS];   // start | len << 16 (LDS byte index)
   __shared__ uint32_t wdst[TOK_WORDS];   // index into wid[]
   __shared__ uint8_t wtop[TOK_WORDS];    // topic within the block
@@ -352,9 +365,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
       const uint32_t pw = act[u] ? wpos[i] : 0u;
       st[u] = pw & 0xFFFFu;
       wl[u] = pw >> 16;
-      uint64_t x = FNV_BASIS;
-      for (uint32_t k = 0; k < wl[u]; ++k) x = fnv_step(x, (uint8_t)lds_byte(sw, st[u] + k));
-      h[u] = word_hash_finish(x, wl[u]);
+      h[u] = lds_word_hash(sw, st[u], wl[u]);
       spec[u] = false;
       res[u] = WID_NONE;
       if (wl[u] == 1) {
@@ -539,11 +550,13 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
   if (s.cur + need > s.end) {
     if (tail_fill)
       for (unsigned long long i = s.cur + lane; i < s.end && i < tail_cap; i += 64)
-        tail_fill[i] = make_uint4(NONE, 0, 0, 0);
+        tail_fill[i] = empty_piece();
     const unsigned long long sz = need > grain ? need : grain;
     unsigned long long b = 0;
     if (lane == 0) b = atomicAdd(counter, sz);
     b = __shfl(b, 0, 64);
+    b = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+        __builtin_amdgcn_readfirstlane((uint32_t)b);   // wave-uniform: keep it in SGPRs
     s.cur = b;
     s.end = b + sz;
   }
@@ -557,7 +570,12 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
 // with T_BITS ballots; one LDS add per topic per 64 entries), then scattered
 // into the wave's ids slab grouped by topic, one piece per topic present
 // carrying the topic's running count as its offset inside the CSR row.
-__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane,
+#ifdef EGM_FLUSH_NOINLINE   // a call: fewer live registers in the walk loop, a call frame in scratch
+#define EGM_FLUSH_INLINE __noinline__
+#else
+#define EGM_FLUSH_INLINE __forceinline__
+#endif
+__device__ EGM_FLUSH_INLINE void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane,
                                             const MatchWork& w, Slab& sid, Slab& spc) {
   for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {
     const uint32_t i = i0 + lane;
@@ -637,7 +655,7 @@ __device__ __forceinline__ bool edge_probe_from(const DevTable& tab, uint32_t b,
 // One popped item between issuing its reads and consuming them.
 struct Pend {
   uint4 it;                 // the item
-  uint32_t b, ti, nw;       // bucket, its topic's info, the word at level + 1
+  uint32_t ti, nw;          // its topic's info, the word at level + 1
   bool act, lit, plus;
   uint4 prec, l0, h0, l1, h1;
 };
@@ -665,9 +683,9 @@ __device__ __forceinline__ void issue(const DevTable& tab, const WaveLds& L, Pen
   const uint32_t fl = (meta >> MF_SHIFT) & 0xFu;
   p.plus = p.act && (fl & F_PLUS);
   p.lit = p.act && (fl & F_LIT) && p.it.w < WID_MAX;
-  p.b = edge_bucket(p.it.x, p.it.w, tab.edge_mask);
+  const uint32_t bkt = edge_bucket(p.it.x, p.it.w, tab.edge_mask);
   p.prec = ld16(tab.nodes + (p.plus ? p.it.z : 0u));
-  const uint8_t* bp = (const uint8_t*)(tab.edges + (size_t)(p.lit ? p.b : 0u) * EDGE_BUCKET);
+  const uint8_t* bp = (const uint8_t*)(tab.edges + (size_t)(p.lit ? bkt : 0u) * EDGE_BUCKET);
   p.l0 = ld16(bp);
   p.h0 = ld16(bp + 16);
   p.l1 = ld16(bp + 32);
@@ -710,7 +728,7 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, Pend& p, O
     bool found = m0 || m1;
     if (!m0 && !z0 && !m1 && !z1) {   // both first slots hold other keys: keep probing
       uint4 lo, hi;
-      found = edge_probe_from(tab, p.b, 2, node, p.it.w, &lo, &hi);
+      found = edge_probe_from(tab, edge_bucket(node, p.it.w, tab.edge_mask), 2, node, p.it.w, &lo, &hi);
       cz = lo.z;
       cw = lo.w;
       hx = hi.x;
@@ -764,14 +782,23 @@ __device__ bool exact_walk(const DevTable& tab, const WaveLds& L, uint32_t j, ui
   return (r.flags & F_TERM) != 0;
 }
 
-__global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const uint32_t* __restrict__ off,
+#ifdef EGM_WALK_MINW   // minimum waves per SIMD: caps the VGPRs (occupancy tuning)
+#define EGM_WALK_LB __launch_bounds__(64 * WALK_WAVES, EGM_WALK_MINW)
+#else
+#define EGM_WALK_LB __launch_bounds__(64 * WALK_WAVES)
+#endif
+__global__ EGM_WALK_LB void k_walk(DevTable tab, const uint32_t* __restrict__ off,
                                                           uint32_t n, int mode, MatchWork w) {
   __shared__ WaveLds lds_all[WALK_WAVES];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   WaveLds& L = lds_all[wave];
   const uint32_t nwaves = gridDim.x * WALK_WAVES;
   const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
-  const uint4 root = ld16(tab.nodes);
+  uint4 root = ld16(tab.nodes);   // wave-uniform: keep it in SGPRs
+  root.x = __builtin_amdgcn_readfirstlane(root.x);
+  root.y = __builtin_amdgcn_readfirstlane(root.y);
+  root.z = __builtin_amdgcn_readfirstlane(root.z);
+  root.w = __builtin_amdgcn_readfirstlane(root.w);
   uint32_t created = 0;
   unsigned long long iters = 0, popped = 0;
   Slab sid{0, 0}, spc{0, 0};
@@ -997,7 +1024,7 @@ __global__ __launch_bounds__(64 * WALK_WAVES) void k_walk(DevTable tab, const ui
     wave_sync();
   }
   for (unsigned long long i = spc.cur + lane; i < spc.end && i < w.pieces_cap; i += 64)
-    w.pieces[i] = make_uint4(NONE, 0, 0, 0);   // unused tail of the last pieces slab
+    w.pieces[i] = empty_piece();   // unused tail of the last pieces slab
   unsigned long long v = created;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -1244,13 +1271,24 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
     s_src[wave][lane] = src;
     s_dst[wave][lane] = dst;
     wave_sync();
-    for (uint32_t q = lane; q < tot; q += 64) {
-      uint32_t k = 0;
+    // four ids per lane per round: their searches, loads and stores overlap
+    for (uint32_t q0 = lane; q0 < tot; q0 += 256) {
+      uint32_t v[4];
+      uint64_t d[4];
 #pragma unroll
-      for (uint32_t step = 32; step >= 1; step >>= 1)
-        if (s_scan[wave][k + step] <= q) k += step;
-      const uint32_t o = q - s_scan[wave][k];
-      ids[s_dst[wave][k] + o] = ids_tmp[s_src[wave][k] + o];
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t q = min(q0 + 64u * r, tot - 1);
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t step = 32; step >= 1; step >>= 1)
+          if (s_scan[wave][k + step] <= q) k += step;
+        const uint32_t o = q - s_scan[wave][k];
+        d[r] = s_dst[wave][k] + o;
+        v[r] = ids_tmp[s_src[wave][k] + o];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (q0 + 64u * r < tot) ids[d[r]] = v[r];
     }
     wave_sync();
   }
