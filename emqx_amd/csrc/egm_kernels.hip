@@ -1250,26 +1250,24 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
   }
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t np = min((uint64_t)stats->pieces, pieces_cap);
-  const uint64_t stride = (uint64_t)gridDim.x * COMPACT_WAVES * 64;
-  for (uint64_t w0 = ((uint64_t)blockIdx.x * COMPACT_WAVES + wave) * 64; w0 < np; w0 += stride) {
+  const bool any_heavy = stats->n_deferred != 0;   // else no light piece can be stale
+  // a contiguous range of windows per wave (not a grid stride): the flushes
+  // of one chunk sit next to each other in pieces[], so one wave completes
+  // the cache lines of a chunk's rows
+  const uint64_t nwin = (np + 63) / 64, nw = (uint64_t)gridDim.x * COMPACT_WAVES;
+  const uint64_t per = (nwin + nw - 1) / nw, me = (uint64_t)blockIdx.x * COMPACT_WAVES + wave;
+  const uint64_t wend = min(nwin, (me + 1) * per) * 64;
+  for (uint64_t w0 = me * per * 64; w0 < wend; w0 += 64) {
     const uint64_t i = w0 + lane;
-    uint32_t c = 0, src = 0;
-    uint64_t dst = 0;
-    if (i < np) {
-      const uint4 pc = pieces[i];
-      c = pc.y & ~HEAVY_PIECE;
-      if (c && !((tfl[pc.x] & TF_HEAVY) && !(pc.y & HEAVY_PIECE))) {
-        src = pc.z;
-        dst = row_ptr[pc.x] + pc.w;
-      } else {
-        c = 0;
-      }
-    }
+    const uint4 pc = pieces[min(i, np - 1)];   // unconditional (a load under a branch is waited for at once)
+    uint32_t c = i < np ? (pc.y & ~HEAVY_PIECE) : 0u;
+    const uint64_t rp = row_ptr[c ? pc.x : 0u];
+    if (any_heavy && c && (tfl[pc.x] & TF_HEAVY) && !(pc.y & HEAVY_PIECE)) c = 0;
     uint32_t tot;
     const uint32_t ex = wave_excl_scan(c, lane, &tot);
     s_scan[wave][lane] = ex;
-    s_src[wave][lane] = src;
-    s_dst[wave][lane] = dst;
+    s_src[wave][lane] = pc.z;
+    s_dst[wave][lane] = rp + pc.w;
     wave_sync();
     // four ids per lane per round: their searches, loads and stores overlap
     for (uint32_t q0 = lane; q0 < tot; q0 += 256) {
