@@ -62,6 +62,24 @@ def levels_sum(blob: np.ndarray, off: np.ndarray) -> int:
     return int(np.count_nonzero(blob[:nbytes] == ord("/"))) + (len(off) - 1)
 
 
+def walk_traffic(config: str, filters: int, topics: int):
+    """HBM bytes per k_walk launch from the committed PMC record of this exact
+    workload (tools/pmc_traffic.py over rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes), or None.  bench.py cannot collect counters itself: PMC passes
+    need their own rocprofv3 runs."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_walk_pmc.json"))):
+        try:
+            with open(p) as fh:
+                r = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if r.get("workload") == config and r.get("filters") == filters and r.get("topics") == topics:
+            best = (r, os.path.relpath(p, ROOT))
+    return best
+
+
 def cpu_baseline(f, t, match_mode: int, seconds: float) -> dict:
     """C++ restatement of emqx_trie (compact) + route lookup, timed on host cores."""
     from oracle.cpp import OracleTrie
@@ -80,7 +98,14 @@ def cpu_baseline(f, t, match_mode: int, seconds: float) -> dict:
     t0 = time.time()
     m = o.match_count(sub.blob, sub.off, threads)
     dt = time.time() - t0
+    # one thread on a short prefix of the same sample (1 and N threads)
+    n1 = max(1, min(n, int(n / threads / 4)))
+    sub1 = t.subset(np.arange(n1))
+    t1 = time.time()
+    o.match_count(sub1.blob, sub1.off, 1)
+    dt1 = max(time.time() - t1, 1e-3)
     return {"value": n / dt, "unit": "topics/s", "cores": threads, "kind": "port",
+            "value_1thread": n1 / dt1, "sample_1thread": f"first {n1} topics, 1 thread",
             "sample": f"first {n} topics of the same batch, {threads} threads, static partition; "
                       f"C++ restatement of emqx_trie compact DFS + lookup_routes (oracle/trie_oracle.cpp), "
                       f"not BEAM; {m} matches; table build {build_s:.1f}s untimed",
@@ -240,6 +265,7 @@ def main():
     achieved = walk_bytes / (walk_ms * 1e-3) / 1e9
     path_bytes = (nbytes + 4 * n) + 16 * sum_d + 32 * visited + 4 * (n_ids + n)
 
+    traffic = walk_traffic(args.config, f.n, n) if args.mode == "replicate" or world == 1 else None
     if rank == 0:
         cpu = None
         if args.cpu_baseline == "auto" and world == 1:
@@ -255,7 +281,9 @@ def main():
                        else "emqx_trie:match", "parallelism": f"{args.mode}{world}",
                        "table": tstats},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic[0]["traffic_bytes_per_launch"] if traffic else None,
+                         "traffic_source": traffic[1] if traffic else None,
                          "kernel": "k_walk", "kernel_ms": walk_ms, "bytes_per_launch": walk_bytes,
                          "path_frac": path_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "stats": {"ids_per_step": n_ids, "visited_per_step": visited, "levels_per_step": sum_d,

@@ -63,6 +63,12 @@ class egm_image_view(C.Structure):
                 ("n_filters", C.c_uint64), ("n_live_nodes", C.c_uint64), ("n_edges", C.c_uint64)]
 
 
+class egm_dirty_view(C.Structure):
+    _fields_ = [("nodes", _u32p), ("n_nodes", C.c_uint64), ("edges", _u32p), ("n_edges", C.c_uint64),
+                ("dict", _u32p), ("n_dict", C.c_uint64), ("nodes_full", C.c_uint32),
+                ("edges_full", C.c_uint32), ("dict_full", C.c_uint32), ("words_full", C.c_uint32)]
+
+
 _P = C.c_void_p
 # name: (restype, argtypes) — every symbol the public header declares
 SIGNATURES = {
@@ -73,6 +79,7 @@ SIGNATURES = {
     "egm_table_build": (C.c_int, [_P, _P, _P, C.c_uint32, _P]),
     "egm_table_apply_delta": (C.c_int, [_P, C.POINTER(egm_delta), C.POINTER(egm_delta)]),
     "egm_table_commit": (C.c_int, [_P, _u64p]),
+    "egm_last_commit_stats": (C.c_int, [_P, _u64p, _u64p, _u64p, C.POINTER(C.c_double)]),
     "egm_table_empty": (C.c_int, [_P]),
     "egm_table_stats": (C.c_int, [_P, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "egm_filter_id": (C.c_int, [_P, _P, C.c_uint32, _u32p]),
@@ -94,6 +101,7 @@ SIGNATURES = {
     "egm_image_remove": (C.c_int, [_P, _P, C.c_uint32]),
     "egm_image_relayout": (None, [_P]),
     "egm_image_get_view": (C.c_int, [_P, C.POINTER(egm_image_view)]),
+    "egm_image_take_dirty": (C.c_int, [_P, C.POINTER(egm_dirty_view)]),
     "egm_shard_assign": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P]),
     "egm_word_hash": (C.c_uint64, [_P, C.c_uint32]),
     "egm_edge_bucket": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),

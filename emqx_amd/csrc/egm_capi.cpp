@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -51,21 +52,33 @@ struct DevBuf {
   T* as() const { return (T*)p; }
 };
 
-struct Epoch {
+// One device copy of the table image.  Two slots alternate: a commit writes
+// the slot that is NOT current, so batches still reading the current epoch are
+// never disturbed, and it brings that slot up to date with the records the
+// host changed since the slot was last written (its pending log + this
+// commit's) instead of re-uploading the whole image.
+struct Slot {
   DevBuf nodes, hash_child, edges, dict, dict_blob, dict_off;
+  uint64_t n_nodes = 0, n_hc = 0, n_edges = 0, n_dict = 0, n_blob = 0, n_off = 0;   // elements held
+  bool valid = false;
+  DirtyLog pending;                                          // host changes not yet applied here
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;      // last reading launch per stream
+  uint64_t bytes() const {
+    return nodes.cap + hash_child.cap + edges.cap + dict.cap + dict_blob.cap + dict_off.cap;
+  }
+};
+
+struct Epoch {
   DevTable view{};
+  int slot = 0;
   uint64_t id = 0;
   uint64_t n_filters = 0, n_nodes = 0, n_edges = 0, n_words = 0, bytes = 0;
 };
 
-template <class T>
-static hipError_t upload(DevBuf& b, const std::vector<T>& v) {
-  size_t bytes = v.size() * sizeof(T);
-  hipError_t e = b.ensure(bytes ? bytes : 16);
-  if (e != hipSuccess) return e;
-  if (bytes) e = hipMemcpy(b.p, v.data(), bytes, hipMemcpyHostToDevice);
-  return e;
-}
+struct CommitStats {
+  uint64_t h2d = 0, d2d = 0, patched = 0;
+  double ms = 0;
+};
 
 }  // namespace
 
@@ -76,6 +89,12 @@ struct egm_ctx {
   HostTable table;
   std::shared_ptr<Epoch> cur;
   uint64_t next_epoch = 1;
+  Slot slots[2];
+  int cur_slot = -1;
+  uint8_t* patch_host = nullptr;     // pinned staging of patch records
+  size_t patch_host_cap = 0;
+  DevBuf patch_dev;
+  CommitStats last_commit;
   std::string err;
 
   // per-batch workspace
@@ -147,36 +166,200 @@ static int set_device(egm_ctx* c) {
   return e == hipSuccess ? 0 : c->hip_fail(e, "hipSetDevice");
 }
 
-static int commit_locked(egm_ctx* c, uint64_t* epoch) {
-  auto ep = std::make_shared<Epoch>();
-  const HostTable& t = c->table;
+// Wait for every queued launch that reads slot x (it is about to be written).
+static void drain_slot(Slot& sl) {
+  for (auto& u : sl.uses) {
+    hipEventSynchronize(u.second);
+    hipEventDestroy(u.second);
+  }
+  sl.uses.clear();
+}
+
+static void note_use(egm_ctx* c, int slot, hipStream_t s) {
+  auto& u = c->slots[slot].uses;
+  for (auto& p : u)
+    if (p.first == s) {
+      hipEventRecord(p.second, s);
+      return;
+    }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return;
+  hipEventRecord(e, s);
+  u.push_back({s, e});
+}
+
+static void sort_unique(std::vector<uint32_t>& v) {
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+}
+
+// Bring one array of slot `dst` to the host image.  Preference order:
+//  1. patch in place: the slot holds the image minus `need` (its pending log
+//     plus this commit's), and it is big enough;
+//  2. device copy from the current slot (which lacks only this commit's
+//     changes `d`) followed by a patch of `d` — the slot was stale or too
+//     small, the changes were not a rebuild;
+//  3. whole upload from the host (rebuild: relayout, rehash, clear).
+// Returns the indices still to patch in *idx (sorted, unique).
+template <class T>
+static int sync_array(egm_ctx* c, DevBuf& dst, uint64_t& held, const DevBuf* src, uint64_t src_held,
+                      const std::vector<T>& host, bool need_full, bool d_full, const std::vector<uint32_t>& need,
+                      const std::vector<uint32_t>& d, uint64_t headroom, std::vector<uint32_t>* idx,
+                      const char* what) {
+  const uint64_t n = host.size(), sz = sizeof(T);
+  hipStream_t s = c->stream;
   hipError_t e;
-  if ((e = upload(ep->nodes, t.nodes)) != hipSuccess) return c->hip_fail(e, "upload nodes");
-  if ((e = upload(ep->hash_child, t.hash_child)) != hipSuccess) return c->hip_fail(e, "upload hash_child");
-  if ((e = upload(ep->edges, t.edges)) != hipSuccess) return c->hip_fail(e, "upload edges");
-  if ((e = upload(ep->dict, t.dict)) != hipSuccess) return c->hip_fail(e, "upload dict");
-  if ((e = upload(ep->dict_blob, t.dict_blob)) != hipSuccess) return c->hip_fail(e, "upload dict_blob");
-  if ((e = upload(ep->dict_off, t.dict_off)) != hipSuccess) return c->hip_fail(e, "upload dict_off");
-  ep->view.nodes = ep->nodes.as<NodeRec>();
-  ep->view.hash_child = ep->hash_child.as<uint32_t>();
-  ep->view.edges = ep->edges.as<EdgeSlot>();
+  idx->clear();
+  if (!need_full && held <= n && n * sz <= dst.cap && dst.p) {
+    *idx = need;
+  } else if (!d_full && src && src->p && src_held <= n) {
+    if ((e = dst.ensure((n + headroom) * sz)) != hipSuccess) return c->hip_fail(e, what);
+    if (src_held && (e = hipMemcpyAsync(dst.p, src->p, src_held * sz, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+      return c->hip_fail(e, what);
+    c->last_commit.d2d += src_held * sz;
+    *idx = d;
+    for (uint64_t i = src_held; i < n; ++i) idx->push_back((uint32_t)i);   // appended beyond the copy
+  } else {
+    if ((e = dst.ensure((n + headroom) * sz + 16)) != hipSuccess) return c->hip_fail(e, what);
+    if (n && (e = hipMemcpyAsync(dst.p, host.data(), n * sz, hipMemcpyHostToDevice, s)) != hipSuccess)
+      return c->hip_fail(e, what);
+    c->last_commit.h2d += n * sz;
+  }
+  sort_unique(*idx);
+  while (!idx->empty() && idx->back() >= n) idx->pop_back();
+  held = n;
+  return EGM_OK;
+}
+
+// Append-only arrays (dictionary words and their offsets): upload the tail.
+template <class T>
+static int sync_tail(egm_ctx* c, DevBuf& dst, uint64_t& held, const DevBuf* src, uint64_t src_held,
+                     const std::vector<T>& host, bool need_full, bool d_full, const char* what) {
+  const uint64_t n = host.size(), sz = sizeof(T);
+  hipStream_t s = c->stream;
+  hipError_t e;
+  uint64_t from;
+  if (!need_full && held <= n && n * sz <= dst.cap && dst.p) {
+    from = held;
+  } else if (!d_full && src && src->p && src_held <= n) {
+    if ((e = dst.ensure(n * sz + n * sz / 4 + 4096)) != hipSuccess) return c->hip_fail(e, what);
+    if (src_held && (e = hipMemcpyAsync(dst.p, src->p, src_held * sz, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+      return c->hip_fail(e, what);
+    c->last_commit.d2d += src_held * sz;
+    from = src_held;
+  } else {
+    if ((e = dst.ensure(n * sz + n * sz / 4 + 4096)) != hipSuccess) return c->hip_fail(e, what);
+    from = 0;
+  }
+  if (n > from) {
+    if ((e = hipMemcpyAsync((uint8_t*)dst.p + from * sz, host.data() + from, (n - from) * sz,
+                            hipMemcpyHostToDevice, s)) != hipSuccess)
+      return c->hip_fail(e, what);
+    c->last_commit.h2d += (n - from) * sz;
+  }
+  held = n;
+  return EGM_OK;
+}
+
+static uint8_t* patch_stage(egm_ctx* c, size_t bytes) {
+  if (bytes > c->patch_host_cap) {
+    if (c->patch_host) hipHostFree(c->patch_host);
+    c->patch_host = nullptr;
+    c->patch_host_cap = 0;
+    size_t want = bytes + bytes / 2 + 65536;
+    if (hipHostMalloc((void**)&c->patch_host, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+    c->patch_host_cap = want;
+  }
+  return c->patch_host;
+}
+
+// Publish the host table as a new epoch (egm_table_commit).
+static int commit_locked(egm_ctx* c, uint64_t* epoch) {
+  auto t0 = std::chrono::steady_clock::now();
+  c->last_commit = CommitStats{};
+  const HostTable& t = c->table;
+  DirtyLog d = c->table.take_dirty();
+  const int x = c->cur_slot < 0 ? 0 : 1 - c->cur_slot;
+  Slot& S = c->slots[x];
+  Slot* C = c->cur_slot < 0 ? nullptr : &c->slots[c->cur_slot];
+  drain_slot(S);
+  hipError_t e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return c->hip_fail(e, "commit: stream");
+  DirtyLog need = S.pending;
+  need.merge(d);
+  if (!S.valid) need.nodes_full = need.edges_full = need.dict_full = need.words_full = true;
+  // a failure below leaves S half-written: it stays invalid (full copy next time)
+  S.valid = false;
+  const uint64_t nn = t.nodes.size();
+  std::vector<uint32_t> in, ih, ie, id;
+  int r;
+  if ((r = sync_array(c, S.nodes, S.n_nodes, C ? &C->nodes : nullptr, C ? C->n_nodes : 0, t.nodes,
+                      need.nodes_full, d.nodes_full, need.nodes, d.nodes, nn / 8 + 4096, &in, "nodes")) ||
+      (r = sync_array(c, S.hash_child, S.n_hc, C ? &C->hash_child : nullptr, C ? C->n_hc : 0, t.hash_child,
+                      need.nodes_full, d.nodes_full, need.nodes, d.nodes, nn / 8 + 4096, &ih, "hash_child")) ||
+      (r = sync_array(c, S.edges, S.n_edges, C ? &C->edges : nullptr, C ? C->n_edges : 0, t.edges,
+                      need.edges_full, d.edges_full, need.edges, d.edges, 0, &ie, "edges")) ||
+      (r = sync_array(c, S.dict, S.n_dict, C ? &C->dict : nullptr, C ? C->n_dict : 0, t.dict, need.dict_full,
+                      d.dict_full, need.dict, d.dict, 0, &id, "dict")) ||
+      (r = sync_tail(c, S.dict_blob, S.n_blob, C ? &C->dict_blob : nullptr, C ? C->n_blob : 0, t.dict_blob,
+                     need.words_full, d.words_full, "dict_blob")) ||
+      (r = sync_tail(c, S.dict_off, S.n_off, C ? &C->dict_off : nullptr, C ? C->n_off : 0, t.dict_off,
+                     need.words_full, d.words_full, "dict_off")))
+    return r;
+  // pack {indices, records} of all four patched arrays into one pinned buffer
+  auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  const size_t o_in = 0, o_rn = al(o_in + in.size() * 4), o_ih = o_rn + in.size() * 16,
+               o_rh = al(o_ih + ih.size() * 4), o_ie = al(o_rh + ih.size() * 4), o_re = al(o_ie + ie.size() * 4),
+               o_id = o_re + ie.size() * 32, o_rd = al(o_id + id.size() * 4), total = o_rd + id.size() * 32;
+  const uint64_t np = in.size() + ih.size() + ie.size() + id.size();
+  if (np) {
+    uint8_t* h = patch_stage(c, total);
+    if (!h) return c->fail(EGM_E_NOMEM, "commit: pinned staging");
+    memcpy(h + o_in, in.data(), in.size() * 4);
+    memcpy(h + o_ih, ih.data(), ih.size() * 4);
+    memcpy(h + o_ie, ie.data(), ie.size() * 4);
+    memcpy(h + o_id, id.data(), id.size() * 4);
+    for (size_t i = 0; i < in.size(); ++i) memcpy(h + o_rn + i * 16, &t.nodes[in[i]], 16);
+    for (size_t i = 0; i < ih.size(); ++i) memcpy(h + o_rh + i * 4, &t.hash_child[ih[i]], 4);
+    for (size_t i = 0; i < ie.size(); ++i) memcpy(h + o_re + i * 32, &t.edges[ie[i]], 32);
+    for (size_t i = 0; i < id.size(); ++i) memcpy(h + o_rd + i * 32, &t.dict[id[i]], 32);
+    if ((e = c->patch_dev.ensure(total)) != hipSuccess) return c->hip_fail(e, "commit: patch buffer");
+    if ((e = hipMemcpyAsync(c->patch_dev.p, h, total, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "commit: patch upload");
+    c->last_commit.h2d += total;
+    uint8_t* dp = (uint8_t*)c->patch_dev.p;
+    if ((e = launch_patch(S.nodes.p, 16, (const uint32_t*)(dp + o_in), dp + o_rn, in.size(), c->stream)) ||
+        (e = launch_patch(S.hash_child.p, 4, (const uint32_t*)(dp + o_ih), dp + o_rh, ih.size(), c->stream)) ||
+        (e = launch_patch(S.edges.p, 32, (const uint32_t*)(dp + o_ie), dp + o_re, ie.size(), c->stream)) ||
+        (e = launch_patch(S.dict.p, 32, (const uint32_t*)(dp + o_id), dp + o_rd, id.size(), c->stream)))
+      return c->hip_fail(e, "commit: patch");
+    c->last_commit.patched = np;
+  }
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "commit: sync");
+  S.valid = true;
+  S.pending.clear();
+  if (C) C->pending.merge(d);   // the previous epoch's slot now lacks this commit's changes
+
+  auto ep = std::make_shared<Epoch>();
+  ep->slot = x;
+  ep->view.nodes = S.nodes.as<NodeRec>();
+  ep->view.hash_child = S.hash_child.as<uint32_t>();
+  ep->view.edges = S.edges.as<EdgeSlot>();
   ep->view.edge_mask = t.edge_mask();
-  ep->view.dict = ep->dict.as<DictSlot>();
+  ep->view.dict = S.dict.as<DictSlot>();
   ep->view.dict_mask = t.dict_mask();
-  ep->view.dict_blob = ep->dict_blob.as<uint8_t>();
-  ep->view.dict_off = ep->dict_off.as<uint64_t>();
+  ep->view.dict_blob = S.dict_blob.as<uint8_t>();
+  ep->view.dict_off = S.dict_off.as<uint64_t>();
   ep->n_filters = t.n_filters();
   ep->n_nodes = t.n_nodes_live();
   ep->n_edges = t.n_edges();
   ep->n_words = t.n_words();
-  ep->bytes = ep->nodes.cap + ep->hash_child.cap + ep->edges.cap + ep->dict.cap + ep->dict_blob.cap +
-              ep->dict_off.cap;
+  ep->bytes = S.bytes();
   ep->id = c->next_epoch++;
-  // readers holding the previous shared_ptr keep it alive until they finish;
-  // make sure no queued kernel still reads it before it can be freed
-  hipStreamSynchronize(c->stream);
   c->cur = ep;
+  c->cur_slot = x;
   if (epoch) *epoch = ep->id;
+  c->last_commit.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return EGM_OK;
 }
 
@@ -231,6 +414,7 @@ static int run_match(egm_ctx* c, const Epoch& ep, const uint8_t* d_blob, const u
     evp[1] = c->take_event();
   }
   hipError_t e = launch_match(ep.view, d_blob, d_off, n, mode, w, o, s, c->timing ? evp : nullptr);
+  note_use(c, ep.slot, s);   // a later commit must not overwrite this slot before the walk is done
   if (c->timing) {
     c->ev_walk.push_back(evp[0]);
     c->ev_walk.push_back(evp[1]);
@@ -297,6 +481,10 @@ void egm_close(egm_ctx* c) {
     c->drain_timing();
     for (hipEvent_t e : c->ev_free) hipEventDestroy(e);
     c->cur.reset();
+    drain_slot(c->slots[0]);
+    drain_slot(c->slots[1]);
+    if (c->patch_host) hipHostFree(c->patch_host);
+    c->patch_host = nullptr;
   }
   hipStreamDestroy(c->stream);
   delete c;
@@ -393,6 +581,17 @@ int egm_match_device(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, con
     hipError_t e = hipMemcpyAsync(d_flags, c->tfl.p, n, hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) return c->hip_fail(e, "flags copy");
   }
+  return EGM_OK;
+}
+
+int egm_last_commit_stats(egm_ctx* c, uint64_t* h2d_bytes, uint64_t* d2d_bytes, uint64_t* patched,
+                          double* ms) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (h2d_bytes) *h2d_bytes = c->last_commit.h2d;
+  if (d2d_bytes) *d2d_bytes = c->last_commit.d2d;
+  if (patched) *patched = c->last_commit.patched;
+  if (ms) *ms = c->last_commit.ms;
   return EGM_OK;
 }
 
@@ -656,6 +855,7 @@ void egm_result_free(void* r) { free(r); }
 // ---------------------------------------------------- host-only image API --
 struct egm_image {
   HostTable t;
+  DirtyLog d;   // the log egm_image_take_dirty last handed out
 };
 
 egm_image* egm_image_new(void) { return new (std::nothrow) egm_image(); }
@@ -670,6 +870,22 @@ int egm_image_remove(egm_image* im, const uint8_t* f, uint32_t len) {
 }
 void egm_image_relayout(egm_image* im) {
   if (im) im->t.relayout();
+}
+int egm_image_take_dirty(egm_image* im, egm_dirty_view* v) {
+  if (!im || !v) return EGM_E_INVAL;
+  im->d = im->t.take_dirty();
+  for (auto* x : {&im->d.nodes, &im->d.edges, &im->d.dict}) sort_unique(*x);
+  v->nodes = im->d.nodes.data();
+  v->n_nodes = im->d.nodes.size();
+  v->edges = im->d.edges.data();
+  v->n_edges = im->d.edges.size();
+  v->dict = im->d.dict.data();
+  v->n_dict = im->d.dict.size();
+  v->nodes_full = im->d.nodes_full;
+  v->edges_full = im->d.edges_full;
+  v->dict_full = im->d.dict_full;
+  v->words_full = im->d.words_full;
+  return EGM_OK;
 }
 int egm_image_get_view(egm_image* im, egm_image_view* v) {
   if (!im || !v) return EGM_E_INVAL;

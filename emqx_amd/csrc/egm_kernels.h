@@ -106,4 +106,9 @@ hipError_t launch_fanout(const SubTable& st, const uint64_t* match_row, const ui
                          uint32_t* deliv_sub, uint64_t deliv_cap, uint32_t* dcount, uint64_t* dpos,
                          uint64_t* tile_sums, unsigned int* overflow, hipStream_t s, hipEvent_t* ev);
 
+// Scatter n records of rec_bytes (4, 16 or 32) from src[] to dst[idx[i]]:
+// the incremental epoch commit of egm_capi.cpp.
+hipError_t launch_patch(void* dst, uint32_t rec_bytes, const uint32_t* idx, const void* src, uint64_t n,
+                        hipStream_t s);
+
 }  // namespace egm

@@ -1394,4 +1394,49 @@ hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_
   return hipGetLastError();
 }
 
+// -------------------------------------------------------------- table patch --
+// Incremental epoch commit: the records a batch of route
+// adds/deletes changed (emqx_router.erl:114-125,164-170 -> emqx_trie:insert/
+// delete, emqx_trie.erl:82-96) are packed on the host as {index, record} and
+// scattered into the device copy of the previous image.  One lane per
+// 16-byte piece of a record: a 32-B slot is two neighbouring lanes, so the
+// stores of a wave cover whole 64-B lines where the indices are adjacent.
+template <int Q>   // 16-byte quads per record
+__global__ __launch_bounds__(256) void k_patch(uint4* __restrict__ dst, const uint32_t* __restrict__ idx,
+                                               const uint4* __restrict__ src, uint64_t n) {
+  const uint64_t total = n * Q;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = i / Q, q = i % Q;
+    dst[(uint64_t)idx[r] * Q + q] = src[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_patch_u32(uint32_t* __restrict__ dst, const uint32_t* __restrict__ idx,
+                                                   const uint32_t* __restrict__ src, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[idx[i]] = src[i];
+}
+
+hipError_t launch_patch(void* dst, uint32_t rec_bytes, const uint32_t* idx, const void* src, uint64_t n,
+                        hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t lanes = rec_bytes == 4 ? n : n * (rec_bytes / 16);
+  const uint32_t g = (uint32_t)std::min<uint64_t>((lanes + 255) / 256, 4096);
+  switch (rec_bytes) {
+    case 4:
+      hipLaunchKernelGGL(k_patch_u32, dim3(g), dim3(256), 0, s, (uint32_t*)dst, idx, (const uint32_t*)src, n);
+      break;
+    case 16:
+      hipLaunchKernelGGL(k_patch<1>, dim3(g), dim3(256), 0, s, (uint4*)dst, idx, (const uint4*)src, n);
+      break;
+    case 32:
+      hipLaunchKernelGGL(k_patch<2>, dim3(g), dim3(256), 0, s, (uint4*)dst, idx, (const uint4*)src, n);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 }  // namespace egm

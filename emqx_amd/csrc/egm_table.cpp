@@ -66,10 +66,63 @@ bool IndexMap::erase(uint64_t h, Eq eq) {
   }
 }
 
+// ---------------------------------------------------------------- DirtyLog --
+static void append_or_full(std::vector<uint32_t>& v, bool& full, const std::vector<uint32_t>& o) {
+  if (full) return;
+  v.insert(v.end(), o.begin(), o.end());
+}
+
+void DirtyLog::merge(const DirtyLog& o) {
+  nodes_full |= o.nodes_full;
+  edges_full |= o.edges_full;
+  dict_full |= o.dict_full;
+  words_full |= o.words_full;
+  append_or_full(nodes, nodes_full, o.nodes);
+  append_or_full(edges, edges_full, o.edges);
+  append_or_full(dict, dict_full, o.dict);
+  if (nodes_full) std::vector<uint32_t>().swap(nodes);
+  if (edges_full) std::vector<uint32_t>().swap(edges);
+  if (dict_full) std::vector<uint32_t>().swap(dict);
+}
+
+void DirtyLog::clear() {
+  std::vector<uint32_t>().swap(nodes);
+  std::vector<uint32_t>().swap(edges);
+  std::vector<uint32_t>().swap(dict);
+  nodes_full = edges_full = dict_full = words_full = false;
+}
+
+// A log longer than a quarter of its array costs more to apply than a copy.
+void HostTable::mark_node(uint32_t n) {
+  if (dirty_.nodes_full) return;
+  dirty_.nodes.push_back(n);
+  if (dirty_.nodes.size() > nodes.size() / 4 + 4096) {
+    dirty_.nodes_full = true;
+    std::vector<uint32_t>().swap(dirty_.nodes);
+  }
+}
+
+void HostTable::mark_edge(uint32_t s) {
+  if (dirty_.edges_full) return;
+  dirty_.edges.push_back(s);
+  if (dirty_.edges.size() > edges.size() / 4 + 4096) {
+    dirty_.edges_full = true;
+    std::vector<uint32_t>().swap(dirty_.edges);
+  }
+}
+
+DirtyLog HostTable::take_dirty() {
+  DirtyLog d;
+  std::swap(d, dirty_);
+  return d;
+}
+
 // --------------------------------------------------------------- HostTable --
 HostTable::HostTable() { clear(); }
 
 void HostTable::clear() {
+  dirty_.clear();
+  dirty_.nodes_full = dirty_.edges_full = dirty_.dict_full = dirty_.words_full = true;
   nodes.clear();
   hash_child.clear();
   parent_.clear();
@@ -122,6 +175,7 @@ uint32_t HostTable::new_node(uint32_t parent, uint32_t via) {
   sig_[n] = 0;
   edge_slot_[n] = NONE;
   ++n_live_nodes_;
+  mark_node(n);
   return n;
 }
 
@@ -133,6 +187,7 @@ void HostTable::free_node(uint32_t n) {
   edge_slot_[n] = NONE;
   free_nodes_.push_back(n);
   --n_live_nodes_;
+  mark_node(n);
 }
 
 uint32_t HostTable::own_flags(uint32_t n) const {
@@ -147,7 +202,9 @@ uint32_t HostTable::own_flags(uint32_t n) const {
 void HostTable::update_flags(uint32_t n) {
   NodeRec& r = nodes[n];
   r.flags = own_flags(n);
+  mark_node(n);
   if (parent_[n] == NONE || via_[n] >= WID_MAX) return;
+  mark_edge(edge_slot_[n]);
   EdgeSlot& s = edges[edge_slot_[n]];
   s.child_flags = r.flags;
   s.child_plus = r.plus_child;
@@ -172,6 +229,8 @@ void HostTable::dict_rehash(size_t cap) {
   std::vector<DictSlot> old;
   old.swap(dict);
   dict.assign(cap, DictSlot{0, NONE, 0, {0}});
+  dirty_.dict_full = true;
+  std::vector<uint32_t>().swap(dirty_.dict);
   uint32_t m = (uint32_t)cap - 1;
   for (const DictSlot& s : old) {
     if (s.wid == NONE) continue;
@@ -194,6 +253,7 @@ uint32_t HostTable::dict_add(const uint8_t* p, uint32_t len) {
   DictSlot s{h, w, len, {0}};
   memcpy(s.inl, p, len < 16 ? len : 16);
   dict[i] = s;
+  if (!dirty_.dict_full) dirty_.dict.push_back(i);
   ++n_dict_used_;
   return w;
 }
@@ -229,6 +289,7 @@ uint32_t HostTable::edge_insert(uint32_t parent, uint32_t wid, uint32_t child, u
         const NodeRec& r = nodes[child];
         s = EdgeSlot{parent, wid, child, cflags, r.plus_child, r.hash_fid, r.term_fid, 0};
         ++n_edges_;
+        mark_edge((uint32_t)(b * EDGE_BUCKET + k));
         return (uint32_t)(b * EDGE_BUCKET + k);
       }
     }
@@ -241,6 +302,8 @@ void HostTable::edge_rehash(size_t n_buckets) {
   old.swap(edges);
   edges.assign(n_buckets * EDGE_BUCKET, EdgeSlot{NONE, 0, 0, 0, NONE, NONE, NONE, 0});
   n_edges_ = n_edge_tombs_ = 0;
+  dirty_.edges_full = true;
+  std::vector<uint32_t>().swap(dirty_.edges);
   for (const EdgeSlot& s : old) {
     if (s.parent == NONE || s.parent == TOMB) continue;
     uint32_t slot = edge_insert(s.parent, s.wid, s.child, s.child_flags);
@@ -305,6 +368,7 @@ int HostTable::insert(const uint8_t* p, uint32_t len, uint32_t fid, uint32_t* ou
       if (c == NONE) {
         c = new_node(cur, WID_HASH);
         hash_child[cur] = c;
+        mark_node(cur);
       }
       last_hash = true;
     } else {
@@ -380,6 +444,7 @@ int HostTable::remove(const uint8_t* p, uint32_t len) {
       hash_child[par] = NONE;
     } else {
       edges[edge_slot_[n]].parent = TOMB;
+      mark_edge(edge_slot_[n]);
       --n_edges_;
       ++n_edge_tombs_;
       --lit_count_[par];
@@ -400,6 +465,9 @@ int HostTable::remove(const uint8_t* p, uint32_t len) {
 // contiguous id range (the hot upper levels then share cache lines), and
 // rebuild the edge table at <= 25 % load.
 void HostTable::relayout() {
+  dirty_.nodes_full = dirty_.edges_full = true;   // every node id changes
+  std::vector<uint32_t>().swap(dirty_.nodes);
+  std::vector<uint32_t>().swap(dirty_.edges);
   const uint32_t N = (uint32_t)nodes.size();
   // children lists via counting sort by parent
   std::vector<uint32_t> cnt(N + 1, 0);

@@ -37,6 +37,26 @@ class IndexMap {
   void grow(size_t want);
 };
 
+// Records of the device image written since the last take_dirty(): what an
+// epoch commit has to patch into a device copy of the previous image instead
+// of re-uploading it (the reference mutates its trie one
+// key at a time inside mnesia transactions, emqx_trie.erl:171-188).
+// Indices may repeat; *_full means the array was rebuilt (rehash, relayout,
+// clear) and must be copied whole.  dict_blob/dict_off only ever grow between
+// clears, so their tails are found from the sizes.
+struct DirtyLog {
+  std::vector<uint32_t> nodes;   // indices into nodes[] and hash_child[]
+  std::vector<uint32_t> edges;   // edge slot indices
+  std::vector<uint32_t> dict;    // dictionary slot indices
+  bool nodes_full = false, edges_full = false, dict_full = false, words_full = false;
+  void merge(const DirtyLog& o);
+  void clear();
+  bool empty() const {
+    return nodes.empty() && edges.empty() && dict.empty() && !nodes_full && !edges_full && !dict_full &&
+           !words_full;
+  }
+};
+
 class HostTable {
  public:
   HostTable();
@@ -72,7 +92,14 @@ class HostTable {
   // exact lookup of a word (host mirror of the device tokeniser's probe)
   uint32_t dict_find(const uint8_t* p, uint32_t len) const;
 
+  // changes since the previous call (see DirtyLog)
+  DirtyLog take_dirty();
+  const DirtyLog& dirty() const { return dirty_; }
+
  private:
+  DirtyLog dirty_;
+  void mark_node(uint32_t n);
+  void mark_edge(uint32_t s);
   // host-only per-node bookkeeping
   std::vector<uint32_t> parent_, via_, ref_, lit_count_, edge_slot_, sig_;
   std::vector<uint32_t> free_nodes_;

@@ -119,6 +119,14 @@ class GpuMatcher:
         self._check(self.lib.egm_table_commit(self.ctx, C.byref(ep)), "egm_table_commit")
         return ep.value
 
+    def commit_stats(self) -> dict:
+        """What the last commit moved (incremental patch vs whole copy)."""
+        h, d, p = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        ms = C.c_double()
+        self._check(self.lib.egm_last_commit_stats(self.ctx, C.byref(h), C.byref(d), C.byref(p), C.byref(ms)),
+                    "egm_last_commit_stats")
+        return {"h2d_bytes": h.value, "d2d_bytes": d.value, "patched": p.value, "ms": ms.value}
+
     def empty(self) -> bool:
         return self.lib.egm_table_empty(self.ctx) == 1
 
@@ -275,6 +283,18 @@ class TableImage:
             "dict_blob": arr(v.dict_blob, int(arr(v.dict_off, v.n_words + 1, np.uint64)[-1]), np.uint8),
             "n_filters": v.n_filters, "n_live_nodes": v.n_live_nodes, "n_edges": v.n_edges,
         }
+
+    def take_dirty(self) -> dict:
+        """Records changed since the previous call (what a commit patches)."""
+        v = L.egm_dirty_view()
+        assert self.lib.egm_image_take_dirty(self.h, C.byref(v)) == 0
+
+        def arr(p, n):
+            return np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
+
+        return {"nodes": arr(v.nodes, v.n_nodes), "edges": arr(v.edges, v.n_edges), "dict": arr(v.dict, v.n_dict),
+                "nodes_full": bool(v.nodes_full), "edges_full": bool(v.edges_full),
+                "dict_full": bool(v.dict_full), "words_full": bool(v.words_full)}
 
     def word_hash(self, w: bytes) -> int:
         return self.lib.egm_word_hash(w, len(w))

@@ -105,8 +105,17 @@ int egm_table_build(egm_ctx* ctx, const uint8_t* filters_blob, const uint32_t* o
                     const uint32_t* filter_ids);
 /* Stage inserts then deletes (either may be NULL); visible after commit. */
 int egm_table_apply_delta(egm_ctx* ctx, const egm_delta* ins, const egm_delta* del);
-/* Publish the staged table as a new epoch (readers in flight keep the old). */
+/* Publish the staged table as a new epoch (readers in flight keep the old).
+   Incremental: the device keeps two copies of the image; a commit writes the
+   one no reader is using and patches into it only the records the staged
+   deltas changed (a rebuild — relayout, table growth — copies whole).
+   The whole-table analogue of the mnesia transaction around
+   emqx_trie:insert/delete, apps/emqx/src/emqx_router.erl:252-303. */
 int egm_table_commit(egm_ctx* ctx, uint64_t* epoch);
+/* What the last commit moved: host->device bytes, device->device bytes,
+   records patched, host wall time (ms). */
+int egm_last_commit_stats(egm_ctx* ctx, uint64_t* h2d_bytes, uint64_t* d2d_bytes, uint64_t* patched,
+                          double* ms);
 /* 1 if the committed table holds no filter, 0 otherwise. */
 int egm_table_empty(egm_ctx* ctx);
 /* Counts of the committed table: filters, trie nodes, literal edges, words. */
@@ -164,7 +173,7 @@ typedef struct egm_image egm_image;
 typedef struct egm_image_view {
   const void* nodes;      uint64_t n_nodes;      /* 16 B {plus_child, hash_fid, term_fid, meta} */
   const uint32_t* hash_child;
-  const void* edges;      uint64_t n_edge_slots; /* 16 B {parent, word, child, child_flags}, 4 per bucket */
+  const void* edges;      uint64_t n_edge_slots; /* 32 B {parent, word, child, child record}, 4 per bucket */
   uint32_t edge_mask;                            /* buckets - 1 */
   const void* dict;       uint64_t n_dict_slots; /* 32 B {hash64, word, len, inline[16]} */
   uint32_t dict_mask;
@@ -179,6 +188,16 @@ int egm_image_insert(egm_image* im, const uint8_t* filter, uint32_t len, uint32_
 int egm_image_remove(egm_image* im, const uint8_t* filter, uint32_t len);
 void egm_image_relayout(egm_image* im);
 int egm_image_get_view(egm_image* im, egm_image_view* out);
+/* Records of the image changed since the previous call (sorted, unique
+   indices; *_full = the array was rebuilt): what egm_table_commit patches.
+   Pointers stay valid until the next call. */
+typedef struct egm_dirty_view {
+  const uint32_t* nodes;  uint64_t n_nodes;   /* indices into nodes[] and hash_child[] */
+  const uint32_t* edges;  uint64_t n_edges;   /* edge slot indices */
+  const uint32_t* dict;   uint64_t n_dict;    /* dictionary slot indices */
+  uint32_t nodes_full, edges_full, dict_full, words_full;
+} egm_dirty_view;
+int egm_image_take_dirty(egm_image* im, egm_dirty_view* out);
 /* Filter -> shard for multi-GPU filter sharding: out[i] =
    word_hash(filter i) mod n_shards.  Host-only. */
 int egm_shard_assign(const uint8_t* blob, const uint32_t* offsets, uint32_t n, uint32_t n_shards,

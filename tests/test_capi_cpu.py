@@ -7,6 +7,7 @@ import os
 import random
 import re
 
+import numpy as np
 import pytest
 
 from emqx_amd import _lib as L
@@ -152,3 +153,110 @@ def test_image_delete_all_frees_everything():
     assert a["n_filters"] == 0 and a["n_live_nodes"] == 1 and a["n_edges"] == 0
     root = a["nodes"][0]
     assert list(root[:3]) == [L.NONE_ID] * 3 and int(root[3]) == 0
+
+
+# ---- incremental commit: the dirty log must name every
+# record a delta changes, so patching a copy of the previous image with it
+# reproduces the new image exactly (what egm_table_commit does on the device).
+def _apply_log(prev, cur, log):
+    out = {}
+    for key, idx_key, full_key in (("nodes", "nodes", "nodes_full"), ("hash_child", "nodes", "nodes_full"),
+                                   ("edges", "edges", "edges_full"), ("dict", "dict", "dict_full")):
+        if log[full_key] or prev is None:
+            out[key] = cur[key].copy()
+            continue
+        a = prev[key]
+        if len(cur[key]) > len(a):   # appended records are in the log; the copy grows first
+            a = np.concatenate([a, np.zeros((len(cur[key]) - len(a),) + a.shape[1:], a.dtype)])
+        else:
+            a = a.copy()
+        idx = log[idx_key]
+        a[idx] = cur[key][idx]
+        out[key] = a
+    for key in ("dict_blob", "dict_off"):   # append-only: copy + tail
+        if log["words_full"] or prev is None:
+            out[key] = cur[key].copy()
+        else:
+            n0 = len(prev[key])
+            out[key] = np.concatenate([prev[key], cur[key][n0:]])
+    return out
+
+
+def _same_image(a, b):
+    for key in ("nodes", "hash_child", "edges", "dict", "dict_blob", "dict_off"):
+        assert a[key].shape == b[key].shape, key
+        assert np.array_equal(a[key], b[key]), key
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_dirty_log_patches_reproduce_image(seed):
+    rng = random.Random(100 + seed)
+    im = TableImage()
+    live = []
+    for f in dict.fromkeys(rand_filter(rng) for _ in range(60)):
+        assert im.insert(f) == 0
+        live.append(f)
+    im.relayout()
+    log = im.take_dirty()
+    assert log["nodes_full"] and log["edges_full"]        # a rebuild copies whole
+    dev = im.arrays()
+    saw_patch = saw_growth = False
+    for rnd in range(25):
+        # a delta: inserts (some new words -> dictionary/edge growth), deletes
+        for _ in range(rng.randint(1, 40 if rnd % 5 else 400)):
+            if live and rng.random() < 0.4:
+                f = live.pop(rng.randrange(len(live)))
+                assert im.remove(f) == 0
+            else:
+                f = rand_filter(rng) + b"/n%d" % rng.randrange(10 ** 6)
+                if im.insert(f) == 0:
+                    live.append(f)
+        cur = im.arrays()
+        log = im.take_dirty()
+        saw_patch |= not log["edges_full"] and len(log["edges"]) > 0
+        saw_growth |= log["edges_full"] or log["dict_full"]
+        assert np.all(np.diff(log["nodes"].astype(np.int64)) > 0)   # sorted, unique
+        dev = _apply_log(dev, cur, log)
+        _same_image(dev, cur)
+    assert saw_patch and saw_growth
+    # an empty delta logs nothing
+    assert not any(len(v) if isinstance(v, np.ndarray) else v for v in im.take_dirty().values())
+
+
+def test_dirty_log_two_slot_protocol():
+    """The device keeps two copies and writes the one not in use; a copy that
+    skipped commits must get the union of their logs (egm_capi.cpp
+    commit_locked: slot.pending ∪ this commit's log)."""
+    rng = random.Random(7)
+    im = TableImage()
+    live = []
+    for f in dict.fromkeys(rand_filter(rng) for _ in range(50)):
+        im.insert(f)
+        live.append(f)
+    im.relayout()
+    slots = [None, None]
+    pending = [None, None]
+    cur = -1
+    for rnd in range(20):
+        for _ in range(rng.randint(1, 30)):
+            if live and rng.random() < 0.5:
+                im.remove(live.pop(rng.randrange(len(live))))
+            else:
+                f = rand_filter(rng) + b"/s%d" % rng.randrange(1000)
+                if im.insert(f) == 0:
+                    live.append(f)
+        img = im.arrays()
+        d = im.take_dirty()
+        x = 0 if cur < 0 else 1 - cur
+        if slots[x] is None or pending[x] is None:
+            slots[x] = _apply_log(None, img, d)
+        else:
+            need = {k: (np.union1d(pending[x][k], d[k]).astype(np.uint32) if isinstance(d[k], np.ndarray)
+                        else pending[x][k] or d[k]) for k in d}
+            slots[x] = _apply_log(slots[x], img, need)
+        _same_image(slots[x], img)
+        pending[x] = {k: (np.zeros(0, np.uint32) if isinstance(v, np.ndarray) else False) for k, v in d.items()}
+        if cur >= 0:
+            pending[cur] = {k: (np.union1d(pending[cur][k], d[k]).astype(np.uint32) if isinstance(d[k], np.ndarray)
+                                else pending[cur][k] or d[k]) for k in d}
+        cur = x

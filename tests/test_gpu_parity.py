@@ -177,6 +177,23 @@ def test_config_c0_heavy_path_vs_cpp_oracle(gm, mode):
     assert np.array_equal(canonical(res.row_ptr, res.ids), canonical(row, ids))
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_config_c3_vs_cpp_oracle(gm, mode):
+    """C3 shape at reduced size (depth-16 topics and filters,
+    '+' p=.35, last-level '#' p=.7): deep chunks are walked as sub-chunks of
+    staged words, and wide frontiers exercise the stack-overflow hand-off to
+    k_heavy.  Bit-exact against the C++ oracle in both match modes."""
+    f, t = synth.config("c3", n_filters=20_000, n_topics=20_000)
+    gm.build(f.blob, f.off)
+    res = gm.match(t.blob, t.off, mode)
+    assert res.n_error == 0
+    o = OracleTrie(True, mode)
+    o.add(f.blob, f.off)
+    row, ids = o.match(t.blob, t.off, threads=8)
+    assert np.array_equal(res.row_ptr, row)
+    assert np.array_equal(canonical(res.row_ptr, res.ids), canonical(row, ids))
+
+
 def test_golden_fixture(gm):
     import gzip
     import json
@@ -220,6 +237,91 @@ def test_device_api_matches_host_api(gm):
     gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_TRIE, s, d_row.data_ptr(),
                     d_ids.data_ptr(), 16, 0)
     assert gm.last_stats()["overflow"] != 0
+
+
+def _pack(items):
+    return pack_strings(items)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_incremental_commits_vs_cpp_oracle(gm, mode):
+    """Route churn (emqx_router add/delete -> emqx_trie
+    insert/delete, emqx_trie.erl:82-96): rounds of deletes + inserts, each
+    committed incrementally (records patched into the idle device copy), are
+    bit-exact against the C++ oracle mutated the same way, and a small delta
+    moves a small fraction of the table."""
+    pool = synth.filters(40_000, seed=0xE3C0_1234)
+    pl = list(dict.fromkeys(pool.to_list()))
+    assert len(pl) > 30_000
+    f0 = list(range(10_000))
+    gm.build(*_pack([pl[i] for i in f0]), np.array(f0, dtype=np.uint32))
+    o = OracleTrie(True, mode)
+    o.add(*_pack([pl[i] for i in f0]), np.array(f0, dtype=np.uint32))
+    live = set(f0)
+    nxt = 10_000
+    t = synth.topics(20_000, pool, seed=0xE3C0_4321)
+    rng = random.Random(mode)
+    full_bytes = gm.stats()["device_bytes"]
+    for rnd in range(8):
+        dels = rng.sample(sorted(live), 300)
+        ins = list(range(nxt, nxt + 400 + 200 * rnd))
+        nxt = ins[-1] + 1
+        gm.apply(inserts=[pl[i] for i in ins], deletes=[pl[i] for i in dels], insert_ids=ins)
+        gm.commit()
+        cs = gm.commit_stats()
+        if rnd >= 1:   # the first commit after a build may copy the other slot on device
+            assert cs["patched"] > 0 and cs["h2d_bytes"] < full_bytes // 10, cs
+        o.add(*_pack([pl[i] for i in ins]), np.array(ins, dtype=np.uint32))
+        o.remove(*_pack([pl[i] for i in dels]))
+        live.update(ins)
+        live.difference_update(dels)
+        res = gm.match(t.blob, t.off, mode)
+        row, ids = o.match(t.blob, t.off, threads=8)
+        assert np.array_equal(res.row_ptr, row), rnd
+        assert np.array_equal(canonical(res.row_ptr, res.ids), canonical(row, ids)), rnd
+    # a rebuild of the same live set gives the same answers
+    m2 = GpuMatcher(0)
+    try:
+        lv = sorted(live)
+        m2.build(*_pack([pl[i] for i in lv]), np.array(lv, dtype=np.uint32))
+        r2 = m2.match(t.blob, t.off, mode)
+        assert np.array_equal(canonical(r2.row_ptr, r2.ids), canonical(res.row_ptr, res.ids))
+    finally:
+        m2.close()
+
+
+def test_commit_waits_for_batches_in_flight(gm):
+    """A batch enqueued on a caller stream keeps the epoch it started with:
+    two commits later its device copy is rewritten only after it finished."""
+    import torch
+    f, t = synth.config("c0", n_topics=100_000)
+    fl = f.to_list()
+    gm.build(f.blob, f.off)
+    host = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    dev = torch.device("cuda:0")
+    d_blob = torch.from_numpy(t.blob).to(dev)
+    d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+    n = t.n
+    cap = len(host.ids) + 1024
+    d_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for _ in range(3):   # queue several batches so the walk is still running
+        gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES,
+                        stream.cuda_stream, d_row.data_ptr(), d_ids.data_ptr(), cap, 0)
+    gm.apply(deletes=fl[:5000])
+    gm.commit()
+    gm.apply(deletes=fl[5000:])
+    gm.commit()          # writes the copy the queued batches read
+    stream.synchronize()
+    row = d_row.cpu().numpy().view(np.uint64)
+    ids = d_ids.cpu().numpy().view(np.uint32)[: len(host.ids)]
+    assert np.array_equal(row, host.row_ptr)
+    assert np.array_equal(canonical(row, ids), canonical(host.row_ptr, host.ids))
+    assert gm.empty()
+    gone = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    assert len(gone.ids) == 0
 
 
 def test_logical_shards_union(gm):
