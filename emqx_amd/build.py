@@ -63,11 +63,11 @@ def build_lib(verbose=False, force=False) -> str:
         src = os.path.join(CSRC, name)
         o = os.path.join(BUILD, name.replace(".cpp", ".o"))
         if force or _stale(o, [src] + HEADERS):
-            _run(["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result", "-Wno-unused-value", "-D__HIP_PLATFORM_AMD__",
+            _run(["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result", "-Wno-unused-value", "-pthread", "-D__HIP_PLATFORM_AMD__",
                   f"-I{ROCM}/include", "-c", src, "-o", o], verbose)
         objs.append(o)
     if force or _stale(LIB, objs + [os.path.abspath(__file__)]):
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs, verbose)
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", LIB] + objs, verbose)
     return LIB
 
 

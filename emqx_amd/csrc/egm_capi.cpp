@@ -14,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/emqx_gpu_match.h"
@@ -188,9 +189,43 @@ static void note_use(egm_ctx* c, int slot, hipStream_t s) {
   u.push_back({s, e});
 }
 
-static void sort_unique(std::vector<uint32_t>& v) {
-  std::sort(v.begin(), v.end());
-  v.erase(std::unique(v.begin(), v.end()), v.end());
+// Sorted, unique indices.  Large logs go through a bitmap over the array
+// (O(n + size/64)) rather than a sort.
+static void sort_unique(std::vector<uint32_t>& v, uint64_t size = 0) {
+  if (v.size() < 8192 || size == 0 || size > (1ull << 32)) {
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    return;
+  }
+  std::vector<uint64_t> bits((size + 63) / 64, 0);
+  for (uint32_t i : v)
+    if (i < size) bits[i >> 6] |= 1ull << (i & 63);
+  v.clear();
+  for (uint64_t w = 0; w < bits.size(); ++w)
+    for (uint64_t b = bits[w]; b; b &= b - 1) v.push_back((uint32_t)(w * 64 + __builtin_ctzll(b)));
+}
+
+// out[i] = rec[idx[i]] for records of R bytes; the records are random reads
+// of a multi-GB host image, so large patches use several threads.
+template <size_t R>
+static void gather(uint8_t* out, const void* rec, const std::vector<uint32_t>& idx) {
+  const uint8_t* base = (const uint8_t*)rec;
+  auto work = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) memcpy(out + i * R, base + (size_t)idx[i] * R, R);
+  };
+  const size_t n = idx.size();
+  unsigned nt = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+  if (n < 65536 || nt == 1) {
+    work(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t per = (n + nt - 1) / nt;
+  for (unsigned k = 0; k < nt; ++k) {
+    size_t lo = k * per, hi = std::min(n, lo + per);
+    if (lo < hi) th.emplace_back(work, lo, hi);
+  }
+  for (auto& x : th) x.join();
 }
 
 // Bring one array of slot `dst` to the host image.  Preference order:
@@ -225,7 +260,7 @@ static int sync_array(egm_ctx* c, DevBuf& dst, uint64_t& held, const DevBuf* src
       return c->hip_fail(e, what);
     c->last_commit.h2d += n * sz;
   }
-  sort_unique(*idx);
+  sort_unique(*idx, n);
   while (!idx->empty() && idx->back() >= n) idx->pop_back();
   held = n;
   return EGM_OK;
@@ -319,10 +354,10 @@ static int commit_locked(egm_ctx* c, uint64_t* epoch) {
     memcpy(h + o_ih, ih.data(), ih.size() * 4);
     memcpy(h + o_ie, ie.data(), ie.size() * 4);
     memcpy(h + o_id, id.data(), id.size() * 4);
-    for (size_t i = 0; i < in.size(); ++i) memcpy(h + o_rn + i * 16, &t.nodes[in[i]], 16);
-    for (size_t i = 0; i < ih.size(); ++i) memcpy(h + o_rh + i * 4, &t.hash_child[ih[i]], 4);
-    for (size_t i = 0; i < ie.size(); ++i) memcpy(h + o_re + i * 32, &t.edges[ie[i]], 32);
-    for (size_t i = 0; i < id.size(); ++i) memcpy(h + o_rd + i * 32, &t.dict[id[i]], 32);
+    gather<16>(h + o_rn, t.nodes.data(), in);
+    gather<4>(h + o_rh, t.hash_child.data(), ih);
+    gather<32>(h + o_re, t.edges.data(), ie);
+    gather<32>(h + o_rd, t.dict.data(), id);
     if ((e = c->patch_dev.ensure(total)) != hipSuccess) return c->hip_fail(e, "commit: patch buffer");
     if ((e = hipMemcpyAsync(c->patch_dev.p, h, total, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
       return c->hip_fail(e, "commit: patch upload");
@@ -874,7 +909,9 @@ void egm_image_relayout(egm_image* im) {
 int egm_image_take_dirty(egm_image* im, egm_dirty_view* v) {
   if (!im || !v) return EGM_E_INVAL;
   im->d = im->t.take_dirty();
-  for (auto* x : {&im->d.nodes, &im->d.edges, &im->d.dict}) sort_unique(*x);
+  sort_unique(im->d.nodes, im->t.nodes.size());
+  sort_unique(im->d.edges, im->t.edges.size());
+  sort_unique(im->d.dict, im->t.dict.size());
   v->nodes = im->d.nodes.data();
   v->n_nodes = im->d.nodes.size();
   v->edges = im->d.edges.data();

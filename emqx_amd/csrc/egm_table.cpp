@@ -518,6 +518,11 @@ void HostTable::relayout() {
   edge_slot_.assign(L, NONE);
   free_nodes_.clear();
   n_live_nodes_ = L;
+  // room to grow: route churn after a rebuild appends nodes without moving
+  // multi-GB vectors
+  const size_t room = L + L / 8 + 1024;
+  for (auto* v : {&hash_child, &parent_, &via_, &ref_, &lit_count_, &sig_, &edge_slot_}) v->reserve(room);
+  nodes.reserve(room);
 
   size_t nb = 16;
   while (nb * EDGE_BUCKET < (size_t)n_edges_ * 2) nb <<= 1;  // 25-50 % slot load
