@@ -21,6 +21,8 @@ EGM_E_NOTFOUND = -6
 
 EGM_MODE_TRIE = 0
 EGM_MODE_ROUTES = 1
+EGM_RMODE_MATCH = 0
+EGM_RMODE_DISPATCH = 1
 
 EGM_TF_WILDCARD = 1
 EGM_TF_DOLLAR = 2
@@ -95,6 +97,16 @@ SIGNATURES = {
     "egm_fanout_batch": (C.c_int, [_P, C.POINTER(egm_result), C.POINTER(C.POINTER(egm_delivery))]),
     "egm_fanout_device": (C.c_int, [_P, _P, _P, C.c_uint32, _P, _P, _P, _P, C.c_uint64]),
     "egm_result_free": (None, [_P]),
+    "egm_rstore_open": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "egm_rstore_close": (None, [_P]),
+    "egm_rstore_last_error": (C.c_char_p, [_P]),
+    "egm_rstore_put": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint64]),
+    "egm_rstore_delete": (C.c_int, [_P, _P, C.c_uint32]),
+    "egm_rstore_clean": (C.c_int, [_P]),
+    "egm_rstore_size": (C.c_int, [_P, _u64p]),
+    "egm_rstore_commit": (C.c_int, [_P]),
+    "egm_rstore_match": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.c_int,
+                                   C.POINTER(C.POINTER(egm_result))]),
     "egm_image_new": (_P, []),
     "egm_image_free": (None, [_P]),
     "egm_image_insert": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32]),

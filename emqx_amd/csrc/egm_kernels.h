@@ -111,4 +111,49 @@ hipError_t launch_fanout(const SubTable& st, const uint64_t* match_row, const ui
 hipError_t launch_patch(void* dst, uint32_t rec_bytes, const uint32_t* idx, const void* src, uint64_t n,
                         hipStream_t s);
 
+// ---- retained reverse match (emqx_retainer_mnesia:match_messages/1) ----
+constexpr uint32_t RN_TERM = 0x80000000u;   // node's own topic is stored (in n_children)
+constexpr uint32_t RS_SINGLE = 0x80000000u; // range = one already-checked rank (in hi)
+
+struct RetainView {            // a committed retained store in HBM
+  const uint4* nodes;          // {first_child, n_children | RN_TERM, lo, hi}: ranks under the node
+  const uint4* edges;          // 16 B {parent, word, child, 0}, 4 per 64 B bucket
+  uint32_t edge_mask;          // buckets - 1
+  const uint32_t* msg;         // rank -> message id
+  const uint64_t* expiry;      // rank -> expiry time in ms (0 = never)
+  uint32_t n_topics;
+};
+
+struct RetainWork {            // per query batch
+  const uint32_t* off;         // filter offsets (wid layout of k_tokenise)
+  const uint32_t* wid;
+  const uint32_t* lv;
+  const uint8_t* tfl;
+  uint32_t* pc;                // per frontier pair: pairs it creates
+  uint32_t* paux;              // per frontier pair: first created node
+  uint64_t* poff;              // scan of pc
+  uint64_t* tiles;
+  uint32_t *rf, *rlo, *rhi;    // emitted rank ranges (filter, lo, hi | RS_SINGLE)
+  uint32_t* n_ranges;
+  uint32_t range_cap;
+  uint32_t* alive;             // per rank: alive at `now` (strict rule)
+  uint64_t* apre;              // scan of alive
+  uint32_t* fcnt;              // per filter: ids
+  uint32_t* roff;              // per range: offset inside the filter's row
+  uint64_t now;
+  int ge_plain;                // dispatch: plain topics use read_message's Et >= Now
+};
+
+hipError_t launch_tokenise(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n, uint32_t* wid,
+                           uint32_t* lv, uint8_t* tfl, hipStream_t s);
+hipError_t launch_rs_alive(const RetainView& v, const RetainWork& w, hipStream_t s);
+hipError_t launch_rs_init(uint32_t n, uint32_t* pf, uint32_t* pn, hipStream_t s);
+hipError_t launch_rs_level(const RetainView& v, const RetainWork& w, uint32_t level, uint32_t np,
+                           const uint32_t* pf, const uint32_t* pn, hipStream_t s);
+hipError_t launch_rs_fill(const RetainWork& w, uint32_t np, uint64_t nnext, const uint32_t* pf, uint32_t* pf2,
+                          uint32_t* pn2, hipStream_t s);
+hipError_t launch_rs_rows(const RetainWork& w, uint32_t nr, uint32_t n, uint64_t* row, hipStream_t s);
+hipError_t launch_rs_expand(const RetainView& v, const RetainWork& w, uint32_t nr, const uint64_t* row,
+                            uint32_t* ids, hipStream_t s);
+
 }  // namespace egm

@@ -1439,4 +1439,220 @@ hipError_t launch_patch(void* dst, uint32_t rec_bytes, const uint32_t* idx, cons
   return hipGetLastError();
 }
 
+// ------------------------------------------------- retained reverse match ----
+// emqx_retainer_mnesia:match_messages/1 (apps/emqx_retainer/src/
+// emqx_retainer_mnesia.erl:200-204, 215-228): one subscription filter against
+// every stored retained topic.  The store is a word trie of the topics whose
+// topics are ranked in depth-first order, so the topics under a node are the
+// contiguous rank range [lo, hi) — a trailing '#' (the improper tail '_' of
+// condition/1) emits that range whole, '+' (the match-spec '_') fans out to
+// every child.  Filters advance level-synchronously over a (filter, node)
+// frontier: count -> scan -> fill per level, balanced by output position.
+__device__ __forceinline__ uint32_t rs_edge(const RetainView& v, uint32_t node, uint32_t w) {
+  uint32_t b = edge_bucket(node, w, v.edge_mask);
+  for (;;) {
+    const uint4* sl = v.edges + (size_t)b * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 e = sl[k];
+      if (e.x == node && e.y == w) return e.z;
+      if (e.x == NONE) return NONE;
+    }
+    b = (b + 1) & v.edge_mask;
+  }
+}
+
+__device__ __forceinline__ bool rs_alive(uint64_t e, uint64_t now, bool ge) {
+  return e == 0 || e > now || (ge && e == now);
+}
+
+// one emitted range per lane at most: wave-aggregated append
+__device__ __forceinline__ void rs_emit(const RetainWork& w, bool on, uint32_t f, uint32_t lo, uint32_t hi) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t m = __ballot(on);
+  if (!m) return;
+  const uint32_t leader = __builtin_ctzll(m);
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(w.n_ranges, (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (!on) return;
+  const uint32_t i = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+  if (i < w.range_cap) {
+    w.rf[i] = f;
+    w.rlo[i] = lo;
+    w.rhi[i] = hi;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rs_alive(const uint64_t* __restrict__ expiry, uint32_t m, uint64_t now,
+                                                  uint32_t* __restrict__ alive) {
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < m; r += gridDim.x * blockDim.x)
+    alive[r] = rs_alive(expiry[r], now, false) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_rs_init(uint32_t n, uint32_t* __restrict__ pf, uint32_t* __restrict__ pn) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    pf[i] = i;
+    pn[i] = 0;   // the root: no words consumed
+  }
+}
+
+// one (filter, node) pair per lane at word index `level`
+__global__ __launch_bounds__(256) void k_rs_step(RetainView v, RetainWork w, uint32_t level, uint32_t np,
+                                                 const uint32_t* __restrict__ pf, const uint32_t* __restrict__ pn) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t n_iter = (np + stride - 1) / stride;   // uniform trip count: rs_emit ballots the whole wave
+  for (uint32_t it = 0; it < n_iter; ++it) {
+    const uint32_t p = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+    bool emit = false;
+    uint32_t f = 0, lo = 0, hi = 0;
+    if (p < np) {
+      f = pf[p];
+      const uint32_t node = pn[p];
+      const uint32_t L = w.lv[f];
+      const uint4 rec = v.nodes[node];   // {first_child, n_children | RN_TERM, lo, hi}
+      uint32_t c = 0, aux = 0;
+      if (level == L) {                  // every word consumed: the topic at this node
+        const bool ge = w.ge_plain && !(w.tfl[f] & TF_WILDCARD);
+        if ((rec.y & RN_TERM) && rs_alive(v.expiry[rec.z], w.now, ge)) {
+          emit = true;
+          lo = rec.z;
+          hi = (rec.z + 1) | RS_SINGLE;
+        }
+      } else {
+        const uint32_t wd = w.wid[w.off[f] + f + level];
+        if (wd == WID_HASH) {            // '#' : only as the last word (condition/1, :217-219)
+          if (level + 1 == L && rec.w > rec.z) {
+            emit = true;
+            lo = rec.z;
+            hi = rec.w;
+          }
+        } else if (wd == WID_PLUS) {     // '_' : every child
+          c = rec.y & ~RN_TERM;
+          aux = rec.x;
+        } else if (wd < WID_MAX && (rec.y & ~RN_TERM)) {
+          const uint32_t ch = rs_edge(v, node, wd);
+          if (ch != NONE) {
+            c = 1;
+            aux = ch;
+          }
+        }
+      }
+      w.pc[p] = c;
+      w.paux[p] = aux;
+    }
+    rs_emit(w, emit, f, lo, hi);
+  }
+}
+
+// next frontier, one lane per output pair: its source pair by binary search
+__global__ __launch_bounds__(256) void k_rs_fill(RetainWork w, uint32_t np, uint64_t nnext,
+                                                 const uint32_t* __restrict__ pf, uint32_t* __restrict__ pf2,
+                                                 uint32_t* __restrict__ pn2) {
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nnext;
+       q += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t lo = 0, hi = np;            // largest src with poff[src] <= q
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (w.poff[mid] <= q) lo = mid;
+      else hi = mid;
+    }
+    pf2[q] = pf[lo];
+    pn2[q] = w.paux[lo] + (uint32_t)(q - w.poff[lo]);
+  }
+}
+
+// per range: its alive count and its offset inside the filter's row
+__global__ __launch_bounds__(256) void k_rs_count(RetainWork w, uint32_t nr) {
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nr; r += gridDim.x * blockDim.x) {
+    const uint32_t hi = w.rhi[r], lo = w.rlo[r];
+    const uint32_t c = (hi & RS_SINGLE) ? 1u : (uint32_t)(w.apre[hi] - w.apre[lo]);
+    w.roff[r] = atomicAdd(&w.fcnt[w.rf[r]], c);
+  }
+}
+
+// one wave per range: its alive ranks -> message ids in the filter's row
+__global__ __launch_bounds__(256) void k_rs_expand(RetainView v, RetainWork w, uint32_t nr,
+                                                   const uint64_t* __restrict__ row, uint32_t* __restrict__ ids) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < nr; r += nw) {
+    const uint32_t hr = w.rhi[r], lo = w.rlo[r];
+    uint32_t* out = ids + row[w.rf[r]] + w.roff[r];
+    if (hr & RS_SINGLE) {
+      if (lane == 0) out[0] = v.msg[lo];
+      continue;
+    }
+    const uint64_t a0 = w.apre[lo];
+    const uint32_t cnt = (uint32_t)(w.apre[hr] - a0);
+    if (cnt == hr - lo) {                // nothing expired in the range: ranks in order
+      for (uint32_t k = lane; k < cnt; k += 64) out[k] = v.msg[lo + k];
+      continue;
+    }
+    for (uint32_t k = lane; k < cnt; k += 64) {   // k-th alive rank: apre[rank + 1] > a0 + k
+      uint32_t a = lo, b = hr - 1;
+      while (a < b) {
+        const uint32_t mid = (a + b) >> 1;
+        if (w.apre[mid + 1] > a0 + k) b = mid;
+        else a = mid + 1;
+      }
+      out[k] = v.msg[a];
+    }
+  }
+}
+
+hipError_t launch_tokenise(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n, uint32_t* wid,
+                           uint32_t* lv, uint8_t* tfl, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_tokenise, dim3((n + TOK_BLOCK - 1) / TOK_BLOCK), dim3(TOK_BLOCK), 0, s, tab, blob, off, n,
+                     wid, lv, tfl);
+  return hipGetLastError();
+}
+
+static uint32_t grid_for(uint64_t n, uint32_t cap = 8192) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, cap));
+}
+
+hipError_t launch_rs_alive(const RetainView& v, const RetainWork& w, hipStream_t s) {
+  if (v.n_topics) {
+    hipLaunchKernelGGL(k_rs_alive, dim3(grid_for(v.n_topics)), dim3(256), 0, s, v.expiry, v.n_topics, w.now, w.alive);
+  }
+  scan_counts(w.alive, v.n_topics, w.tiles, w.apre, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_init(uint32_t n, uint32_t* pf, uint32_t* pn, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_rs_init, dim3(grid_for(n)), dim3(256), 0, s, n, pf, pn);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_level(const RetainView& v, const RetainWork& w, uint32_t level, uint32_t np,
+                           const uint32_t* pf, const uint32_t* pn, hipStream_t s) {
+  hipLaunchKernelGGL(k_rs_step, dim3(grid_for(np)), dim3(256), 0, s, v, w, level, np, pf, pn);
+  scan_counts(w.pc, np, w.tiles, w.poff, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_fill(const RetainWork& w, uint32_t np, uint64_t nnext, const uint32_t* pf, uint32_t* pf2,
+                          uint32_t* pn2, hipStream_t s) {
+  if (nnext) hipLaunchKernelGGL(k_rs_fill, dim3(grid_for(nnext)), dim3(256), 0, s, w, np, nnext, pf, pf2, pn2);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_rows(const RetainWork& w, uint32_t nr, uint32_t n, uint64_t* row, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(w.fcnt, 0, ((size_t)n + 1) * 4, s);
+  if (e != hipSuccess) return e;
+  if (nr) hipLaunchKernelGGL(k_rs_count, dim3(grid_for(nr)), dim3(256), 0, s, w, nr);
+  scan_counts(w.fcnt, n, w.tiles, row, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_expand(const RetainView& v, const RetainWork& w, uint32_t nr, const uint64_t* row,
+                            uint32_t* ids, hipStream_t s) {
+  if (nr)
+    hipLaunchKernelGGL(k_rs_expand, dim3(std::min<uint32_t>((nr + 3) / 4, 16384)), dim3(256), 0, s, v, w, nr, row,
+                       ids);
+  return hipGetLastError();
+}
+
 }  // namespace egm

@@ -166,6 +166,38 @@ int egm_fanout_device(egm_ctx* ctx, const uint64_t* d_match_row, const uint32_t*
 
 void egm_result_free(void* result);
 
+/* ---- retained messages: reverse match ----
+   One subscription filter against every stored retained topic, for a batch of
+   filters.  Replaces apps/emqx_retainer/src/emqx_retainer_mnesia.erl:
+     egm_rstore_put     <- store_retained/2  :73-101 (one record per topic;
+                           topics with a '+'/'#' word are rejected: EGM_E_INVAL)
+     egm_rstore_delete  <- delete_message/2  :114-129 (plain topic)
+     egm_rstore_clean   <- clean/1           :148-150
+     egm_rstore_match   <- match_messages/1  :200-204 with condition/1 :215-220
+                           and make_match_spec/1 :222-228: '+' matches any one
+                           word, a last '#' any rest (also none), NO '$' rule;
+                           alive when expiry == 0 or expiry > now_ms.
+                           EGM_RMODE_DISPATCH routes plain topics through
+                           read_messages/1 :187-198 instead (alive when expiry
+                           >= now_ms), as emqx_retainer:dispatch/4 does
+                           (apps/emqx_retainer/src/emqx_retainer.erl:107-117).
+   Result rows hold message ids (order within a row unspecified: the reference
+   sorts by timestamp, sort_retained/1 :154-159, on the host).  Changes are
+   visible to the next match (the device image is rebuilt on demand). */
+typedef struct egm_rstore egm_rstore;
+enum { EGM_RMODE_MATCH = 0, EGM_RMODE_DISPATCH = 1 };
+int egm_rstore_open(int device, egm_rstore** out);
+void egm_rstore_close(egm_rstore* rs);
+const char* egm_rstore_last_error(egm_rstore* rs);
+int egm_rstore_put(egm_rstore* rs, const uint8_t* topic, uint32_t len, uint32_t msg_id, uint64_t expiry_ms);
+int egm_rstore_delete(egm_rstore* rs, const uint8_t* topic, uint32_t len);
+int egm_rstore_clean(egm_rstore* rs);
+int egm_rstore_size(egm_rstore* rs, uint64_t* n);
+/* Upload the current records now (otherwise done by the next match). */
+int egm_rstore_commit(egm_rstore* rs);
+int egm_rstore_match(egm_rstore* rs, const uint8_t* filters_blob, const uint32_t* offsets, uint32_t n,
+                     uint64_t now_ms, int mode, egm_result** out);
+
 /* ---- host-only table image (diagnostics; needs no device) ----
    Builds the same HBM image egm_table_commit uploads, so the layout can be
    inspected and tested on a host without a GPU. */
