@@ -79,9 +79,9 @@ def build_synth(verbose=False, force=False) -> str:
 
 
 def build_oracle(verbose=False, force=False) -> str:
-    src = os.path.join(ROOT, "oracle", "trie_oracle.cpp")
-    if force or _stale(ORACLE, [src]):
-        _run(["g++", "-O3", "-fPIC", "-shared", "-std=c++17", "-pthread", "-o", ORACLE, src], verbose)
+    srcs = [os.path.join(ROOT, "oracle", f) for f in ("trie_oracle.cpp", "retainer_scan.cpp")]
+    if force or _stale(ORACLE, srcs):
+        _run(["g++", "-O3", "-fPIC", "-shared", "-std=c++17", "-pthread", "-o", ORACLE] + srcs, verbose)
     return ORACLE
 
 

@@ -1562,12 +1562,40 @@ __global__ __launch_bounds__(256) void k_rs_fill(RetainWork w, uint32_t np, uint
   }
 }
 
-// per range: its alive count and its offset inside the filter's row
+// per range: its alive count and its offset inside the filter's row.  A
+// filter's ranges are mostly adjacent in the list (frontiers stay ordered by
+// filter), so lanes holding the same filter are summed with a segmented wave
+// scan and reserve their space with ONE atomic per segment — a '+'-heavy
+// filter emits thousands of ranges, which as per-range atomics on one counter
+// serialised the whole kernel.
 __global__ __launch_bounds__(256) void k_rs_count(RetainWork w, uint32_t nr) {
-  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nr; r += gridDim.x * blockDim.x) {
-    const uint32_t hi = w.rhi[r], lo = w.rlo[r];
-    const uint32_t c = (hi & RS_SINGLE) ? 1u : (uint32_t)(w.apre[hi] - w.apre[lo]);
-    w.roff[r] = atomicAdd(&w.fcnt[w.rf[r]], c);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t n_iter = (nr + stride - 1) / stride;   // uniform: the wave works together
+  for (uint32_t it = 0; it < n_iter; ++it) {
+    const uint32_t r = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+    const bool on = r < nr;
+    uint32_t f = NONE, c = 0;
+    if (on) {
+      const uint32_t hi = w.rhi[r], lo = w.rlo[r];
+      f = w.rf[r];
+      c = (hi & RS_SINGLE) ? 1u : (uint32_t)(w.apre[hi] - w.apre[lo]);
+    }
+    const uint32_t fprev = __shfl_up(f, 1, 64);
+    const uint64_t heads = __ballot(lane == 0 || f != fprev);
+    const uint32_t seg0 = 63 - __builtin_clzll(heads & ((2ull << lane) - 1));   // my segment's head
+    uint32_t x = c;   // segmented inclusive scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= seg0 + (uint32_t)d) x += y;
+    }
+    const uint64_t later = heads & ~((2ull << lane) - 1);
+    const uint32_t tail = later ? (uint32_t)__builtin_ctzll(later) - 1 : 63u;
+    uint32_t base = 0;
+    if (lane == tail && on && x) base = atomicAdd(&w.fcnt[f], x);
+    base = __shfl(base, tail, 64);
+    if (on) w.roff[r] = base + x - c;
   }
 }
 

@@ -34,6 +34,11 @@ def _load():
         lib.ot_n_keys.restype = C.c_uint64
         lib.ot_n_keys.argtypes = [P]
         lib.ot_free_ptr.argtypes = [P]
+        lib.rs_new.restype = P
+        lib.rs_free.argtypes = [P]
+        lib.rs_put.argtypes = [P, P, P, C.c_uint32, P, P]
+        lib.rs_match_count.restype = C.c_uint64
+        lib.rs_match_count.argtypes = [P, P, P, C.c_uint32, C.c_uint64, C.c_int, C.c_int, P]
         _lib = lib
     return _lib
 
@@ -90,3 +95,30 @@ def canonical(row, ids):
     rid = np.repeat(np.arange(n, dtype=np.int64), np.diff(row).astype(np.int64))
     order = np.lexsort((out, rid))
     return out[order]
+
+
+class OracleRetained:
+    """retainer_scan.cpp: the reference's retained lookup as a full-table scan
+    per filter (mnesia dirty_select with a partially bound key)."""
+
+    def __init__(self):
+        self.lib = _load()
+        self.h = self.lib.rs_new()
+
+    def __del__(self):  # pragma: no cover
+        if getattr(self, "h", None):
+            self.lib.rs_free(self.h)
+            self.h = None
+
+    def put(self, blob, off, ids, expiry):
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        expiry = np.ascontiguousarray(expiry, dtype=np.uint64)
+        self.lib.rs_put(self.h, _p(blob), _p(off), len(off) - 1, _p(ids), _p(expiry))
+
+    def match_counts(self, blob, off, now: int, mode: int, threads: int = 1):
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        n = len(off) - 1
+        counts = np.zeros(n, dtype=np.uint32)
+        tot = self.lib.rs_match_count(self.h, _p(blob), _p(off), n, now, mode, threads, _p(counts))
+        return int(tot), counts

@@ -106,3 +106,28 @@ def test_match_messages_vs_independent(seed):
     st.delete_message(f)
     assert not any(_independent(t, f) for t in (b"/".join(k_ if isinstance(k_, bytes) else b"" for k_ in k)
                                                  for k in st.recs))
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_cpp_scan_vs_python_oracle(seed):
+    """oracle/retainer_scan.cpp (the CPU baseline) agrees with the restatement."""
+    import numpy as np
+
+    from emqx_amd.engine import pack_strings
+    from oracle.cpp import OracleRetained
+    rng = random.Random(10 + seed)
+    st = RR.RetainedTable()
+    cs = OracleRetained()
+    topics = list(dict.fromkeys(_topic(rng) for _ in range(400)))
+    exp = [rng.choice([0, 0, 500, 1500]) for _ in topics]
+    for t, e in zip(topics, exp):
+        st.store_retained(t, t, e)
+    blob, off = pack_strings(topics)
+    cs.put(blob, off, np.arange(len(topics), dtype=np.uint32), np.array(exp, dtype=np.uint64))
+    filters = [_filter(rng) for _ in range(300)] + [t for t in topics[:50]]
+    fb, fo = pack_strings(filters)
+    for now in (0, 500, 1000):
+        for mode in (0, 1):
+            tot, counts = cs.match_counts(fb, fo, now, mode, threads=2)
+            want = [len(st.dispatch(f, now) if mode else st.match_messages(f, now)) for f in filters]
+            assert counts.tolist() == want and tot == sum(want)
