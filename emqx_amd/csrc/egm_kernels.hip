@@ -1232,6 +1232,10 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
 // row_ptr loads coalesce.  Light pieces of topics re-run by k_heavy and unused
 // slab slots (count 0) are skipped.
 constexpr int COMPACT_WAVES = 4;
+#ifndef EGM_COMPACT_IPL
+#define EGM_COMPACT_IPL 8   // 8: 2.06 -> 1.91 ms at C2 (A/B, rocprof)
+#endif
+constexpr int COMPACT_IPL = EGM_COMPACT_IPL;
 __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __restrict__ pieces,
                                                                 const uint8_t* __restrict__ tfl,
                                                                 const uint32_t* __restrict__ ids_tmp, uint32_t n,
@@ -1257,9 +1261,10 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
   const uint64_t nwin = (np + 63) / 64, nw = (uint64_t)gridDim.x * COMPACT_WAVES;
   const uint64_t per = (nwin + nw - 1) / nw, me = (uint64_t)blockIdx.x * COMPACT_WAVES + wave;
   const uint64_t wend = min(nwin, (me + 1) * per) * 64;
-  for (uint64_t w0 = me * per * 64; w0 < wend; w0 += 64) {
+  uint64_t w0 = me * per * 64;
+  uint4 pc = pieces[min(w0 + lane, np - 1)];   // unconditional (a load under a branch is waited for at once)
+  for (; w0 < wend; w0 += 64) {
     const uint64_t i = w0 + lane;
-    const uint4 pc = pieces[min(i, np - 1)];   // unconditional (a load under a branch is waited for at once)
     uint32_t c = i < np ? (pc.y & ~HEAVY_PIECE) : 0u;
     const uint64_t rp = row_ptr[c ? pc.x : 0u];
     if (any_heavy && c && (tfl[pc.x] & TF_HEAVY) && !(pc.y & HEAVY_PIECE)) c = 0;
@@ -1269,12 +1274,13 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
     s_src[wave][lane] = pc.z;
     s_dst[wave][lane] = rp + pc.w;
     wave_sync();
-    // four ids per lane per round: their searches, loads and stores overlap
-    for (uint32_t q0 = lane; q0 < tot; q0 += 256) {
-      uint32_t v[4];
-      uint64_t d[4];
+    pc = pieces[min(i + 64, np - 1)];   // the next window's piece, in flight during the copy
+    // COMPACT_IPL ids per lane per round: their searches, loads and stores overlap
+    for (uint32_t q0 = lane; q0 < tot; q0 += 64 * COMPACT_IPL) {
+      uint32_t v[COMPACT_IPL];
+      uint64_t d[COMPACT_IPL];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < COMPACT_IPL; ++r) {
         const uint32_t q = min(q0 + 64u * r, tot - 1);
         uint32_t k = 0;
 #pragma unroll
@@ -1285,8 +1291,10 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
         v[r] = ids_tmp[s_src[wave][k] + o];
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (q0 + 64u * r < tot) ids[d[r]] = v[r];
+      for (int r = 0; r < COMPACT_IPL; ++r)
+        if (q0 + 64u * r < tot) {
+          ids[d[r]] = v[r];   // plain stores: nontemporal ones measured 2x slower here
+        }
     }
     wave_sync();
   }
