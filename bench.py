@@ -39,6 +39,8 @@ WORKLOADS = {
     "c1": "C1: 1M filters (depth 4-8, 20% wildcard) x 10M-topic batch per GPU",
     "c2": "C2: 10M wildcard filters (depth 4-8, '+' p=.15, '#' p=.5) x 10M-topic batch per GPU",
     "c3": "C3: 10M wildcard filters, depth-16 topics, '+' p=.35, '#' p=.7",
+    "c4": "C4: 100M filters (depth 4-8, 20% wildcard) x 10M-topic batch per GPU, match + subscriber fan-out "
+          "(1+Poisson(1) subscribers, 0.1% of filters with 2000, 10% $share groups)",
 }
 
 
@@ -88,7 +90,7 @@ def cpu_baseline(f, t, match_mode: int, seconds: float) -> dict:
     t0 = time.time()
     o.add(f.blob, f.off)
     build_s = time.time() - t0
-    probe = min(t.n, 20_000 * threads)
+    probe = min(t.n, 2_000 * threads)
     sub = t.subset(np.arange(probe))
     t0 = time.time()
     o.match_count(sub.blob, sub.off, threads)
@@ -112,6 +114,20 @@ def cpu_baseline(f, t, match_mode: int, seconds: float) -> dict:
             "cpu_model": cpu_model(), "nproc": os.cpu_count()}
 
 
+def _heartbeat(period: float = 30.0):
+    """Progress on stderr while long host steps (100M-filter generation and
+    table build) run inside ctypes calls, so a watchdog sees a live process."""
+    import threading
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            log(f"[heartbeat] {time.time() - t0:.0f}s")
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -122,11 +138,17 @@ def main():
     ap.add_argument("--topics", type=int, default=None, help="override topics per batch")
     ap.add_argument("--mode", default="replicate", choices=["replicate", "shard"])
     ap.add_argument("--match", default="routes", choices=["routes", "trie"])
+    ap.add_argument("--fanout", default="auto", choices=["auto", "on", "off"],
+                    help="add emqx_broker:dispatch/2 subscriber fan-out to each step (auto: on for c4)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--x-presort", action="store_true",
                     help="EXPERIMENT ONLY: sort the batch on the host before upload (not a valid bench line)")
     args = ap.parse_args()
+    fanout = args.fanout == "on" or (args.fanout == "auto" and args.config == "c4")
+    if fanout and args.mode == "shard":
+        ap.error("--fanout runs with --mode replicate (a shard's fan-out would precede the id gather)")
+    _heartbeat()
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -179,6 +201,14 @@ def main():
         gm.build(f.blob, f.off)
     tstats = gm.stats()
     log(f"[rank {rank}] table built in {time.time() - t0:.1f}s: {tstats}")
+    if fanout:
+        # filter id -> subscriber CSR (emqx_subscriber bag, shards flattened)
+        t0 = time.time()
+        srow, ssubs = synth.subscribers(f.n, lam=1.0, p_big=0.001, n_big=2000, p_share=0.1, seed=seed)
+        gm.subs_build(srow, ssubs)
+        sub_entries = len(ssubs)
+        del srow, ssubs
+        log(f"[rank {rank}] subscriber table: {sub_entries} entries in {time.time() - t0:.1f}s")
 
     # one explicit stream for every kernel and copy of the step (the library
     # and torch share one HIP runtime: emqx_amd._lib loads torch first)
@@ -193,9 +223,19 @@ def main():
     d_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
 
+    fcap = max(8 * n, 1 << 20) if fanout else 0
+    d_drow = torch.zeros(n + 1, dtype=torch.int64, device=dev) if fanout else None
+    d_fid = torch.zeros(fcap, dtype=torch.int32, device=dev) if fanout else None
+    d_sub = torch.zeros(fcap, dtype=torch.int32, device=dev) if fanout else None
+
+    fan_on = False   # enabled once the id buffer holds a whole match batch
+
     def run_local():
         gm.match_device(d_blob.data_ptr(), nbytes, d_off.data_ptr(), n, mode, sp, d_row.data_ptr(),
                         d_ids.data_ptr(), cap)
+        if fan_on:
+            gm.fanout_device(d_row.data_ptr(), d_ids.data_ptr(), cap, n, sp, d_drow.data_ptr(), d_fid.data_ptr(),
+                             d_sub.data_ptr(), fcap)
 
     exchange = None
     if args.mode == "shard" and world > 1:
@@ -227,6 +267,17 @@ def main():
         cap = int(st["n_ids"] * 1.25) + 1024
         d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
         log(f"[rank {rank}] grew id buffer to {cap}")
+    if fanout:
+        fan_on = True
+        step()
+        torch.cuda.synchronize(dev)
+        need = int(d_drow[n].item())
+        if need > fcap:   # k_fan_fill wrote nothing: size the delivery buffers and run again
+            fcap = int(need * 1.1) + 1024
+            del d_fid, d_sub
+            d_fid = torch.zeros(fcap, dtype=torch.int32, device=dev)
+            d_sub = torch.zeros(fcap, dtype=torch.int32, device=dev)
+            log(f"[rank {rank}] grew delivery buffers to {fcap}")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -249,6 +300,9 @@ def main():
         elapsed = float(e.item())
     tim = gm.get_timing()
     st = gm.last_stats()
+    deliveries = int(d_drow[n].item()) if fanout else None
+    if fanout:
+        assert deliveries <= fcap, (deliveries, fcap)
     wc = gm.walk_counters()
     gm.set_timing(False)
 
@@ -268,7 +322,10 @@ def main():
     traffic = walk_traffic(args.config, f.n, n) if args.mode == "replicate" or world == 1 else None
     if rank == 0:
         cpu = None
-        if args.cpu_baseline == "auto" and world == 1:
+        if args.cpu_baseline == "auto" and world == 1 and f.n > 20_000_000:
+            log("[rank 0] CPU baseline skipped: the string-keyed oracle table does not fit this host at "
+                f"{f.n} filters")
+        elif args.cpu_baseline == "auto" and world == 1:
             log("[rank 0] timing the CPU baseline ...")
             cpu = cpu_baseline(f, t, mode, args.cpu_seconds)
         line = {
@@ -289,6 +346,11 @@ def main():
             "stats": {"ids_per_step": n_ids, "visited_per_step": visited, "levels_per_step": sum_d,
                       "deferred_chunks": st["deferred_chunks"], "walk_iters": wc["iters"],
                       "walk_popped": wc["popped"], "walk_lane_occupancy": wc["lane_occupancy"]},
+            "fanout": ({"deliveries_per_step": deliveries, "subscriber_entries": sub_entries,
+                        "fanout_ms": tim["fanout_ms"] / max(1, tim["fanout_launches"]),
+                        "deliveries_per_s": deliveries * world * args.steps / elapsed,
+                        "bytes_per_launch": 12 * deliveries + 20 * n_ids + 8 * (n + 1)}
+                       if fanout else None),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -298,4 +360,11 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except BaseException:
+        # leave at once: after a device fault the runtime's teardown can hang
+        import traceback
+        traceback.print_exc()
+        sys.stderr.flush()
+        os._exit(1)

@@ -95,7 +95,7 @@ SIGNATURES = {
     "egm_get_timing": (C.c_int, [_P, C.POINTER(C.c_double), _u64p, C.POINTER(C.c_double), _u64p]),
     "egm_subs_build": (C.c_int, [_P, _P, C.c_uint32, _P]),
     "egm_fanout_batch": (C.c_int, [_P, C.POINTER(egm_result), C.POINTER(C.POINTER(egm_delivery))]),
-    "egm_fanout_device": (C.c_int, [_P, _P, _P, C.c_uint32, _P, _P, _P, _P, C.c_uint64]),
+    "egm_fanout_device": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P, _P, C.c_uint64]),
     "egm_result_free": (None, [_P]),
     "egm_rstore_open": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "egm_rstore_close": (None, [_P]),

@@ -109,7 +109,7 @@ struct egm_ctx {
   hipStream_t last_stream = nullptr;
 
   // fan-out
-  DevBuf sub_row, sub_ids, f_dc, f_dpos, f_tiles, f_ovf, f_mrow, f_mids, f_drow, f_dfid, f_dsub;
+  DevBuf sub_row, sub_ids, f_dc, f_ds0, f_dpos, f_tiles, f_ovf, f_mrow, f_mids, f_drow, f_dfid, f_dsub;
   uint32_t n_fid_slots = 0;
 
   // timing
@@ -789,14 +789,17 @@ int egm_subs_build(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint
   return EGM_OK;
 }
 
-static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids, uint32_t n, hipStream_t s,
+static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids, uint64_t mids_len, uint32_t n,
+                      hipStream_t s,
                       uint64_t* d_drow, uint32_t* d_fid, uint32_t* d_sub, uint64_t cap, uint64_t* total) {
   uint64_t nids = 0;
   hipError_t e = hipMemcpyAsync(&nids, d_mrow + n, 8, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return c->hip_fail(e, "match_row readback");
   if (nids >= 0xFFFFFFF0ull) return c->fail(EGM_E_INVAL, "too many matched ids for one fan-out batch");
+  if (nids > mids_len) return c->fail(EGM_E_OVERFLOW, "match row total exceeds the id buffer (overflowed match batch)");
   if ((e = c->f_dc.ensure((nids + 1) * 4)) != hipSuccess) return c->hip_fail(e, "f_dc");
+  if ((e = c->f_ds0.ensure((nids + 1) * 8)) != hipSuccess) return c->hip_fail(e, "f_ds0");
   if ((e = c->f_dpos.ensure((nids + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_dpos");
   if ((e = c->f_tiles.ensure((scan_tiles((uint32_t)nids) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_tiles");
   if ((e = c->f_ovf.ensure(16)) != hipSuccess) return c->hip_fail(e, "f_ovf");
@@ -807,7 +810,7 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
     evp[1] = c->take_event();
   }
   e = launch_fanout(st, d_mrow, d_mids, n, nids, d_drow, d_fid, d_sub, cap, c->f_dc.as<uint32_t>(),
-                    c->f_dpos.as<uint64_t>(), c->f_tiles.as<uint64_t>(), c->f_ovf.as<unsigned int>(), s,
+                    c->f_ds0.as<uint64_t>(), c->f_dpos.as<uint64_t>(), c->f_tiles.as<uint64_t>(), c->f_ovf.as<unsigned int>(), s,
                     c->timing ? evp : nullptr);
   if (c->timing) {
     c->ev_fan.push_back(evp[0]);
@@ -825,13 +828,14 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   return EGM_OK;
 }
 
-int egm_fanout_device(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids, uint32_t n, void* hip_stream,
+int egm_fanout_device(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids, uint64_t mids_len, uint32_t n,
+                      void* hip_stream,
                       uint64_t* d_drow, uint32_t* d_fid, uint32_t* d_sub, uint64_t cap) {
   if (!c || !d_mrow || !d_drow) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
-  return run_fanout(c, d_mrow, d_mids, n, s, d_drow, d_fid, d_sub, cap, nullptr);
+  return run_fanout(c, d_mrow, d_mids, mids_len, n, s, d_drow, d_fid, d_sub, cap, nullptr);
 }
 
 int egm_fanout_batch(egm_ctx* c, const egm_result* m, egm_delivery** out) {
@@ -854,7 +858,7 @@ int egm_fanout_batch(egm_ctx* c, const egm_result* m, egm_delivery** out) {
   for (int attempt = 0; attempt < 2; ++attempt) {
     if ((e = c->f_dfid.ensure(cap * 4)) != hipSuccess) return c->hip_fail(e, "f_dfid");
     if ((e = c->f_dsub.ensure(cap * 4)) != hipSuccess) return c->hip_fail(e, "f_dsub");
-    int r = run_fanout(c, c->f_mrow.as<uint64_t>(), c->f_mids.as<uint32_t>(), n, s, c->f_drow.as<uint64_t>(),
+    int r = run_fanout(c, c->f_mrow.as<uint64_t>(), c->f_mids.as<uint32_t>(), nids, n, s, c->f_drow.as<uint64_t>(),
                        c->f_dfid.as<uint32_t>(), c->f_dsub.as<uint32_t>(), cap, &total);
     if (r == EGM_OK) break;
     if (r != EGM_E_OVERFLOW || attempt == 1) return r;

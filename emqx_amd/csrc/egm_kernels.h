@@ -103,8 +103,9 @@ struct SubTable {
 };
 hipError_t launch_fanout(const SubTable& st, const uint64_t* match_row, const uint32_t* match_ids,
                          uint32_t n, uint64_t nids, uint64_t* deliv_row, uint32_t* deliv_fid,
-                         uint32_t* deliv_sub, uint64_t deliv_cap, uint32_t* dcount, uint64_t* dpos,
-                         uint64_t* tile_sums, unsigned int* overflow, hipStream_t s, hipEvent_t* ev);
+                         uint32_t* deliv_sub, uint64_t deliv_cap, uint32_t* dcount, uint64_t* dsrc,
+                         uint64_t* dpos, uint64_t* tile_sums, unsigned int* overflow, hipStream_t s,
+                         hipEvent_t* ev);
 
 // Scatter n records of rec_bytes (4, 16 or 32) from src[] to dst[idx[i]]:
 // the incremental epoch commit of egm_capi.cpp.

@@ -903,10 +903,19 @@ __global__ EGM_WALK_LB void k_walk(DevTable tab, const uint32_t* __restrict__ of
       wave_sync();                                                                                     \
     }
 
-// Pop up to 64 items (one per lane) and issue all their reads.
+// Pop up to 64 items (one per lane) and issue all their reads.  An item
+// pushes at most two children (net +1), so popping k <= room - dmax items
+// keeps room >= dmax afterwards; with room <= dmax the wave pops one item at a
+// time, i.e. a plain DFS, whose stack grows by at most one pending sibling per
+// level below the top item (< dmax).  So the frontier never overflows the LDS
+// stack: a deep, wide one (C3: depth 16, '+' p=.35) narrows the wave instead of
+// deferring the chunk to k_heavy.
 #define WALK_POP(P, TAKE)                                                                              \
     {                                                                                                  \
-      const uint32_t take_ = min(64u, sp), bi_ = sp - take_;                                           \
+      const uint32_t room_ = (uint32_t)WALK_STACK - sp;                                                \
+      const uint32_t lim_ = room_ > dmax ? room_ - dmax : (room_ ? 1u : 0u);                          \
+      const uint32_t take_ = min(min(64u, sp), lim_), bi_ = sp - take_;                                \
+      if (take_ == 0 && sp) ovf = true;                                                                \
       P.act = lane < take_;                                                                            \
       P.it = L.stack[min(bi_ + lane, (uint32_t)WALK_STACK - 1)]; /* unconditional: see issue() */     \
       sp = bi_;                                                                                        \
@@ -1349,14 +1358,23 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
 // matched filter, the {shard, Topic, I} bags flattened into the same list
 // (:297-308, emqx_broker_helper.erl:82-86), shared groups as (filter, group)
 // entries (emqx_broker.erl:246-247).  Flattened over match entries: count ->
-// scan -> fill, so a 2 000-subscriber filter costs one lane's loop, not a
-// whole topic's.
+// scan -> fill.  The fill is wave-cooperative: a wave takes a window of 64
+// match entries, whose deliveries are contiguous in the output (the scan), and
+// its lanes write them in order — coalesced stores, and a 2 000-subscriber
+// filter is spread over 64 lanes instead of looping in one.
 __global__ __launch_bounds__(256) void k_fan_count(const uint32_t* __restrict__ mids, uint64_t nids,
-                                                   SubTable st, uint32_t* __restrict__ dc) {
+                                                   SubTable st, uint32_t* __restrict__ dc,
+                                                   uint64_t* __restrict__ ds0) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nids;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t f = mids[i];
-    dc[i] = f < st.n_fid_slots ? (uint32_t)(st.row[f + 1] - st.row[f]) : 0u;
+    uint64_t r0 = 0, r1 = 0;
+    if (f < st.n_fid_slots) {
+      r0 = st.row[f];
+      r1 = st.row[f + 1];
+    }
+    dc[i] = (uint32_t)(r1 - r0);
+    ds0[i] = r0;   // the fill reads this coalesced instead of re-probing the row table
   }
 }
 
@@ -1366,38 +1384,58 @@ __global__ __launch_bounds__(256) void k_fan_rows(const uint64_t* __restrict__ m
     drow[t] = dpos[mrow[t]];
 }
 
-__global__ __launch_bounds__(256) void k_fan_fill(const uint32_t* __restrict__ mids, uint64_t nids, SubTable st,
-                                                  const uint32_t* __restrict__ dc, const uint64_t* __restrict__ dpos,
-                                                  uint32_t* __restrict__ dfid, uint32_t* __restrict__ dsub,
-                                                  uint64_t cap, unsigned int* overflow) {
+constexpr int FAN_WAVES = 4;
+__global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __restrict__ mids, uint64_t nids,
+                                                             SubTable st, const uint64_t* __restrict__ ds0,
+                                                             const uint64_t* __restrict__ dpos,
+                                                             uint32_t* __restrict__ dfid, uint32_t* __restrict__ dsub,
+                                                             uint64_t cap, unsigned int* overflow) {
   if (dpos[nids] > cap) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *overflow = 1u;
     return;
   }
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nids;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t f = mids[i], c = dc[i];
-    if (!c) continue;
-    const uint64_t s0 = st.row[f], d = dpos[i];
-    for (uint32_t k = 0; k < c; ++k) {
-      dfid[d + k] = f;
-      dsub[d + k] = st.subs[s0 + k];
+  __shared__ uint32_t s_pre[FAN_WAVES][64], s_fid[FAN_WAVES][64];
+  __shared__ uint64_t s_src[FAN_WAVES][64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t nwin = (nids + 63) / 64;
+  for (uint64_t w = (uint64_t)blockIdx.x * FAN_WAVES + wave; w < nwin; w += (uint64_t)gridDim.x * FAN_WAVES) {
+    const uint64_t w0 = w * 64, i = min(w0 + lane, nids);   // lanes past the end read dpos[nids]
+    const uint64_t base = dpos[w0], tot = dpos[min(w0 + 64, nids)] - base;
+    s_pre[wave][lane] = (uint32_t)(dpos[i] - base);
+    s_fid[wave][lane] = mids[min(i, nids - 1)];
+    s_src[wave][lane] = ds0[min(i, nids - 1)];
+    wave_sync();
+    for (uint64_t q = lane; q < tot; q += 64) {
+      // the entry owning output q: the last k with pre[k] <= q (a zero-count entry
+      // shares its successor's pre, so the last one found has deliveries)
+      uint32_t k = 0;
+#pragma unroll
+      for (uint32_t b = 32; b; b >>= 1)
+        if (s_pre[wave][k + b] <= q) k += b;
+      const uint32_t o = (uint32_t)q - s_pre[wave][k];
+      dfid[base + q] = s_fid[wave][k];
+      dsub[base + q] = st.subs[s_src[wave][k] + o];
     }
+    wave_sync();
   }
 }
 
 hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_t* mids, uint32_t n,
                          uint64_t nids, uint64_t* drow, uint32_t* dfid, uint32_t* dsub, uint64_t cap,
-                         uint32_t* dc, uint64_t* dpos, uint64_t* tile_sums, unsigned int* overflow,
-                         hipStream_t s, hipEvent_t* ev) {
+                         uint32_t* dc, uint64_t* ds0, uint64_t* dpos, uint64_t* tile_sums,
+                         unsigned int* overflow, hipStream_t s, hipEvent_t* ev) {
   hipError_t e = hipMemsetAsync(overflow, 0, 4, s);
   if (e != hipSuccess) return e;
   if (ev) hipEventRecord(ev[0], s);
   const uint32_t g = (uint32_t)std::min<uint64_t>((nids + 255) / 256 + 1, 8192);
-  if (nids) hipLaunchKernelGGL(k_fan_count, dim3(g), dim3(256), 0, s, mids, nids, st, dc);
+  if (nids) hipLaunchKernelGGL(k_fan_count, dim3(g), dim3(256), 0, s, mids, nids, st, dc, ds0);
   scan_counts(dc, (uint32_t)nids, tile_sums, dpos, s);
   hipLaunchKernelGGL(k_fan_rows, dim3(std::min<uint32_t>(n / 256 + 1, 8192)), dim3(256), 0, s, mrow, n, dpos, drow);
-  if (nids) hipLaunchKernelGGL(k_fan_fill, dim3(g), dim3(256), 0, s, mids, nids, st, dc, dpos, dfid, dsub, cap, overflow);
+  if (nids) {
+    const uint32_t gf = (uint32_t)std::min<uint64_t>((nids + 64 * FAN_WAVES - 1) / (64 * FAN_WAVES), 16384);
+    hipLaunchKernelGGL(k_fan_fill, dim3(gf), dim3(64 * FAN_WAVES), 0, s, mids, nids, st, ds0, dpos, dfid, dsub, cap,
+                       overflow);
+  }
   if (ev) hipEventRecord(ev[1], s);
   return hipGetLastError();
 }

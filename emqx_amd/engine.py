@@ -236,10 +236,10 @@ class GpuMatcher:
         finally:
             self.lib.egm_result_free(out)
 
-    def fanout_device(self, d_mrow: int, d_mids: int, n: int, stream: int, d_drow: int, d_fid: int, d_sub: int,
-                      cap: int):
-        self._check(self.lib.egm_fanout_device(self.ctx, d_mrow, d_mids, n, stream or None, d_drow, d_fid,
-                                               d_sub, cap), "egm_fanout_device")
+    def fanout_device(self, d_mrow: int, d_mids: int, mids_len: int, n: int, stream: int, d_drow: int, d_fid: int,
+                      d_sub: int, cap: int):
+        self._check(self.lib.egm_fanout_device(self.ctx, d_mrow, d_mids, mids_len, n, stream or None, d_drow,
+                                               d_fid, d_sub, cap), "egm_fanout_device")
 
 
 class TableImage:

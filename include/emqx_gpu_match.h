@@ -159,9 +159,11 @@ int egm_get_timing(egm_ctx* ctx, double* walk_ms, uint64_t* walk_launches, doubl
 /* filter id -> subscriber ids CSR (sub | 0x80000000 marks a shared group id). */
 int egm_subs_build(egm_ctx* ctx, const uint64_t* row_ptr, uint32_t n_fid_slots, const uint32_t* subs);
 int egm_fanout_batch(egm_ctx* ctx, const egm_result* matched, egm_delivery** out);
-/* Device variant over a device CSR match result. */
+/* Device variant over a device CSR match result.  match_ids_len = entries
+   d_match_ids holds: a match row whose total exceeds it (an overflowed match
+   batch) returns EGM_E_OVERFLOW before any kernel reads the ids. */
 int egm_fanout_device(egm_ctx* ctx, const uint64_t* d_match_row, const uint32_t* d_match_ids,
-                      uint32_t n_topics, void* hip_stream, uint64_t* d_deliv_row, uint32_t* d_fid,
+                      uint64_t match_ids_len, uint32_t n_topics, void* hip_stream, uint64_t* d_deliv_row, uint32_t* d_fid,
                       uint32_t* d_sub, uint64_t deliv_cap);
 
 void egm_result_free(void* result);

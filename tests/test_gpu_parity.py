@@ -355,6 +355,7 @@ def test_fanout_vs_oracle(gm):
     f, t = synth.config("c0", n_topics=20_000)
     gm.build(f.blob, f.off)
     res = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    assert len(res.ids) > 0
     row, subs = synth.subscribers(f.n, p_big=0.002, n_big=2000, p_share=0.1)
     gm.subs_build(row, subs)
     drow, dfid, dsub = gm.fanout(res)
@@ -366,6 +367,71 @@ def test_fanout_vs_oracle(gm):
         got = list(zip(dfid[drow[i]:drow[i + 1]].tolist(), dsub[drow[i]:drow[i + 1]].tolist()))
         assert sorted(got) == sorted(want)
     assert drow[-1] == sum(int(row[x + 1] - row[x]) for x in res.ids.tolist())
+
+
+def _expected_deliveries(mids, srow, subs):
+    """emqx_broker:dispatch/2 order: per match entry, its filter's subscriber row."""
+    mids = mids.astype(np.int64)
+    cnt = (srow[mids + 1] - srow[mids]).astype(np.int64)
+    fid = np.repeat(mids, cnt)
+    starts = np.repeat(srow[mids].astype(np.int64) - np.concatenate([[0], np.cumsum(cnt)[:-1]]), cnt)
+    sub = subs[starts + np.arange(int(cnt.sum()))]
+    return fid.astype(np.uint32), sub.astype(np.uint32)
+
+
+def test_fanout_device_exact_and_guarded(gm):
+    """Device fan-out (the bench's C4 step) element-for-element against numpy,
+    with 1% of filters at 2 000 subscribers (windows of one wave spanning
+    thousands of deliveries); an overflowed match batch is refused, not read."""
+    import torch
+    f, t = synth.config("c1", n_filters=50_000, n_topics=30_000)
+    gm.build(f.blob, f.off)
+    srow, subs = synth.subscribers(f.n, p_big=0.01, n_big=2000, p_share=0.1)
+    gm.subs_build(srow, subs)
+    host = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    assert len(host.ids) > 0, gm.stats()
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    d_blob = torch.from_numpy(t.blob).to(dev)
+    d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+    n, cap = t.n, len(host.ids) + 64
+    d_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
+    gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES, s,
+                    d_row.data_ptr(), d_ids.data_ptr(), cap)
+    torch.cuda.synchronize()   # stream 0 means "the context's stream" at the C-ABI: wait for every stream
+    mrow = d_row.cpu().numpy().view(np.uint64)
+    mids = d_ids.cpu().numpy().view(np.uint32)[: int(mrow[-1])]
+    assert np.array_equal(mrow, host.row_ptr), (int(mrow[-1]), len(host.ids), gm.last_stats())
+    want_fid, want_sub = _expected_deliveries(mids, srow, subs)
+    tot = len(want_fid)
+    assert tot > 100_000
+    d_drow = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    d_fid = torch.zeros(tot + 8, dtype=torch.int32, device=dev)
+    d_sub = torch.zeros(tot + 8, dtype=torch.int32, device=dev)
+    gm.fanout_device(d_row.data_ptr(), d_ids.data_ptr(), cap, n, s, d_drow.data_ptr(), d_fid.data_ptr(),
+                     d_sub.data_ptr(), tot + 8)
+    torch.cuda.synchronize()
+    drow = d_drow.cpu().numpy().view(np.uint64)
+    cnt = (srow[mids.astype(np.int64) + 1] - srow[mids.astype(np.int64)]).astype(np.uint64)
+    want_row = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint64)[mrow.astype(np.int64)]
+    assert np.array_equal(drow, want_row)
+    assert np.array_equal(d_fid.cpu().numpy().view(np.uint32)[:tot], want_fid)
+    assert np.array_equal(d_sub.cpu().numpy().view(np.uint32)[:tot], want_sub)
+    # the host-buffer API gives the same rows
+    hrow, hfid, hsub = gm.fanout(host)
+    assert int(hrow[-1]) == tot
+    # delivery buffer too small: nothing written past it, the total still reported
+    gm.fanout_device(d_row.data_ptr(), d_ids.data_ptr(), cap, n, s, d_drow.data_ptr(), d_fid.data_ptr(),
+                     d_sub.data_ptr(), 1000)
+    torch.cuda.synchronize()
+    assert int(d_drow[n].item()) == tot
+    # an overflowed match batch (row total > id buffer) is refused before any kernel reads ids
+    gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES, s,
+                    d_row.data_ptr(), d_ids.data_ptr(), 16)
+    with pytest.raises(L.EgmError):
+        gm.fanout_device(d_row.data_ptr(), d_ids.data_ptr(), 16, n, s, d_drow.data_ptr(), d_fid.data_ptr(),
+                         d_sub.data_ptr(), tot + 8)
 
 
 @pytest.mark.slow

@@ -1,0 +1,8 @@
+# Walk pop throttle: GPU parity subset, C3 and C2 benches under rocprof
+source tools/gpu_steps.sh
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_api.py -m "gpu and not slow" -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+run c3 420 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_c3 -o run --output-format csv -- python $R/bench.py --config c3 --steps 10 --warmup 2 --cpu-baseline off
+run c2 420 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_c2 -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 3 --cpu-baseline off
