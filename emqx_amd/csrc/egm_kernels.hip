@@ -255,7 +255,10 @@ __device__ __forceinline__ uint32_t dict_resolve(const DevTable& tab, uint64_t h
 //   2. lane per topic: record every word's (start, length, output index)
 //   3. lane per word, two words per lane in flight: FNV-1a of its bytes, the
 //      '+'/'#' words, the byte-exact dictionary probe -> wid[off[t] + t + l]
-// Blocks whose bytes or words do not fit LDS take the lane-per-topic path.
+// The block's topics are taken in segments of S topics, S halved until the
+// segment's bytes fit TOK_LDS and its words TOK_WORDS (C3's depth-16 topics
+// of ~100 B: two segments of 128).  Only a single topic too long for LDS
+// takes the lane-per-topic path from global memory.
 __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint8_t* __restrict__ blob,
                                                         const uint32_t* __restrict__ off, uint32_t n,
                                                         uint32_t* __restrict__ wid, uint32_t* __restrict__ lv,
@@ -263,137 +266,154 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
   __shared__ __attribute__((aligned(16))) uint32_t sw[TOK_LDS / 4 + 1];   // +1: lds_word reads one word past
   __shared__ uint32_t wpos[TOK_WORDS];   // start | len << 16 (LDS byte index)
   __shared__ uint32_t wdst[TOK_WORDS];   // index into wid[]
-  __shared__ uint8_t wtop[TOK_WORDS];    // topic within the block
-  __shared__ uint32_t tbase[TOK_BLOCK];
+  __shared__ uint8_t wtop[TOK_WORDS];    // topic within the segment
   __shared__ uint32_t tflag[TOK_BLOCK];
   __shared__ uint32_t wsum[TOK_BLOCK / 64];
-  const uint32_t t0 = blockIdx.x * TOK_BLOCK;
-  if (t0 >= n) return;
+  const uint32_t blk0 = blockIdx.x * TOK_BLOCK;
+  if (blk0 >= n) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uint32_t t1 = min(t0 + (uint32_t)TOK_BLOCK, n);
-  const uint32_t s = off[t0], e = off[t1];
-  const uint32_t sa = s & ~3u;
-  const uint32_t ea = (e + 3u) & ~3u;   // blob is readable up to a multiple of 4 (ABI)
-  const bool staged = (ea - sa) <= (uint32_t)TOK_LDS && (ea - sa) < 32768u;
-  const uint32_t t = t0 + tid;
-  if (!staged) {   // long topics: lane per topic straight from global memory
-    if (t < t1) {
-      const uint32_t ts = off[t], len = off[t + 1] - ts;
-      uint32_t l;
-      uint8_t fl;
-      tokenise_one(tab, (const uint32_t*)(blob + (ts & ~3u)), ts & 3u, len, ts + t, wid, &l, &fl);
-      lv[t] = l;
-      tfl[t] = fl;
+  const uint32_t tend = min(blk0 + (uint32_t)TOK_BLOCK, n);
+  uint32_t S = TOK_BLOCK;
+  for (uint32_t t0 = blk0; t0 < tend;) {
+    // block-uniform segment choice: every thread reads the same offsets
+    uint32_t t1, sa, ea;
+    for (;;) {
+      t1 = min(t0 + S, tend);
+      sa = off[t0] & ~3u;
+      ea = (off[t1] + 3u) & ~3u;   // blob is readable up to a multiple of 4 (ABI)
+      if ((ea - sa) <= (uint32_t)TOK_LDS || S == 1) break;
+      S >>= 1;
     }
-    return;
-  }
-  {
-    const uint32_t nw = (ea - sa) >> 2;
-    const uint32_t* src = (const uint32_t*)(blob + sa);
-    for (uint32_t i = tid; i < nw; i += TOK_BLOCK) sw[i] = src[i];
-  }
-  __syncthreads();
-
-  // ---- pass 1: levels per topic ----
-  uint32_t ts = 0, len = 0, D = 0, fl = 0;
-  if (t < t1) {
-    ts = off[t] - sa;
-    len = off[t + 1] - off[t];
-    uint32_t c = 0;
-    for (uint32_t q = ts & ~3u; q < ts + len; q += 4) {
-      const uint32_t lo = q < ts ? ts - q : 0u, hi = min(4u, ts + len - q);
-      c += popc((uint64_t)(slash_mask(sw[q >> 2]) & byte_range(lo, hi)));
-    }
-    D = c + 1;
-    if (len > 0 && lds_byte(sw, ts) == '$') fl |= TF_DOLLAR;
-  }
-  uint32_t wtot;
-  uint32_t ex = wave_excl_scan(D, lane, &wtot);
-  if (lane == 0) wsum[wv] = wtot;
-  __syncthreads();
-  uint32_t W = 0;
-#pragma unroll
-  for (int k = 0; k < TOK_BLOCK / 64; ++k) {
-    if ((uint32_t)k < wv) ex += wsum[k];
-    W += wsum[k];
-  }
-  if (W > (uint32_t)TOK_WORDS) {   // too many words for LDS: lane per topic
-    if (t < t1) {
-      uint32_t l;
-      uint8_t f;
-      tokenise_one(tab, sw, ts, len, off[t] + t, wid, &l, &f);
-      lv[t] = l;
-      tfl[t] = f;
-    }
-    return;
-  }
-  tflag[tid] = fl;
-
-  // ---- pass 2: word boundaries ----
-  if (t < t1) {
-    const uint32_t g = off[t] + t;   // wid index of the topic's first word
-    uint32_t l = 0, ws = ts;
-    for (uint32_t q = ts & ~3u; q < ts + len; q += 4) {
-      const uint32_t lo = q < ts ? ts - q : 0u, hi = min(4u, ts + len - q);
-      uint32_t m = slash_mask(sw[q >> 2]) & byte_range(lo, hi);
-      while (m) {
-        const uint32_t p = q + (__builtin_ctz(m) >> 3);
-        m &= m - 1;
-        wpos[ex + l] = ws | ((p - ws) << 16);
-        wdst[ex + l] = g + l;
-        wtop[ex + l] = (uint8_t)tid;
-        ++l;
-        ws = p + 1;
+    const uint32_t t = t0 + tid;
+    if ((ea - sa) > (uint32_t)TOK_LDS) {   // one topic longer than LDS: lane path from global memory
+      if (tid == 0) {
+        const uint32_t ts = off[t0], len = off[t0 + 1] - ts;
+        uint32_t l;
+        uint8_t fl;
+        tokenise_one(tab, (const uint32_t*)(blob + (ts & ~3u)), ts & 3u, len, ts + t0, wid, &l, &fl);
+        lv[t0] = l;
+        tfl[t0] = fl;
       }
+      t0 = t1;
+      continue;
     }
-    wpos[ex + l] = ws | ((ts + len - ws) << 16);
-    wdst[ex + l] = g + l;
-    wtop[ex + l] = (uint8_t)tid;
-    lv[t] = D;
-  }
-  __syncthreads();
+    {
+      const uint32_t nw = (ea - sa) >> 2;
+      const uint32_t* src = (const uint32_t*)(blob + sa);
+      for (uint32_t i = tid; i < nw; i += TOK_BLOCK) sw[i] = src[i];
+    }
+    __syncthreads();
 
-  // ---- pass 3: hash + dictionary probe, lane per word ----
-  for (uint32_t i0 = tid; i0 < W; i0 += 2 * TOK_BLOCK) {
-    uint32_t st[2], wl[2], res[2];
-    uint64_t h[2];
-    bool act[2], spec[2];
+    // ---- pass 1: levels per topic ----
+    uint32_t ts = 0, len = 0, D = 0, fl = 0;
+    if (t < t1) {
+      ts = off[t] - sa;
+      len = off[t + 1] - off[t];
+      uint32_t c = 0;
+      for (uint32_t q = ts & ~3u; q < ts + len; q += 4) {
+        const uint32_t lo = q < ts ? ts - q : 0u, hi = min(4u, ts + len - q);
+        c += popc((uint64_t)(slash_mask(sw[q >> 2]) & byte_range(lo, hi)));
+      }
+      D = c + 1;
+      if (len > 0 && lds_byte(sw, ts) == '$') fl |= TF_DOLLAR;
+    }
+    uint32_t wtot;
+    uint32_t ex = wave_excl_scan(D, lane, &wtot);
+    if (lane == 0) wsum[wv] = wtot;
+    __syncthreads();
+    uint32_t W = 0;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const uint32_t i = i0 + u * TOK_BLOCK;
-      act[u] = i < W;
-      const uint32_t pw = act[u] ? wpos[i] : 0u;
-      st[u] = pw & 0xFFFFu;
-      wl[u] = pw >> 16;
-      h[u] = lds_word_hash(sw, st[u], wl[u]);
-      spec[u] = false;
-      res[u] = WID_NONE;
-      if (wl[u] == 1) {
-        const uint32_t c = lds_byte(sw, st[u]);
-        if (c == '+' || c == '#') {
-          spec[u] = true;
-          res[u] = c == '+' ? WID_PLUS : WID_HASH;
+    for (int k = 0; k < TOK_BLOCK / 64; ++k) {
+      if ((uint32_t)k < wv) ex += wsum[k];
+      W += wsum[k];
+    }
+    __syncthreads();   // wsum and sw are rewritten by the next segment
+    if (W > (uint32_t)TOK_WORDS) {
+      if (S > 1) {     // too many words: retry the same topics in a smaller segment
+        S >>= 1;
+        continue;
+      }
+      if (tid == 0) {  // one topic with more words than LDS holds
+        uint32_t l;
+        uint8_t f;
+        tokenise_one(tab, sw, ts, len, off[t] + t, wid, &l, &f);
+        lv[t] = l;
+        tfl[t] = f;
+      }
+      __syncthreads();
+      t0 = t1;
+      continue;
+    }
+    tflag[tid] = fl;
+
+    // ---- pass 2: word boundaries ----
+    if (t < t1) {
+      const uint32_t g = off[t] + t;   // wid index of the topic's first word
+      uint32_t l = 0, ws = ts;
+      for (uint32_t q = ts & ~3u; q < ts + len; q += 4) {
+        const uint32_t lo = q < ts ? ts - q : 0u, hi = min(4u, ts + len - q);
+        uint32_t m = slash_mask(sw[q >> 2]) & byte_range(lo, hi);
+        while (m) {
+          const uint32_t p = q + (__builtin_ctz(m) >> 3);
+          m &= m - 1;
+          wpos[ex + l] = ws | ((p - ws) << 16);
+          wdst[ex + l] = g + l;
+          wtop[ex + l] = (uint8_t)tid;
+          ++l;
+          ws = p + 1;
         }
       }
+      wpos[ex + l] = ws | ((ts + len - ws) << 16);
+      wdst[ex + l] = g + l;
+      wtop[ex + l] = (uint8_t)tid;
+      lv[t] = D;
     }
-    uint4 a[2], b[2];
+    __syncthreads();
+
+    // ---- pass 3: hash + dictionary probe, lane per word ----
+    for (uint32_t i0 = tid; i0 < W; i0 += 2 * TOK_BLOCK) {
+      uint32_t st[2], wl[2], res[2];
+      uint64_t h[2];
+      bool act[2], spec[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {   // both first-slot reads in flight (unconditional: see issue())
-      const uint8_t* sp = (const uint8_t*)(tab.dict + ((act[u] && !spec[u]) ? ((uint32_t)h[u] & tab.dict_mask) : 0u));
-      a[u] = ld16(sp);
-      b[u] = ld16(sp + 16);
-    }
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t i = i0 + u * TOK_BLOCK;
+        act[u] = i < W;
+        const uint32_t pw = act[u] ? wpos[i] : 0u;
+        st[u] = pw & 0xFFFFu;
+        wl[u] = pw >> 16;
+        h[u] = lds_word_hash(sw, st[u], wl[u]);
+        spec[u] = false;
+        res[u] = WID_NONE;
+        if (wl[u] == 1) {
+          const uint32_t c = lds_byte(sw, st[u]);
+          if (c == '+' || c == '#') {
+            spec[u] = true;
+            res[u] = c == '+' ? WID_PLUS : WID_HASH;
+          }
+        }
+      }
+      uint4 a[2], b[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (!act[u]) continue;
-      const uint32_t i = i0 + u * TOK_BLOCK;
-      if (spec[u]) atomicOr(&tflag[wtop[i]], (uint32_t)TF_WILDCARD);
-      else res[u] = dict_resolve(tab, h[u], a[u], b[u], sw, st[u], wl[u]);
-      wid[wdst[i]] = res[u];
+      for (int u = 0; u < 2; ++u) {   // both first-slot reads in flight (unconditional: see issue())
+        const uint8_t* sp = (const uint8_t*)(tab.dict + ((act[u] && !spec[u]) ? ((uint32_t)h[u] & tab.dict_mask) : 0u));
+        a[u] = ld16(sp);
+        b[u] = ld16(sp + 16);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (!act[u]) continue;
+        const uint32_t i = i0 + u * TOK_BLOCK;
+        if (spec[u]) atomicOr(&tflag[wtop[i]], (uint32_t)TF_WILDCARD);
+        else res[u] = dict_resolve(tab, h[u], a[u], b[u], sw, st[u], wl[u]);
+        wid[wdst[i]] = res[u];
+      }
     }
+    __syncthreads();
+    if (t < t1) tfl[t] = (uint8_t)tflag[tid];
+    __syncthreads();   // tflag, wpos and sw are rewritten by the next segment
+    t0 = t1;
   }
-  __syncthreads();
-  if (t < t1) tfl[t] = (uint8_t)tflag[tid];
 }
 
 // ------------------------------------------------------------ NFA expand ----
@@ -1385,8 +1405,10 @@ __global__ __launch_bounds__(256) void k_fan_rows(const uint64_t* __restrict__ m
 }
 
 constexpr int FAN_WAVES = 4;
+constexpr uint32_t FAN_BIG = 128;   // entries with this many subscribers are copied by the whole wave
 __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __restrict__ mids, uint64_t nids,
-                                                             SubTable st, const uint64_t* __restrict__ ds0,
+                                                             SubTable st, const uint32_t* __restrict__ dc,
+                                                             const uint64_t* __restrict__ ds0,
                                                              const uint64_t* __restrict__ dpos,
                                                              uint32_t* __restrict__ dfid, uint32_t* __restrict__ dsub,
                                                              uint64_t cap, unsigned int* overflow) {
@@ -1394,27 +1416,52 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
     if (blockIdx.x == 0 && threadIdx.x == 0) *overflow = 1u;
     return;
   }
-  __shared__ uint32_t s_pre[FAN_WAVES][64], s_fid[FAN_WAVES][64];
+  __shared__ uint32_t s_pre[FAN_WAVES][64], s_off[FAN_WAVES][64], s_fid[FAN_WAVES][64], s_cnt[FAN_WAVES][64];
   __shared__ uint64_t s_src[FAN_WAVES][64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t nwin = (nids + 63) / 64;
   for (uint64_t w = (uint64_t)blockIdx.x * FAN_WAVES + wave; w < nwin; w += (uint64_t)gridDim.x * FAN_WAVES) {
-    const uint64_t w0 = w * 64, i = min(w0 + lane, nids);   // lanes past the end read dpos[nids]
-    const uint64_t base = dpos[w0], tot = dpos[min(w0 + 64, nids)] - base;
-    s_pre[wave][lane] = (uint32_t)(dpos[i] - base);
-    s_fid[wave][lane] = mids[min(i, nids - 1)];
-    s_src[wave][lane] = ds0[min(i, nids - 1)];
+    const uint64_t w0 = w * 64, i = w0 + lane, ic = min(i, nids - 1);
+    const uint64_t base = dpos[w0];
+    const uint32_t c = i < nids ? dc[ic] : 0u;
+    const bool big = c >= FAN_BIG;
+    uint32_t tot_s;
+    const uint32_t pre_s = wave_excl_scan(big ? 0u : c, lane, &tot_s);   // small entries, packed
+    s_pre[wave][lane] = pre_s;
+    s_off[wave][lane] = (uint32_t)(dpos[min(i, nids)] - base);            // real offset in the window
+    s_fid[wave][lane] = mids[ic];
+    s_cnt[wave][lane] = c;
+    s_src[wave][lane] = ds0[ic];
     wave_sync();
-    for (uint64_t q = lane; q < tot; q += 64) {
-      // the entry owning output q: the last k with pre[k] <= q (a zero-count entry
-      // shares its successor's pre, so the last one found has deliveries)
+    // small entries: lane per delivery, the owning entry found by a 6-step search
+    for (uint32_t q = lane; q < tot_s; q += 64) {
+      // the last k with pre[k] <= q (an entry with no small deliveries shares its
+      // successor's pre, so the last one found has deliveries)
       uint32_t k = 0;
 #pragma unroll
       for (uint32_t b = 32; b; b >>= 1)
         if (s_pre[wave][k + b] <= q) k += b;
-      const uint32_t o = (uint32_t)q - s_pre[wave][k];
-      dfid[base + q] = s_fid[wave][k];
-      dsub[base + q] = st.subs[s_src[wave][k] + o];
+      const uint32_t o = q - s_pre[wave][k];
+      const uint64_t d = base + s_off[wave][k] + o;
+      dfid[d] = s_fid[wave][k];
+      dsub[d] = st.subs[s_src[wave][k] + o];
+    }
+    // big entries (C4: 2 000-subscriber filters): the wave streams the row, 4 per lane in flight
+    for (uint64_t mb = __ballot(big); mb; mb &= mb - 1) {
+      const uint32_t k = (uint32_t)__builtin_ctzll(mb);
+      const uint32_t cnt = s_cnt[wave][k], f = s_fid[wave][k];
+      const uint64_t src = s_src[wave][k], dst = base + s_off[wave][k];
+      for (uint32_t j0 = lane; j0 < cnt; j0 += 256) {
+        uint32_t v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = st.subs[src + min(j0 + 64u * r, cnt - 1)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (j0 + 64u * r < cnt) {
+            dfid[dst + j0 + 64u * r] = f;
+            dsub[dst + j0 + 64u * r] = v[r];
+          }
+      }
     }
     wave_sync();
   }
@@ -1433,8 +1480,8 @@ hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_
   hipLaunchKernelGGL(k_fan_rows, dim3(std::min<uint32_t>(n / 256 + 1, 8192)), dim3(256), 0, s, mrow, n, dpos, drow);
   if (nids) {
     const uint32_t gf = (uint32_t)std::min<uint64_t>((nids + 64 * FAN_WAVES - 1) / (64 * FAN_WAVES), 16384);
-    hipLaunchKernelGGL(k_fan_fill, dim3(gf), dim3(64 * FAN_WAVES), 0, s, mids, nids, st, ds0, dpos, dfid, dsub, cap,
-                       overflow);
+    hipLaunchKernelGGL(k_fan_fill, dim3(gf), dim3(64 * FAN_WAVES), 0, s, mids, nids, st, dc, ds0, dpos, dfid, dsub,
+                       cap, overflow);
   }
   if (ev) hipEventRecord(ev[1], s);
   return hipGetLastError();

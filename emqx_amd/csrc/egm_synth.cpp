@@ -127,7 +127,7 @@ void egs_free(egs_strings* s) {
 // wildcard; the rest are all-literal.  p_empty: a literal level is ''.
 int egs_filters(uint64_t seed, uint32_t n, int dmin, int dmax, double wc_frac, double p_plus, double p_hash,
                 double p_empty, double zipf_s, uint32_t vmax, egs_strings* out) {
-  if (!out || dmin < 1 || dmax < dmin || (uint64_t)n * (dmax * 12 + 8) > 0xF0000000ull) return -1;
+  if (!out || dmin < 1 || dmax < dmin) return -1;
   Rng r(seed);
   Vocab voc(zipf_s, vmax);
   Strings res;
@@ -166,6 +166,9 @@ int egs_filters(uint64_t seed, uint32_t n, int dmin, int dmax, double wc_frac, d
     }
   }
   // string_views in `seen` may dangle after reallocation; we reserved n so no realloc
+  uint64_t total = 0;
+  for (const auto& s : store) total += s.size();
+  if (total > 0xFFFFFFF0ull) return -1;   // offsets are u32 (the C-ABI's egm_table_build)
   for (const auto& s : store) res.push(s);
   return export_strings(res, out);
 }

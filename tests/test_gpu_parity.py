@@ -117,6 +117,27 @@ def test_deep_and_long(gm):
             assert got[i] == sorted(want), (mode, t[:40])
 
 
+def test_tokenise_segments_and_long_topics(gm):
+    """k_tokenise splits a block into segments that fit LDS: C3-sized topics
+    (~100 B, 16 levels), a topic longer than the LDS byte stage, one with more
+    words than the LDS word table, and short topics around them in one block."""
+    rng = random.Random(11)
+    huge = b"h" * 30_000 + b"/t"                   # > TOK_LDS bytes: lane path from global memory
+    many = b"/".join([b"w"] * 4_000)               # > TOK_WORDS words
+    deep = [b"/".join(b"d%d_%d" % (l, rng.randrange(4)) for l in range(16)) for _ in range(700)]
+    short = [b"s/%d" % rng.randrange(50) for _ in range(300)]
+    topics = short[:150] + [huge] + deep[:350] + [many] + short[150:] + deep[350:] + [b"", b"$SYS/x", b"a/+"]
+    filters = [b"#", b"s/+", b"h" * 30_000 + b"/+", b"w/w/#", b"$SYS/#", b"a/+", b"/".join([b"+"] * 16),
+               b"d0_1/#", b"d0_2/+/d2_3/#"] + deep[:5] + [b"/".join([b"w"] * 4_000)]
+    gm.build_strings(filters)
+    names = dict(enumerate(filters))
+    for mode in MODES:
+        got = sets_of(gm.match_strings(topics, mode), names)
+        for i, t in enumerate(topics):
+            want = R.trie_semantics(t, filters) if mode == 0 else R.routes_semantics(t, filters)
+            assert got[i] == sorted(want), (mode, i, t[:40])
+
+
 def test_heavy_path_wide_frontier(gm):
     # every filter of depth 11 over {'+', 'k<l>'} : a matching topic hits 2^11
     # filters, far above the per-wave LDS stage -> chunk deferred to k_heavy
