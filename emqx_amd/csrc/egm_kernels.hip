@@ -1260,7 +1260,13 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
 // flush have contiguous sources and topics of one chunk, so the reads and the
 // row_ptr loads coalesce.  Light pieces of topics re-run by k_heavy and unused
 // slab slots (count 0) are skipped.
-constexpr int COMPACT_WAVES = 4;
+#ifndef EGM_COMPACT_WAVES
+#define EGM_COMPACT_WAVES 4
+#endif
+#ifndef EGM_COMPACT_BLOCKS
+#define EGM_COMPACT_BLOCKS 65536   // grid cap; A/B at C2: 8192 -> 2.07 ms, 32768 -> 1.80, 65536 -> 1.74
+#endif
+constexpr int COMPACT_WAVES = EGM_COMPACT_WAVES;
 #ifndef EGM_COMPACT_IPL
 #define EGM_COMPACT_IPL 8   // 8: 2.06 -> 1.91 ms at C2 (A/B, rocprof)
 #endif
@@ -1368,7 +1374,10 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   if (ev_walk) hipEventRecord(ev_walk[1], s);
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
   scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);
-  hipLaunchKernelGGL(k_compact, dim3(8192), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.tfl, w.ids_tmp, n, out.row_ptr, out.ids,
+  // shorter window ranges per wave keep more copies in flight; small batches
+  // get a small grid (the piece count is only known on the device)
+  const uint32_t cblocks = (uint32_t)std::min<uint64_t>(EGM_COMPACT_BLOCKS, std::max<uint64_t>(256, ((uint64_t)n + 63) / 64));
+  hipLaunchKernelGGL(k_compact, dim3(cblocks), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.tfl, w.ids_tmp, n, out.row_ptr, out.ids,
                      out.ids_cap, w.pieces_cap, w.stats);
   return hipGetLastError();
 }
