@@ -52,11 +52,11 @@ constexpr int WALK_WORDS = EGM_WALK_WORDS;
 constexpr int HEAVY_STACK = 6144;    // items (120 KB LDS) per heavy wave
 constexpr int TOK_BLOCK = 256;
 #ifndef EGM_TOK_LDS
-#define EGM_TOK_LDS 24576   // staged topic bytes per tokenise block
+#define EGM_TOK_LDS 16384   // staged topic bytes per tokenise block (A/B at C2: 24 KB -> 1.09 ms, 16 KB -> 0.92, 12 KB -> 1.12)
 #endif
 constexpr int TOK_LDS = EGM_TOK_LDS;
 #ifndef EGM_TOK_WORDS
-#define EGM_TOK_WORDS 3072   // words per tokenise block (9 B of LDS each)
+#define EGM_TOK_WORDS 2048   // words per tokenise block (9 B of LDS each; 34 KB per block -> 4 blocks per CU)
 #endif
 constexpr int TOK_WORDS = EGM_TOK_WORDS;
 constexpr int SCAN_TILE = 2048;      // counts per scan tile (256 threads x 8)
