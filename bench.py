@@ -23,7 +23,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import platform
 import sys
 import time
 
@@ -48,15 +47,15 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_model() -> str:
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return platform.processor() or "unknown"
+def kernel_src_sha() -> str:
+    """Hash of the kernel sources: a PMC traffic record is only used for the
+    build it was collected on (tools/pmc_traffic.py stores the same hash)."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in ("egm_kernels.hip", "egm_kernels.h", "egm_common.h"):
+        with open(os.path.join(ROOT, "emqx_amd", "csrc", name), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def levels_sum(blob: np.ndarray, off: np.ndarray) -> int:
@@ -77,15 +76,17 @@ def walk_traffic(config: str, filters: int, topics: int):
                 r = json.load(fh)
         except (OSError, ValueError):
             continue
-        if r.get("workload") == config and r.get("filters") == filters and r.get("topics") == topics:
+        if (r.get("workload") == config and r.get("filters") == filters and r.get("topics") == topics
+                and r.get("kernel_src_sha") == kernel_src_sha()):
             best = (r, os.path.relpath(p, ROOT))
     return best
 
 
 def cpu_baseline(f, t, match_mode: int, seconds: float) -> dict:
     """C++ restatement of emqx_trie (compact) + route lookup, timed on host cores."""
+    from emqx_amd import hostinfo
     from oracle.cpp import OracleTrie
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = hostinfo.usable_cpus()   # every CPU this process may run on (affinity and cgroup quota)
     o = OracleTrie(True, match_mode)
     t0 = time.time()
     o.add(f.blob, f.off)
@@ -111,7 +112,7 @@ def cpu_baseline(f, t, match_mode: int, seconds: float) -> dict:
             "sample": f"first {n} topics of the same batch, {threads} threads, static partition; "
                       f"C++ restatement of emqx_trie compact DFS + lookup_routes (oracle/trie_oracle.cpp), "
                       f"not BEAM; {m} matches; table build {build_s:.1f}s untimed",
-            "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+            "host": hostinfo.describe()}
 
 
 def _heartbeat(period: float = 30.0):

@@ -630,14 +630,14 @@ int egm_last_commit_stats(egm_ctx* c, uint64_t* h2d_bytes, uint64_t* d2d_bytes, 
   return EGM_OK;
 }
 
-int egm_last_walk_counters(egm_ctx* c, uint64_t* iters, uint64_t* popped, uint32_t* items_per_lane) {
+int egm_last_walk_counters(egm_ctx* c, uint64_t* iters, uint64_t* popped, uint64_t* bounded) {
   if (!c) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   int r = sync_last(c);
   if (r) return r;
   if (iters) *iters = c->last.iters;
   if (popped) *popped = c->last.popped;
-  if (items_per_lane) *items_per_lane = (uint32_t)walk_items_per_lane();
+  if (bounded) *bounded = c->last.bounded;
   return EGM_OK;
 }
 

@@ -29,7 +29,8 @@ struct MatchStats {               // device-side counters, zeroed per batch
   unsigned int overflow;          // bit 0: ids_tmp/pieces full, bit 1: output ids full
   unsigned int errors;            // topics the heavy kernel could not finish
   unsigned long long iters;       // walk iterations (instrumentation)
-  unsigned long long popped;      // items popped by the walk (lane occupancy = popped / (iters * 64 * IPL))
+  unsigned long long popped;      // items popped by the walk (lane occupancy = popped / (iters * 64))
+  unsigned long long bounded;     // walk iterations whose pop was cut by the stack-room bound (DFS regime)
 };
 
 // A piece is one flush's run of a topic's ids in ids_tmp:
@@ -77,7 +78,6 @@ struct MatchOut {                 // CSR result (device)
 constexpr int WALK_CHUNK = EGM_WALK_CHUNK;
 int walk_grid_blocks(uint32_t n_topics);
 int walk_waves_per_block();
-int walk_items_per_lane();
 size_t scan_tiles(uint32_t n);
 // ids_tmp / pieces capacity a batch needs beyond its matched ids: slab tails
 inline uint64_t ids_tmp_capacity(uint64_t ids, uint32_t n) {

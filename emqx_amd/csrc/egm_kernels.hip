@@ -41,10 +41,6 @@ constexpr int WALK_STACK = EGM_WALK_STACK;
 #define EGM_WALK_STAGE 320   // staged matches per flush (7 B each)
 #endif
 constexpr int WALK_STAGE = EGM_WALK_STAGE;
-#ifndef EGM_WALK_IPL
-#define EGM_WALK_IPL 1   // work items per lane per iteration (2 doubles the stack growth per iteration)
-#endif
-constexpr int WALK_IPL = EGM_WALK_IPL;
 #ifndef EGM_WALK_WORDS
 #define EGM_WALK_WORDS 448   // staged topic word ids per wave chunk
 #endif
@@ -105,22 +101,6 @@ __device__ __forceinline__ uint4 empty_piece() {
   return make_uint4(x, z, z, z);
 }
 
-// EGM_FOR_U(stmts): run stmts once per work item of a lane with a constant
-// index u (WALK_IPL <= 2).  A macro, not a lambda: arrays of per-item state
-// indexed by constants then stay in registers (a lambda capturing them by
-// reference made LLVM keep them in scratch).
-#define EGM_FOR_U(...)                                 \
-  do {                                                 \
-    {                                                  \
-      constexpr int u = 0;                             \
-      __VA_ARGS__                                      \
-    }                                                  \
-    if constexpr (WALK_IPL > 1) {                      \
-      constexpr int u = WALK_IPL > 1 ? 1 : 0;          \
-      __VA_ARGS__                                      \
-    }                                                  \
-  } while (0)
-static_assert(WALK_IPL == 1 || WALK_IPL == 2, "WALK_IPL");
 
 // ------------------------------------------------------------ dictionary ----
 __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t k) {
@@ -590,12 +570,7 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
 // with T_BITS ballots; one LDS add per topic per 64 entries), then scattered
 // into the wave's ids slab grouped by topic, one piece per topic present
 // carrying the topic's running count as its offset inside the CSR row.
-#ifdef EGM_FLUSH_NOINLINE   // a call: fewer live registers in the walk loop, a call frame in scratch
-#define EGM_FLUSH_INLINE __noinline__
-#else
-#define EGM_FLUSH_INLINE __forceinline__
-#endif
-__device__ EGM_FLUSH_INLINE void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane,
+__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane,
                                             const MatchWork& w, Slab& sid, Slab& spc) {
   for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {
     const uint32_t i = i0 + lane;
@@ -820,19 +795,10 @@ __global__ EGM_WALK_LB void k_walk(DevTable tab, const uint32_t* __restrict__ of
   root.z = __builtin_amdgcn_readfirstlane(root.z);
   root.w = __builtin_amdgcn_readfirstlane(root.w);
   uint32_t created = 0;
-  unsigned long long iters = 0, popped = 0;
+  unsigned long long iters = 0, popped = 0, bounded = 0;
   Slab sid{0, 0}, spc{0, 0};
-  constexpr uint32_t POP = 64u * WALK_IPL;
 
-#ifdef EGM_XCD_MAP
-  // blocks are dealt round-robin to the 8 XCDs: give XCD x the contiguous
-  // x-th eighth of the chunks, so neighbouring topics share one L2
-  const uint32_t xcd = blockIdx.x & 7u, nslot = gridDim.x >> 3;
-  const uint32_t c_lo = (uint32_t)((uint64_t)nchunks * xcd / 8), c_hi = (uint32_t)((uint64_t)nchunks * (xcd + 1) / 8);
-  for (uint32_t c = c_lo + (blockIdx.x >> 3) * WALK_WAVES + wave; c < c_hi; c += nslot * WALK_WAVES) {
-#else
   for (uint32_t c = blockIdx.x * WALK_WAVES + wave; c < nchunks; c += nwaves) {
-#endif
     const uint32_t t0 = c * WALK_CHUNK;
     const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
 
@@ -934,8 +900,9 @@ __global__ EGM_WALK_LB void k_walk(DevTable tab, const uint32_t* __restrict__ of
     {                                                                                                  \
       const uint32_t room_ = (uint32_t)WALK_STACK - sp;                                                \
       const uint32_t lim_ = room_ > dmax ? room_ - dmax : (room_ ? 1u : 0u);                          \
-      const uint32_t take_ = min(min(64u, sp), lim_), bi_ = sp - take_;                                \
+      const uint32_t want_ = min(64u, sp), take_ = min(want_, lim_), bi_ = sp - take_;                 \
       if (take_ == 0 && sp) ovf = true;                                                                \
+      bounded += take_ < want_ ? 1u : 0u;                                                              \
       P.act = lane < take_;                                                                            \
       P.it = L.stack[min(bi_ + lane, (uint32_t)WALK_STACK - 1)]; /* unconditional: see issue() */     \
       sp = bi_;                                                                                        \
@@ -995,30 +962,6 @@ __global__ EGM_WALK_LB void k_walk(DevTable tab, const uint32_t* __restrict__ of
       wave_sync();                                                                                     \
     }
 
-#ifdef EGM_WALK_PIPE
-    // Software pipeline over two batches A and B: the reads of the next batch
-    // are issued before the current one is retired.  (Measured: LLVM copies
-    // the loop-carried load results and waits for them right after issue, so
-    // this buys nothing today; kept for the A/B harness.)
-    Pend pa, pb;
-    uint32_t ta = 0, tb = 0;
-    if (!ovf) {
-      WALK_REFILL();
-      WALK_POP(pa, ta);
-    }
-    while (!ovf) {
-      WALK_REFILL();
-      WALK_POP(pb, tb);
-      wave_sync();
-      if (ta) WALK_RETIRE(pa);
-      if (ovf || (!tb && sp == 0 && next >= end)) break;
-      WALK_REFILL();
-      WALK_POP(pa, ta);
-      wave_sync();
-      if (tb) WALK_RETIRE(pb);
-      if (ovf || (!ta && sp == 0 && next >= end)) break;
-    }
-#else
     while (!ovf) {
       WALK_REFILL();
       if (sp == 0) {
@@ -1031,7 +974,6 @@ __global__ EGM_WALK_LB void k_walk(DevTable tab, const uint32_t* __restrict__ of
       wave_sync();
       WALK_RETIRE(pa);
     }
-#endif
     }  // sub-chunks
 #undef WALK_REFILL
 #undef WALK_POP
@@ -1061,6 +1003,7 @@ __global__ EGM_WALK_LB void k_walk(DevTable tab, const uint32_t* __restrict__ of
     if (v) atomicAdd(&w.stats->visited, v);
     atomicAdd(&w.stats->iters, iters);
     atomicAdd(&w.stats->popped, popped);
+    if (bounded) atomicAdd(&w.stats->bounded, bounded);
   }
 }
 
@@ -1341,12 +1284,11 @@ int walk_grid_blocks(uint32_t n) {
   uint32_t blocks = (chunks + WALK_WAVES - 1) / WALK_WAVES;
   const uint32_t cap = 256 * 32 / WALK_WAVES;  // grid-stride beyond 32 waves per CU
   if (blocks > cap) blocks = cap;
-  blocks = (blocks + 7) & ~7u;                 // a multiple of the 8 XCDs (EGM_XCD_MAP)
+  blocks = (blocks + 7) & ~7u;                 // a multiple of the 8 XCDs
   return blocks ? (int)blocks : 1;
 }
 
 int walk_waves_per_block() { return WALK_WAVES; }
-int walk_items_per_lane() { return WALK_IPL; }
 
 size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 

@@ -192,11 +192,11 @@ class GpuMatcher:
                 "errors": e.value}
 
     def walk_counters(self) -> dict:
-        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint32()
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
         self._check(self.lib.egm_last_walk_counters(self.ctx, C.byref(a), C.byref(b), C.byref(c)),
                     "egm_last_walk_counters")
-        occ = b.value / max(1, a.value * 64 * c.value)
-        return {"iters": a.value, "popped": b.value, "items_per_lane": c.value, "lane_occupancy": occ}
+        occ = b.value / max(1, a.value * 64)
+        return {"iters": a.value, "popped": b.value, "bounded": c.value, "lane_occupancy": occ}
 
     def set_debug(self, flags: int):
         self._check(self.lib.egm_set_debug(self.ctx, flags), "egm_set_debug")

@@ -31,6 +31,8 @@ def _load():
         lib.ot_match.argtypes = [P, P, P, C.c_uint32, C.c_int, P, C.POINTER(C.POINTER(C.c_uint32))]
         lib.ot_match_count.restype = C.c_uint64
         lib.ot_match_count.argtypes = [P, P, P, C.c_uint32, C.c_int]
+        lib.ot_match_counts.restype = C.c_uint64
+        lib.ot_match_counts.argtypes = [P, P, P, C.c_uint32, C.c_int, P]
         lib.ot_n_keys.restype = C.c_uint64
         lib.ot_n_keys.argtypes = [P]
         lib.ot_free_ptr.argtypes = [P]
@@ -82,6 +84,14 @@ class OracleTrie:
     def match_count(self, blob, off, threads: int = 1) -> int:
         off = np.ascontiguousarray(off, dtype=np.uint32)
         return int(self.lib.ot_match_count(self.h, _p(blob), _p(off), len(off) - 1, threads))
+
+    def match_counts(self, blob, off, threads: int = 1) -> np.ndarray:
+        """Per-topic match counts (u32[n]), no ids."""
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        n = len(off) - 1
+        counts = np.zeros(n, dtype=np.uint32)
+        self.lib.ot_match_counts(self.h, _p(blob), _p(off), n, threads, _p(counts))
+        return counts
 
     def n_keys(self) -> int:
         return int(self.lib.ot_n_keys(self.h))

@@ -333,6 +333,34 @@ uint64_t ot_match_count(void* h, const uint8_t* blob, const uint32_t* off, uint3
   return s;
 }
 
+// Per-topic match counts for n topics (no ids): the whole-batch row totals a
+// GPU result is checked against at full config size.
+uint64_t ot_match_counts(void* h, const uint8_t* blob, const uint32_t* off, uint32_t n, int threads,
+                         uint32_t* counts) {
+  const Oracle* o = (const Oracle*)h;
+  if (threads < 1) threads = 1;
+  std::vector<uint64_t> tot(threads, 0);
+  std::vector<std::thread> th;
+  for (int k = 0; k < threads; ++k) {
+    th.emplace_back([&, k]() {
+      uint32_t a = (uint32_t)((uint64_t)n * k / threads), b = (uint32_t)((uint64_t)n * (k + 1) / threads);
+      uint64_t s = 0;
+      std::vector<uint32_t> tmp;
+      for (uint32_t i = a; i < b; ++i) {
+        tmp.clear();
+        match_one(o, (const char*)blob + off[i], off[i + 1] - off[i], tmp);
+        counts[i] = (uint32_t)tmp.size();
+        s += tmp.size();
+      }
+      tot[k] = s;
+    });
+  }
+  for (auto& t : th) t.join();
+  uint64_t s = 0;
+  for (auto v : tot) s += v;
+  return s;
+}
+
 uint64_t ot_n_keys(void* h) { return ((Oracle*)h)->trie.tab.size(); }
 void ot_free_ptr(void* p) { free(p); }
 

@@ -1,5 +1,7 @@
 import os
 import sys
+import threading
+import time
 
 import pytest
 
@@ -10,4 +12,28 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
-    config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "slow: long-running test (full-size configs)")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _heartbeat():
+    """Full-size GPU tests spend minutes in host-side generation and oracle
+    work inside ctypes calls; a line appended every 30 s to
+    gpurun_out/heartbeat.txt (when that directory exists, i.e. on a GPU job)
+    shows a watchdog the run is alive."""
+    d = os.path.join(ROOT, "gpurun_out")
+    if not os.path.isdir(d):
+        yield
+        return
+    stop = threading.Event()
+    t0 = time.time()
+
+    def beat():
+        while not stop.wait(30.0):
+            with open(os.path.join(d, "heartbeat.txt"), "a") as fh:
+                fh.write(f"pytest alive {time.time() - t0:.0f}s\n")
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    yield
+    stop.set()

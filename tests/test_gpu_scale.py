@@ -1,0 +1,196 @@
+"""GPU parity at the benchmarked sizes (C2, C4 and dense C3 were
+benchmarked but never checked).
+
+* C2 at full size — 10M wildcard filters x 10M topics, the bench's own
+  workload: every topic's row total against the C++ oracle (in four parts, so
+  no single test is silent for minutes), 200K sampled rows id-exact, and
+  determinism of the whole batch through a per-row order-independent checksum.
+* C4-shaped fan-out at 10M filters (20% wildcard, 1+Poisson(1) subscribers,
+  0.1% of filters with 2 000, 10% $share groups): the match rows against the
+  oracle, the delivery row pointers complete, sampled delivery rows
+  element-for-element in emqx_broker:dispatch/2 order
+  (apps/emqx/src/emqx_broker.erl:283-308).
+* C3 at 1M depth-16 filters ('+' p=.35, '#' p=.7): the walk must run in its
+  depth-first regime (pops cut by the stack-room bound, counted by the
+  kernel), sampled rows id-exact in both match modes and all row totals.
+
+The oracle is the pinned C++ restatement of emqx_trie compact mode
+(oracle/trie_oracle.cpp; apps/emqx/src/emqx_trie.erl:251-266).
+"""
+import numpy as np
+import pytest
+
+from emqx_amd import _lib as L
+from emqx_amd import synth
+from emqx_amd.engine import GpuMatcher
+from emqx_amd.hostinfo import usable_cpus
+from oracle.cpp import OracleTrie, canonical
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+THREADS = max(4, usable_cpus())
+
+
+def row_checksums(row, ids):
+    """Per-row order-independent checksum: sum of a 64-bit mix of each id."""
+    x = ids.astype(np.uint64)
+    x ^= x >> np.uint64(16)
+    x *= np.uint64(0x9E3779B97F4A7C15)
+    x ^= x >> np.uint64(29)
+    cnt = np.diff(row).astype(np.int64)
+    out = np.zeros(len(cnt), np.uint64)
+    nz = np.nonzero(cnt)[0]
+    if len(nz):
+        out[nz] = np.add.reduceat(x, row[:-1].astype(np.int64)[nz])
+    return out
+
+
+def sampled_rows(res_row, res_ids, idx):
+    r = np.zeros(len(idx) + 1, np.uint64)
+    r[1:] = np.cumsum(np.diff(res_row)[idx])
+    parts = [res_ids[int(res_row[i]):int(res_row[i + 1])] for i in idx]
+    ids = np.concatenate(parts) if parts else np.zeros(0, np.uint32)
+    return r, ids
+
+
+# ------------------------------------------------------------------ C2 -------
+@pytest.fixture(scope="module")
+def c2():
+    f, t = synth.config("c2")
+    gm = GpuMatcher(0, max_batch=t.n)
+    gm.build(f.blob, f.off)
+    res = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    assert res.n_error == 0
+    o = OracleTrie(True, L.EGM_MODE_ROUTES)
+    o.add(f.blob, f.off)
+    yield {"f": f, "t": t, "gm": gm, "res": res, "o": o}
+    gm.close()
+
+
+@pytest.mark.parametrize("part", range(4))
+def test_c2_full_row_totals(c2, part):
+    t, res, o = c2["t"], c2["res"], c2["o"]
+    lo, hi = t.n * part // 4, t.n * (part + 1) // 4
+    want = o.match_counts(t.blob, t.off[lo:hi + 1], threads=THREADS)   # absolute offsets into one blob
+    got = np.diff(res.row_ptr[lo:hi + 1]).astype(np.uint32)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, (len(bad), [(int(lo + i), int(got[i]), int(want[i])) for i in bad[:5]])
+
+
+def test_c2_full_sampled_rows_exact(c2):
+    t, res, o = c2["t"], c2["res"], c2["o"]
+    idx = np.sort(np.random.default_rng(2).choice(t.n, 200_000, replace=False))
+    sub = t.subset(idx)
+    row, ids = o.match(sub.blob, sub.off, threads=THREADS)
+    grow, gids = sampled_rows(res.row_ptr, res.ids, idx)
+    assert np.array_equal(grow, row)
+    assert np.array_equal(canonical(grow, gids), canonical(row, ids))
+    assert int(res.row_ptr[-1]) > 40 * t.n   # ~50 matches per C2 topic
+
+
+def test_c2_full_determinism(c2):
+    t, res, gm = c2["t"], c2["res"], c2["gm"]
+    again = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    assert np.array_equal(again.row_ptr, res.row_ptr)
+    assert np.array_equal(row_checksums(again.row_ptr, again.ids), row_checksums(res.row_ptr, res.ids))
+    st = gm.walk_counters()
+    assert st["popped"] > 0
+
+
+# ------------------------------------------------------------------ C4 -------
+def _expected_deliveries(mids, srow, subs):
+    mids = mids.astype(np.int64)
+    cnt = (srow[mids + 1] - srow[mids]).astype(np.int64)
+    fid = np.repeat(mids, cnt)
+    starts = np.repeat(srow[mids].astype(np.int64) - np.concatenate([[0], np.cumsum(cnt)[:-1]]), cnt)
+    sub = subs[starts + np.arange(int(cnt.sum()))]
+    return fid.astype(np.uint32), sub.astype(np.uint32)
+
+
+def test_c4_fanout_10m_filters():
+    import torch
+    f, t = synth.config("c4", n_filters=10_000_000, n_topics=1_000_000)
+    srow, subs = synth.subscribers(f.n, lam=1.0, p_big=0.001, n_big=2000, p_share=0.1,
+                                   seed=synth.SEED_BASE + synth.CONFIG_INDEX["c4"])
+    gm = GpuMatcher(0, max_batch=t.n)
+    try:
+        gm.build(f.blob, f.off)
+        gm.subs_build(srow, subs)
+        dev = torch.device("cuda:0")
+        s = torch.cuda.current_stream().cuda_stream
+        d_blob = torch.from_numpy(t.blob).to(dev)
+        d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+        n, cap = t.n, 64 * t.n
+        d_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
+        gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES, s,
+                        d_row.data_ptr(), d_ids.data_ptr(), cap)
+        torch.cuda.synchronize()
+        st = gm.last_stats()
+        assert st["overflow"] == 0 and st["errors"] == 0, st
+        mrow = d_row.cpu().numpy().view(np.uint64)
+        mids = d_ids[: int(mrow[-1])].cpu().numpy().view(np.uint32)
+        # match rows: all row totals and sampled id sets against the oracle
+        o = OracleTrie(True, L.EGM_MODE_ROUTES)
+        o.add(f.blob, f.off)
+        want_cnt = o.match_counts(t.blob, t.off, threads=THREADS)
+        assert np.array_equal(np.diff(mrow).astype(np.uint32), want_cnt)
+        idx = np.sort(np.random.default_rng(4).choice(n, 20_000, replace=False))
+        sub = t.subset(idx)
+        orow, oids = o.match(sub.blob, sub.off, threads=THREADS)
+        grow, gids = sampled_rows(mrow, mids, idx)
+        assert np.array_equal(grow, orow)
+        assert np.array_equal(canonical(grow, gids), canonical(orow, oids))
+        del o
+        # fan-out
+        cnt = (srow[mids.astype(np.int64) + 1] - srow[mids.astype(np.int64)]).astype(np.uint64)
+        dpos = np.zeros(len(mids) + 1, np.uint64)
+        np.cumsum(cnt, out=dpos[1:])
+        tot = int(dpos[-1])
+        assert tot > 100 * n   # the 2 000-subscriber filters dominate
+        d_drow = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        d_fid = torch.zeros(tot + 8, dtype=torch.int32, device=dev)
+        d_sub = torch.zeros(tot + 8, dtype=torch.int32, device=dev)
+        gm.fanout_device(d_row.data_ptr(), d_ids.data_ptr(), cap, n, s, d_drow.data_ptr(), d_fid.data_ptr(),
+                         d_sub.data_ptr(), tot + 8)
+        torch.cuda.synchronize()
+        drow = d_drow.cpu().numpy().view(np.uint64)
+        assert np.array_equal(drow, dpos[mrow.astype(np.int64)])   # every delivery row
+        for i in np.random.default_rng(5).choice(n, 3_000, replace=False):
+            a, b = int(mrow[i]), int(mrow[i + 1])
+            wf, ws = _expected_deliveries(mids[a:b], srow, subs)
+            lo, hi = int(drow[i]), int(drow[i + 1])
+            assert hi - lo == len(wf)
+            if hi > lo:
+                assert np.array_equal(d_fid[lo:hi].cpu().numpy().view(np.uint32), wf), i
+                assert np.array_equal(d_sub[lo:hi].cpu().numpy().view(np.uint32), ws), i
+        # shared groups appear as (filter, group) entries, never as members
+        grp = d_sub[: min(tot, 50_000_000)].cpu().numpy().view(np.uint32)
+        assert np.count_nonzero(grp & np.uint32(L.GROUP_BIT)) > 0
+    finally:
+        gm.close()
+
+
+# ------------------------------------------------------------------ C3 -------
+@pytest.mark.parametrize("mode", [L.EGM_MODE_TRIE, L.EGM_MODE_ROUTES])
+def test_c3_dense_dfs_regime(mode):
+    f, t = synth.config("c3", n_filters=1_000_000, n_topics=200_000)
+    gm = GpuMatcher(0, max_batch=t.n)
+    try:
+        gm.build(f.blob, f.off)
+        res = gm.match(t.blob, t.off, mode)
+        assert res.n_error == 0
+        wc = gm.walk_counters()
+        assert wc["bounded"] > 0, wc   # pops cut by the stack-room bound: the depth-first regime ran
+        o = OracleTrie(True, mode)
+        o.add(f.blob, f.off)
+        want = o.match_counts(t.blob, t.off, threads=THREADS)
+        assert np.array_equal(np.diff(res.row_ptr).astype(np.uint32), want)
+        idx = np.sort(np.random.default_rng(3).choice(t.n, 20_000, replace=False))
+        sub = t.subset(idx)
+        row, ids = o.match(sub.blob, sub.off, threads=THREADS)
+        grow, gids = sampled_rows(res.row_ptr, res.ids, idx)
+        assert np.array_equal(grow, row)
+        assert np.array_equal(canonical(grow, gids), canonical(row, ids))
+    finally:
+        gm.close()

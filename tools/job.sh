@@ -1,0 +1,59 @@
+#!/bin/bash
+# One parameterised GPU job for gpurun (replaces the per-lease run*.sh files).
+#
+#   gpurun --timeout 1200 -- 'bash tools/job.sh TAG step [step ...]'
+#
+# Steps (each under its own time limit, logs in gpurun_out/TAG_<step>.log):
+#   tests      pytest -m gpu, fast tests only (not the full-size ones)
+#   scale      pytest -m "gpu and slow": the full-size C1/C2/C3/C4 parity tests
+#   bench      bench.py C2 (driver command shape) + rocprofv3 --stats -> gpurun_out/TAG_prof
+#   bench_c1|bench_c3|bench_c4   the other configs under rocprofv3 --stats
+#   shard1     bench.py --mode shard at world 1 via torch.distributed.run
+#   pmc        FETCH_SIZE and WRITE_SIZE passes over the C2 bench (one counter per pass)
+#   sq         SQ wait/active counters + TCC hit/miss over the C2 bench
+#   host       host-visible path (egm_match_batch, pinned staging) bench
+#   smoke      __graft_entry__.smoke()
+# An ordinary failure (exit 1..5) moves on; a fault, abort or timeout ends the job.
+set -u
+TAG=$1; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+B="python $R/bench.py"
+
+run() {
+  local name=$1 secs=$2; shift 2
+  local log="gpurun_out/${TAG}_$name.log"
+  echo "[$(date +%T)] start $name"
+  timeout -k 10 "$secs" "$@" > "$log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc"
+  tail -n 4 "$log"
+  case $rc in
+    0|1|2|3|4|5) return 0 ;;
+    *) echo "FATAL: $name exited $rc — stopping"; exit $rc ;;
+  esac
+}
+
+for step in "$@"; do
+  case $step in
+    tests) run tests 900 python -u -m pytest tests -m "gpu and not slow" -x -v --timeout 300 --timeout-method thread ;;
+    scale) run scale 1100 python -u -m pytest tests -m "gpu and slow" -x -v --timeout 600 --timeout-method thread ;;
+    bench) run bench 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o run --output-format csv -- $B --steps 20 --warmup 5 ;;
+    bench_c1|bench_c3|bench_c4)
+      cfg=${step#bench_}
+      run "$step" 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$cfg" -o run --output-format csv -- $B --config "$cfg" --steps 10 --warmup 2 ;;
+    shard1) run shard1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --mode shard --steps 10 --warmup 2 --cpu-baseline off ;;
+    pmc)
+      run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off
+      run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc_write" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off ;;
+    sq)
+      run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU -d "$R/gpurun_out/${TAG}_pmc_sq" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off
+      run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off ;;
+    host) run host 600 python tools/bench_host.py ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[$(date +%T)] job $TAG done"

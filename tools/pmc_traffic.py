@@ -39,8 +39,12 @@ def main():
     a = ap.parse_args()
     f = per_dispatch(a.fetch_dir, "FETCH_SIZE")
     w = per_dispatch(a.write_dir, "WRITE_SIZE")
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_src_sha
     rec = {
         "kernel": "k_walk", "workload": a.workload, "filters": a.filters, "topics": a.topics,
+        "kernel_src_sha": kernel_src_sha(),
         "fetch_bytes_per_launch": statistics.median(f), "write_bytes_per_launch": statistics.median(w),
         "dispatches": [len(f), len(w)],
         "traffic_bytes_per_launch": statistics.median(f) + statistics.median(w),
