@@ -8,13 +8,15 @@ A *step* is one pass of the hot path — tokenise + NFA walk (+ heavy path) +
 CSR finalisation, i.e. emqx_router:match_routes/1's filter sets for a whole
 batch — over one batch of synthetic topics already resident in HBM.
 
-Layouts (emqx_amd/dist.py):
+Layouts (emqx_amd/dist.py), named in the line's config.workload:
   replicate (default)  every GPU holds the 10M-filter table and matches its own
                        10M-topic batch; no data-path collective -> "weak".
   shard                filters split over the GPUs, rank 0's batch broadcast,
-                       counts all-gathered, ids gathered over RCCL -> "strong".
+                       counts and ids gathered to rank 0 over RCCL and merged
+                       by the HIP merge kernel -> "strong" (BASELINE config C2
+                       as worded); runs its collectives at every world size.
 
-    python bench.py [--gpus N --steps K --warmup W] [--config c2] [--mode replicate]
+    python bench.py [--gpus N --steps K --warmup W] [--config c2] [--mode replicate|shard]
 
 Rank 0 prints ONE JSON line on stdout; progress goes to stderr.
 """
@@ -129,6 +131,31 @@ def _heartbeat(period: float = 30.0):
     threading.Thread(target=beat, daemon=True).start()
 
 
+LAYOUTS = {
+    "replicate": "replicated table: every GPU holds all filters and matches its own topic batch "
+                 "(no data-path collective)",
+    "shard": "filter-sharded: filters split over the GPUs by word_hash(filter) mod N, rank 0's topic batch "
+             "broadcast, per-topic counts and ids gathered to rank 0 and merged by the HIP merge kernel "
+             "(RCCL over xGMI; at N=1 the collectives are no-ops)",
+}
+
+
+def _init_dist(args, rank, world, dev):
+    """A process group whenever the layout exchanges data (shard mode runs its
+    collectives at every world size, world 1 included)."""
+    import torch.distributed as dist
+    if world > 1 or args.mode == "shard":
+        if "MASTER_ADDR" not in os.environ:   # plain `python bench.py --mode shard`: a world of one
+            import socket
+            so = socket.socket()
+            so.bind(("127.0.0.1", 0))
+            os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(so.getsockname()[1])
+            so.close()
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        return True
+    return False
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,14 +164,12 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--filters", type=int, default=None, help="override filter count")
     ap.add_argument("--topics", type=int, default=None, help="override topics per batch")
-    ap.add_argument("--mode", default="replicate", choices=["replicate", "shard"])
+    ap.add_argument("--mode", default="replicate", choices=sorted(LAYOUTS))
     ap.add_argument("--match", default="routes", choices=["routes", "trie"])
     ap.add_argument("--fanout", default="auto", choices=["auto", "on", "off"],
                     help="add emqx_broker:dispatch/2 subscriber fan-out to each step (auto: on for c4)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--x-presort", action="store_true",
-                    help="EXPERIMENT ONLY: sort the batch on the host before upload (not a valid bench line)")
     args = ap.parse_args()
     fanout = args.fanout == "on" or (args.fanout == "auto" and args.config == "c4")
     if fanout and args.mode == "shard":
@@ -168,8 +193,8 @@ def main():
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    have_pg = _init_dist(args, rank, world, dev)
+    shard = args.mode == "shard"
     mode = L.EGM_MODE_ROUTES if args.match == "routes" else L.EGM_MODE_TRIE
 
     c = synth.CONFIGS[args.config]
@@ -178,30 +203,26 @@ def main():
     nt = args.topics or c["n_topics"]
     t0 = time.time()
     f = synth.filters(nf, c["dmin"], c["dmax"], c["wc"], c["p_plus"], c["p_hash"], seed=seed)
-    tseed = seed + (7919 * rank if args.mode == "replicate" else 0)
+    tseed = seed + (0 if shard else 7919 * rank)   # shard: rank 0's batch is the one broadcast
     t = synth.topics(nt, f, c["dmin"], c["dmax"], seed=tseed)
     log(f"[rank {rank}] generated {f.n} filters, {t.n} topics in {time.time() - t0:.1f}s")
-    if args.x_presort:
-        tl = t.to_list()
-        order = np.array(sorted(range(len(tl)), key=tl.__getitem__), dtype=np.int64)
-        del tl
-        t = t.subset(order)
-        log(f"[rank {rank}] EXPERIMENT: batch pre-sorted on the host")
 
     gm = GpuMatcher(local, max_batch=nt)
     t0 = time.time()
-    if args.mode == "shard" and world > 1:
+    if shard:
         from emqx_amd.dist import shard_of
         from emqx_amd.engine import pack_strings
-        sh = shard_of(f, world)
-        idx = np.nonzero(sh == rank)[0]
+        idx = np.nonzero(shard_of(f, world) == rank)[0]
         fl = f.to_list()
         blob, off = pack_strings([fl[i] for i in idx])
+        del fl
         gm.build(blob, off, idx.astype(np.uint32))
+        del blob, off
     else:
         gm.build(f.blob, f.off)
     tstats = gm.stats()
     log(f"[rank {rank}] table built in {time.time() - t0:.1f}s: {tstats}")
+    sub_entries = 0
     if fanout:
         # filter id -> subscriber CSR (emqx_subscriber bag, shards flattened)
         t0 = time.time()
@@ -220,54 +241,75 @@ def main():
     nbytes = int(t.off[-1])
     d_blob = torch.from_numpy(t.blob).to(dev)
     d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
-    cap = max(4 * n, 1 << 20)
-    d_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
+    bufs = {"cap": max(4 * n, 1 << 20)}
+    bufs["row"] = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    bufs["ids"] = torch.zeros(bufs["cap"], dtype=torch.int32, device=dev)
 
     fcap = max(8 * n, 1 << 20) if fanout else 0
     d_drow = torch.zeros(n + 1, dtype=torch.int64, device=dev) if fanout else None
     d_fid = torch.zeros(fcap, dtype=torch.int32, device=dev) if fanout else None
     d_sub = torch.zeros(fcap, dtype=torch.int32, device=dev) if fanout else None
-
     fan_on = False   # enabled once the id buffer holds a whole match batch
 
     def run_local():
-        gm.match_device(d_blob.data_ptr(), nbytes, d_off.data_ptr(), n, mode, sp, d_row.data_ptr(),
-                        d_ids.data_ptr(), cap)
+        gm.match_device(d_blob.data_ptr(), nbytes, d_off.data_ptr(), n, mode, sp, bufs["row"].data_ptr(),
+                        bufs["ids"].data_ptr(), bufs["cap"])
         if fan_on:
-            gm.fanout_device(d_row.data_ptr(), d_ids.data_ptr(), cap, n, sp, d_drow.data_ptr(), d_fid.data_ptr(),
-                             d_sub.data_ptr(), fcap)
+            gm.fanout_device(bufs["row"].data_ptr(), bufs["ids"].data_ptr(), bufs["cap"], n, sp, d_drow.data_ptr(),
+                             d_fid.data_ptr(), d_sub.data_ptr(), fcap)
 
     exchange = None
-    if args.mode == "shard" and world > 1:
-        from emqx_amd.dist import ShardExchange
+    if shard:
+        from emqx_amd.dist import ShardExchange, gpu_merge
 
         def local_match(tb, to, nn):
-            gm.match_device(tb.data_ptr(), tb.numel(), to.data_ptr(), nn, mode, sp, d_row.data_ptr(),
-                            d_ids.data_ptr(), cap)
-            m = int(d_row[nn].item())
-            return d_row, d_ids[:m]
+            gm.match_device(tb.data_ptr(), tb.numel(), to.data_ptr(), nn, mode, sp, bufs["row"].data_ptr(),
+                            bufs["ids"].data_ptr(), bufs["cap"])
+            st = gm.last_stats()   # syncs: the id count is needed on the host for the gather
+            return bufs["row"], bufs["ids"], int(st["n_ids"]), bool(st["overflow"])
 
-        exchange = ShardExchange(rank, world, dev, local_match)
+        bufs["mcap"] = max(4 * n, 1 << 20) if rank == 0 else 0
+        bufs["mrow"] = torch.zeros(n + 1, dtype=torch.int64, device=dev) if rank == 0 else None
+        bufs["mids"] = torch.zeros(max(1, bufs["mcap"]), dtype=torch.int32, device=dev) if rank == 0 else None
+
+        def make_exchange():
+            mg = gpu_merge(gm, sp, bufs["mrow"], bufs["mids"]) if rank == 0 else None
+            return ShardExchange(rank, world, dev, local_match, mg)
+
+        exchange = make_exchange()
 
     def step():
         if exchange is None:
             run_local()
-        elif rank == 0:
-            exchange.step(d_blob, d_off)
         else:
-            exchange.step()
+            exchange.step(d_blob if rank == 0 else None, d_off if rank == 0 else None, sizes=(n, d_blob.numel()))
 
-    # size the id buffer (untimed), then warm up
+    # size the id buffers (untimed), then warm up
     for _ in range(4):
         step()
         torch.cuda.synchronize(dev)
         st = gm.last_stats()
+        if exchange is not None:
+            if not exchange.last_overflow:
+                tot = sum(exchange.last_totals)
+                if rank == 0 and tot > bufs["mcap"]:
+                    raise RuntimeError("merge buffer too small")   # gpu_merge refuses before writing
+                break
+            mine = exchange.last_totals[rank]
+            if mine > bufs["cap"]:
+                bufs["cap"] = int(mine * 1.25) + 1024
+                bufs["ids"] = torch.zeros(bufs["cap"], dtype=torch.int32, device=dev)
+            if rank == 0:
+                bufs["mcap"] = int(sum(exchange.last_totals) * 1.25) + 1024
+                bufs["mids"] = torch.zeros(bufs["mcap"], dtype=torch.int32, device=dev)
+            exchange = make_exchange()
+            log(f"[rank {rank}] grew id buffers: local {bufs['cap']}")
+            continue
         if not st["overflow"]:
             break
-        cap = int(st["n_ids"] * 1.25) + 1024
-        d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
-        log(f"[rank {rank}] grew id buffer to {cap}")
+        bufs["cap"] = int(st["n_ids"] * 1.25) + 1024
+        bufs["ids"] = torch.zeros(bufs["cap"], dtype=torch.int32, device=dev)
+        log(f"[rank {rank}] grew id buffer to {bufs['cap']}")
     if fanout:
         fan_on = True
         step()
@@ -284,9 +326,11 @@ def main():
     torch.cuda.synchronize(dev)
     st = gm.last_stats()
     assert st["overflow"] == 0 and st["errors"] == 0, st
+    if exchange is not None:
+        assert not exchange.last_overflow
 
     gm.set_timing(True)
-    if world > 1:
+    if have_pg:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -294,7 +338,7 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if have_pg:
         dist.barrier()
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -306,8 +350,9 @@ def main():
         assert deliveries <= fcap, (deliveries, fcap)
     wc = gm.walk_counters()
     gm.set_timing(False)
+    merged_ids = sum(exchange.last_totals) if exchange is not None else None
 
-    units_per_step = n * world if (args.mode == "replicate" or world == 1) else n
+    units_per_step = n if shard else n * world
     value = units_per_step * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -320,7 +365,7 @@ def main():
     achieved = walk_bytes / (walk_ms * 1e-3) / 1e9
     path_bytes = (nbytes + 4 * n) + 16 * sum_d + 32 * visited + 4 * (n_ids + n)
 
-    traffic = walk_traffic(args.config, f.n, n) if args.mode == "replicate" or world == 1 else None
+    traffic = walk_traffic(args.config, f.n, n) if (not shard and world == 1) else None
     if rank == 0:
         cpu = None
         if args.cpu_baseline == "auto" and world == 1 and f.n > 20_000_000:
@@ -332,21 +377,25 @@ def main():
         line = {
             "metric": METRIC, "value": value, "unit": "topics/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak" if (args.mode == "replicate" or world == 1) else "strong",
+            "scaling": "strong" if shard else "weak",
             "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": WORKLOADS[args.config], "filters": f.n, "topics_per_step": units_per_step,
-                       "topics_per_gpu": n, "match": "emqx_router:match_routes" if args.match == "routes"
-                       else "emqx_trie:match", "parallelism": f"{args.mode}{world}",
-                       "table": tstats},
+            "config": {"workload": f"{WORKLOADS[args.config]}; layout: {LAYOUTS[args.mode]}", "filters": f.n,
+                       "topics_per_step": units_per_step, "topics_per_gpu": n,
+                       "filters_on_rank0": tstats["filters"],
+                       "match": "emqx_router:match_routes" if args.match == "routes" else "emqx_trie:match",
+                       "parallelism": f"{args.mode}{world}", "table": tstats},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic[0]["traffic_bytes_per_launch"] if traffic else None,
                          "traffic_source": traffic[1] if traffic else None,
                          "kernel": "k_walk", "kernel_ms": walk_ms, "bytes_per_launch": walk_bytes,
+                         "kernel_src_sha": kernel_src_sha(),
                          "path_frac": path_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "stats": {"ids_per_step": n_ids, "visited_per_step": visited, "levels_per_step": sum_d,
+                      "merged_ids_per_step": merged_ids,
                       "deferred_chunks": st["deferred_chunks"], "walk_iters": wc["iters"],
-                      "walk_popped": wc["popped"], "walk_lane_occupancy": wc["lane_occupancy"]},
+                      "walk_popped": wc["popped"], "walk_bounded_pops": wc["bounded"],
+                      "walk_lane_occupancy": wc["lane_occupancy"]},
             "fanout": ({"deliveries_per_step": deliveries, "subscriber_entries": sub_entries,
                         "fanout_ms": tim["fanout_ms"] / max(1, tim["fanout_launches"]),
                         "deliveries_per_s": deliveries * world * args.steps / elapsed,
@@ -356,7 +405,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     gm.close()
-    if world > 1:
+    if have_pg:
         dist.destroy_process_group()
 
 

@@ -108,6 +108,9 @@ struct egm_ctx {
   bool last_pending = false;
   hipStream_t last_stream = nullptr;
 
+  // shard merge
+  DevBuf m_srow, m_tiles, m_tot;
+
   // fan-out
   DevBuf sub_row, sub_ids, f_dc, f_ds0, f_dpos, f_tiles, f_ovf, f_mrow, f_mids, f_drow, f_dfid, f_dsub;
   uint32_t n_fid_slots = 0;
@@ -886,6 +889,30 @@ int egm_fanout_batch(egm_ctx* c, const egm_result* m, egm_delivery** out) {
     return c->hip_fail(e, "D2H deliveries");
   }
   *out = d;
+  return EGM_OK;
+}
+
+// ------------------------------------------------------------ shard merge --
+int egm_shard_merge(egm_ctx* c, uint32_t n_shards, uint32_t n, const uint32_t* d_counts,
+                    const uint32_t* const* d_shard_ids, uint64_t total_ids, void* hip_stream, uint64_t* d_row,
+                    uint32_t* d_ids, uint64_t ids_cap) {
+  if (!c || n_shards == 0 || n_shards > MAX_SHARDS || !d_counts || !d_shard_ids || !d_row) return EGM_E_INVAL;
+  if (total_ids > ids_cap || (total_ids && !d_ids)) return EGM_E_OVERFLOW;
+  for (uint32_t g = 0; g < n_shards; ++g)
+    if (!d_shard_ids[g] && total_ids) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipError_t e;
+  const uint64_t nn = (uint64_t)n + 1;
+  if ((e = c->m_srow.ensure(nn * n_shards * 8)) != hipSuccess) return c->hip_fail(e, "merge srow");
+  if ((e = c->m_tiles.ensure((scan_tiles(n) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "merge tiles");
+  if ((e = c->m_tot.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "merge tot");
+  ShardIds src{};
+  for (uint32_t k = 0; k < n_shards; ++k) src.ids[k] = d_shard_ids[k];
+  e = launch_shard_merge(d_counts, n_shards, n, src, c->m_srow.as<uint64_t>(),
+                         c->m_tiles.as<uint64_t>(), c->m_tot.as<uint32_t>(), d_row, d_ids, ids_cap, s);
+  if (e != hipSuccess) return c->hip_fail(e, "launch_shard_merge");
   return EGM_OK;
 }
 

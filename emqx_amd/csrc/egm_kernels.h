@@ -107,6 +107,18 @@ hipError_t launch_fanout(const SubTable& st, const uint64_t* match_row, const ui
                          uint64_t* dpos, uint64_t* tile_sums, unsigned int* overflow, hipStream_t s,
                          hipEvent_t* ev);
 
+// Filter-shard merge: G shard CSRs of one topic batch ->
+// one CSR, per topic shard 0's ids first.  cnt is [G][n]; src[g].ids holds
+// shard g's ids back to back (device array of G pointers); srow is scratch
+// [G][n+1], tot scratch [n]; row [n+1] and out receive the merged CSR.
+constexpr uint32_t MAX_SHARDS = 16;   // GPUs of one node (kernel argument, no upload)
+struct ShardIds {
+  const uint32_t* ids[MAX_SHARDS];
+};
+hipError_t launch_shard_merge(const uint32_t* cnt, uint32_t G, uint32_t n, const ShardIds& src, uint64_t* srow,
+                              uint64_t* tile_sums, uint32_t* tot, uint64_t* row, uint32_t* out, uint64_t cap,
+                              hipStream_t s);
+
 // Scatter n records of rec_bytes (4, 16 or 32) from src[] to dst[idx[i]]:
 // the incremental epoch commit of egm_capi.cpp.
 hipError_t launch_patch(void* dst, uint32_t rec_bytes, const uint32_t* idx, const void* src, uint64_t n,

@@ -1438,6 +1438,86 @@ hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_
   return hipGetLastError();
 }
 
+// ----------------------------------------------------------- shard merge ----
+// Filter-sharded layout: rank 0 holds every shard's CSR for the
+// same topic batch as counts cnt[g][t] plus the shard's ids back to back.
+// The match set over F is the disjoint union over the shards, so the merged
+// row of topic t is shard 0's ids, then shard 1's, ... — no dedup.
+// k_merge_sum: tot[t] = sum_g cnt[g][t] (scanned into the output row_ptr).
+__global__ __launch_bounds__(256) void k_merge_sum(const uint32_t* __restrict__ cnt, uint32_t G, uint32_t n,
+                                                   uint32_t* __restrict__ tot) {
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    uint32_t s = 0;
+    for (uint32_t g = 0; g < G; ++g) s += cnt[(uint64_t)g * n + t];
+    tot[t] = s;
+  }
+}
+
+// One wave per window of 64 topics; for each shard the window's source ids
+// are one contiguous run [srow[g][t0], srow[g][t0 + 64]), laid out by a wave
+// scan and copied lane per id (coalesced reads; writes contiguous per topic).
+constexpr int MERGE_WAVES = 4;
+constexpr int MERGE_IPL = 4;
+__global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge_fill(const uint32_t* __restrict__ cnt,
+                                                                 const uint64_t* __restrict__ srow,
+                                                                 ShardIds src, uint32_t G,
+                                                                 uint32_t n, const uint64_t* __restrict__ row,
+                                                                 uint32_t* __restrict__ out, uint64_t cap) {
+  if (row[n] > cap) return;   // the caller's buffer is too small: write nothing
+  __shared__ uint32_t s_scan[MERGE_WAVES][64];
+  __shared__ uint64_t s_dst[MERGE_WAVES][64];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t nwin = (n + 63) / 64;
+  for (uint32_t w = blockIdx.x * MERGE_WAVES + wave; w < nwin; w += gridDim.x * MERGE_WAVES) {
+    const uint32_t t = w * 64 + lane;
+    const bool on = t < n;
+    uint64_t dst = on ? row[t] : 0;   // advances past each shard's ids of topic t
+    for (uint32_t g = 0; g < G; ++g) {
+      const uint32_t c = on ? cnt[(uint64_t)g * n + t] : 0u;
+      const uint64_t base = srow[(uint64_t)g * (n + 1) + w * 64];   // the window's first source id
+      uint32_t tot;
+      const uint32_t ex = wave_excl_scan(c, lane, &tot);
+      s_scan[wave][lane] = ex;
+      s_dst[wave][lane] = dst;
+      dst += c;
+      wave_sync();
+      const uint32_t* ids = src.ids[g] + base;
+      for (uint32_t q0 = lane; q0 < tot; q0 += 64 * MERGE_IPL) {
+        uint32_t v[MERGE_IPL];
+        uint64_t d[MERGE_IPL];
+#pragma unroll
+        for (int r = 0; r < MERGE_IPL; ++r) {
+          const uint32_t q = min(q0 + 64u * r, tot - 1);
+          uint32_t k = 0;
+#pragma unroll
+          for (uint32_t step = 32; step >= 1; step >>= 1)
+            if (s_scan[wave][k + step] <= q) k += step;
+          d[r] = s_dst[wave][k] + (q - s_scan[wave][k]);
+          v[r] = ids[q];
+        }
+#pragma unroll
+        for (int r = 0; r < MERGE_IPL; ++r)
+          if (q0 + 64u * r < tot) out[d[r]] = v[r];
+      }
+      wave_sync();
+    }
+  }
+}
+
+hipError_t launch_shard_merge(const uint32_t* cnt, uint32_t G, uint32_t n, const ShardIds& src, uint64_t* srow,
+                              uint64_t* tile_sums, uint32_t* tot, uint64_t* row, uint32_t* out, uint64_t cap,
+                              hipStream_t s) {
+  const uint32_t g1 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 8192));
+  for (uint32_t g = 0; g < G; ++g) scan_counts(cnt + (uint64_t)g * n, n, tile_sums, srow + (uint64_t)g * (n + 1), s);
+  hipLaunchKernelGGL(k_merge_sum, dim3(g1), dim3(256), 0, s, cnt, G, n, tot);
+  scan_counts(tot, n, tile_sums, row, s);
+  if (n) {
+    const uint32_t gf = (uint32_t)std::min<uint64_t>((n + 64 * MERGE_WAVES - 1) / (64 * MERGE_WAVES), 16384);
+    hipLaunchKernelGGL(k_merge_fill, dim3(gf), dim3(64 * MERGE_WAVES), 0, s, cnt, srow, src, G, n, row, out, cap);
+  }
+  return hipGetLastError();
+}
+
 // -------------------------------------------------------------- table patch --
 // Incremental epoch commit: the records a batch of route
 // adds/deletes changed (emqx_router.erl:114-125,164-170 -> emqx_trie:insert/

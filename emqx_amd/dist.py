@@ -22,7 +22,7 @@ the intra-node, GPU-native counterpart.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Callable, List, Sequence, Tuple
+from typing import Callable, List, Optional, Tuple
 
 import numpy as np
 
@@ -41,107 +41,115 @@ def shard_of(strings, n_shards: int) -> np.ndarray:
     return out
 
 
-def merge_shard_results(parts: Sequence[Tuple[np.ndarray, np.ndarray]]) -> Tuple[np.ndarray, np.ndarray]:
-    """Per topic, concatenate the shard rows in shard order (host, numpy)."""
-    rows = [np.asarray(r, dtype=np.uint64) for r, _ in parts]
-    n = len(rows[0]) - 1
-    cnts = np.stack([np.diff(r).astype(np.int64) for r in rows])          # [G, n]
-    tot = cnts.sum(axis=0)
-    row = np.zeros(n + 1, dtype=np.uint64)
-    np.cumsum(tot, out=row[1:])
-    before = np.cumsum(cnts, axis=0) - cnts                                 # ids of earlier shards per topic
-    ids = np.zeros(int(row[-1]), dtype=np.uint32)
-    for g, (r, gi) in enumerate(parts):
-        c = cnts[g]
-        if c.sum() == 0:
-            continue
-        tpos = np.repeat(np.arange(n, dtype=np.int64), c)
-        k = np.arange(len(gi), dtype=np.int64) - np.repeat(rows[g][:-1].astype(np.int64), c)
-        ids[row[:-1].astype(np.int64)[tpos] + before[g][tpos] + k] = gi
-    return row, ids
-
-
-def merge_shard_results_torch(counts, ids_list):
-    """Device merge on rank 0: counts [G, n] (int64), ids_list[g] (int32).
-
-    Returns (row int64 [n+1], ids int32) — the same layout as the single-GPU
-    CSR (shard g's ids of topic t follow those of shards < g).
-    """
-    import torch
-    G, n = counts.shape
-    dev = counts.device
-    tot = counts.sum(0)
-    row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(tot, 0, out=row[1:])
-    before = torch.cumsum(counts, 0) - counts
-    out = torch.empty(int(row[-1].item()), dtype=torch.int32, device=dev)
-    for g in range(G):
-        c = counts[g]
-        m = int(c.sum().item())
-        if m == 0:
-            continue
-        t = torch.repeat_interleave(torch.arange(n, device=dev), c)
-        srow = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-        torch.cumsum(c, 0, out=srow[1:])
-        k = torch.arange(m, device=dev) - srow[:-1][t]
-        out[row[:-1][t] + before[g][t] + k] = ids_list[g][:m]
-    return row, out
-
-
-LocalMatch = Callable[["object", "object", int], Tuple["object", "object"]]
+LocalMatch = Callable[["object", "object", int], Tuple["object", "object", int, bool]]
+Merge = Callable[["object", list, int, int], Tuple["object", "object"]]
 
 
 class ShardExchange:
     """Collective steps of the filter-sharded layout (torch.distributed).
 
-    ``local_match(blob, off, n) -> (row int64[n+1], ids int32[m])`` is this
-    rank's matcher (the GPU path in production; tests inject a CPU matcher to
-    exercise the collectives over gloo).
+    ``local_match(blob, off, n) -> (row int64[n+1], ids int32, total, overflow)``
+    is this rank's matcher on its filter shard (the GPU path in production,
+    ``total``/``overflow`` already known on the host); ``merge(counts, ids_list,
+    total, n) -> (row, ids)`` combines the gathered shard CSRs on rank 0 (the
+    HIP kernel behind ``egm_shard_merge``, see ``gpu_merge``).  The CPU tests
+    inject both to run the collectives over gloo.
+
+    One step:
+      1. broadcast the topic batch (blob, offsets) from rank 0      [RCCL]
+      2. every rank matches it against its shard
+      3. all-gather (total, overflow) per rank: 2 x int64          [RCCL]
+      4. gather per-topic counts and ids to rank 0, point to point [RCCL]
+      5. rank 0 merges: per topic, shard 0's ids, then shard 1's ...
+    A rank whose id buffer overflowed is reported to every rank in 3, and the
+    step returns ``None`` everywhere with the true totals (``last_totals``) so
+    the caller can grow its buffers — no rank ever sends a short buffer.
     """
 
-    def __init__(self, rank: int, world: int, device, local_match: LocalMatch, group=None):
+    def __init__(self, rank: int, world: int, device, local_match: LocalMatch, merge: Optional[Merge] = None,
+                 group=None):
+        if rank == 0 and merge is None:
+            raise ValueError("rank 0 needs a merge function (emqx_amd.dist.gpu_merge)")
         self.rank, self.world, self.device = rank, world, device
         self.local_match = local_match
+        self.merge = merge
         self.group = group
+        self.last_totals: List[int] = []
+        self.last_overflow = False
+        self._bufs = {}
 
-    def step(self, blob=None, off=None):
-        """Rank 0 passes (blob u8, off int32); returns merged (row, ids) on rank 0."""
+    def _buf(self, key, numel, dtype):
+        import torch
+        b = self._bufs.get(key)
+        if b is None or b.numel() < numel or b.dtype != dtype:
+            b = torch.empty(max(numel, 1), dtype=dtype, device=self.device)
+            self._bufs[key] = b
+        return b[:numel]
+
+    def step(self, blob=None, off=None, sizes: Optional[Tuple[int, int]] = None):
+        """Rank 0 passes (blob u8, off int32).  ``sizes`` = (n, blob bytes) when
+        every rank knows them already (skips a broadcast and a sync).
+        Returns (row int64[n+1], ids int32[total]) on rank 0, None elsewhere."""
         import torch
         import torch.distributed as dist
-        dev = self.device
-        meta = torch.zeros(2, dtype=torch.int64, device=dev)
-        if self.rank == 0:
-            meta[0] = off.numel() - 1
-            meta[1] = blob.numel()
-        dist.broadcast(meta, 0, group=self.group)                              # 1. sizes
-        n, nb = int(meta[0].item()), int(meta[1].item())
+        dev, G, g = self.device, self.world, self.group
+        if sizes is None:
+            meta = torch.zeros(2, dtype=torch.int64, device=dev)
+            if self.rank == 0:
+                meta[0] = off.numel() - 1
+                meta[1] = blob.numel()
+            dist.broadcast(meta, 0, group=g)                                    # sizes
+            sizes = (int(meta[0].item()), int(meta[1].item()))
+        n, nb = sizes
         if self.rank != 0:
-            blob = torch.empty(nb, dtype=torch.uint8, device=dev)
-            off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        dist.broadcast(blob, 0, group=self.group)                              # 2. topic batch
-        dist.broadcast(off, 0, group=self.group)
-        row, ids = self.local_match(blob, off, n)                              # 3. local shard
-        cnt = (row[1:] - row[:-1]).to(torch.int64)
-        allc = [torch.empty_like(cnt) for _ in range(self.world)]
-        dist.all_gather(allc, cnt, group=self.group)                           # 4. counts
-        totals = [int(c.sum().item()) for c in allc]
-        if self.rank == 0:                                                     # 5. gatherv ids
-            bufs = [ids[: totals[0]].to(torch.int32)]
-            ops = []
-            for g in range(1, self.world):
-                b = torch.empty(max(totals[g], 1), dtype=torch.int32, device=dev)
-                bufs.append(b)
-                if totals[g]:
-                    ops.append(dist.P2POp(dist.irecv, b[: totals[g]], g, group=self.group))
-            for w in (dist.batch_isend_irecv(ops) if ops else []):
+            blob = self._buf("blob", nb, torch.uint8)
+            off = self._buf("off", n + 1, torch.int32)
+        dist.broadcast(blob, 0, group=g)                                        # 1. topic batch
+        dist.broadcast(off, 0, group=g)
+        row, ids, total, ovf = self.local_match(blob, off, n)                   # 2. this shard
+        info = torch.tensor([total, 1 if ovf else 0], dtype=torch.int64, device=dev)
+        allinfo = [torch.empty_like(info) for _ in range(G)]
+        dist.all_gather(allinfo, info, group=g)                                 # 3. totals + overflow
+        allinfo = torch.stack(allinfo).cpu().tolist()
+        self.last_totals = [int(x[0]) for x in allinfo]
+        self.last_overflow = any(x[1] for x in allinfo)
+        if self.last_overflow:
+            return None
+        cnt = (row[1 : n + 1] - row[:n]).to(torch.int32)
+        if self.rank != 0:                                                      # 4. counts + ids -> rank 0
+            ops = [dist.P2POp(dist.isend, cnt.contiguous(), 0, group=g)]
+            if total:
+                ops.append(dist.P2POp(dist.isend, ids[:total].contiguous(), 0, group=g))
+            for w in dist.batch_isend_irecv(ops):
                 w.wait()
-            return merge_shard_results_torch(torch.stack(allc), bufs)
-        if totals[self.rank]:
-            w = dist.batch_isend_irecv([dist.P2POp(dist.isend, ids[: totals[self.rank]].to(torch.int32).contiguous(),
-                                                   0, group=self.group)])
-            for x in w:
-                x.wait()
-        return None
+            return None
+        counts = self._buf("counts", G * n, torch.int32)
+        counts[:n].copy_(cnt)
+        parts = [ids[:total]]
+        ops = []
+        for r in range(1, G):
+            ops.append(dist.P2POp(dist.irecv, counts[r * n:(r + 1) * n], r, group=g))
+            b = self._buf(("ids", r), self.last_totals[r], torch.int32)
+            parts.append(b)
+            if self.last_totals[r]:
+                ops.append(dist.P2POp(dist.irecv, b, r, group=g))
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+        return self.merge(counts, parts, sum(self.last_totals), n)              # 5. merge
+
+
+def gpu_merge(gm, stream: int, out_row, out_ids):
+    """The merge of ShardExchange on rank 0: egm_shard_merge (HIP kernel) into
+    caller-owned device buffers out_row int64[n+1] and out_ids int32[cap]."""
+
+    def merge(counts, parts, total, n):
+        if total > out_ids.numel():
+            raise ValueError(f"merged ids {total} exceed the output buffer {out_ids.numel()}")
+        gm.shard_merge(len(parts), n, counts.data_ptr(), [p.data_ptr() for p in parts], total, stream,
+                       out_row.data_ptr(), out_ids.data_ptr(), out_ids.numel())
+        return out_row[: n + 1], out_ids[:total]
+
+    return merge
 
 
 def topic_slice(n: int, rank: int, world: int) -> Tuple[int, int]:

@@ -242,6 +242,15 @@ class GpuMatcher:
                                                d_fid, d_sub, cap), "egm_fanout_device")
 
 
+    # -- multi-GPU filter shards --------------------------------------------------
+    def shard_merge(self, n_shards: int, n: int, d_counts: int, d_shard_ids: Sequence[int], total: int,
+                    stream: int, d_row: int, d_ids: int, ids_cap: int):
+        """egm_shard_merge: G gathered shard CSRs (device) -> one CSR (device)."""
+        arr = (C.c_void_p * n_shards)(*d_shard_ids)
+        self._check(self.lib.egm_shard_merge(self.ctx, n_shards, n, d_counts, arr, total, stream or None, d_row,
+                                             d_ids, ids_cap), "egm_shard_merge")
+
+
 class TableImage:
     """Host-only build of the HBM image (no device): for layout tests on CPU."""
 

@@ -167,6 +167,21 @@ int egm_fanout_device(egm_ctx* ctx, const uint64_t* d_match_row, const uint32_t*
                       uint64_t match_ids_len, uint32_t n_topics, void* hip_stream, uint64_t* d_deliv_row, uint32_t* d_fid,
                       uint32_t* d_sub, uint64_t deliv_cap);
 
+/* ---- multi-GPU filter sharding ----
+   Merge the match results of one topic batch against n_shards disjoint filter
+   shards (each matched on its own GPU, gathered here over RCCL) into one CSR:
+   per topic, shard 0's ids, then shard 1's, ...  The union is disjoint (a
+   filter lives in exactly one shard), so no dedup.  The reference has no
+   counterpart: it replicates the whole table to every node
+   (apps/emqx/src/emqx_trie.erl:53, apps/emqx/src/emqx_router.erl:71).
+   d_counts: device [n_shards][n] per-topic counts; d_shard_ids: host array of
+   n_shards (<= 16) device pointers (shard g's ids back to back, topic order);
+   total_ids: the sum of all counts (EGM_E_OVERFLOW if > ids_cap).
+   Asynchronous on hip_stream (NULL = the context's stream). */
+int egm_shard_merge(egm_ctx* ctx, uint32_t n_shards, uint32_t n_topics, const uint32_t* d_counts,
+                    const uint32_t* const* d_shard_ids, uint64_t total_ids, void* hip_stream, uint64_t* d_row_ptr,
+                    uint32_t* d_ids, uint64_t ids_cap);
+
 void egm_result_free(void* result);
 
 /* ---- retained messages: reverse match ----

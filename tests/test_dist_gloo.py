@@ -13,9 +13,10 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from emqx_amd import synth
-from emqx_amd.dist import merge_shard_results, merge_shard_results_torch, shard_of, topic_slice, ShardExchange
+from emqx_amd.dist import ShardExchange, shard_of, topic_slice
 from emqx_amd.engine import pack_strings
 from oracle.cpp import OracleTrie, canonical
+from tests.shard_ref import merge_shard_results
 
 
 def _free_port():
@@ -40,9 +41,17 @@ def _worker(rank, world, port, q):
 
     def local_match(tb, to, n):
         row, ids = o.match(tb.numpy(), to.numpy().view(np.uint32), threads=1)
+        return torch.from_numpy(row.astype(np.int64)), torch.from_numpy(ids.astype(np.int32)), len(ids), False
+
+    def merge(counts, parts, total, n):   # test-side numpy merge (the product merge is the HIP kernel)
+        G = len(parts)
+        cs = counts.numpy().reshape(G, n).astype(np.int64)
+        rows = [np.concatenate([[0], np.cumsum(c)]).astype(np.uint64) for c in cs]
+        row, ids = merge_shard_results([(rows[k], parts[k].numpy().view(np.uint32)) for k in range(G)])
+        assert int(row[-1]) == total
         return torch.from_numpy(row.astype(np.int64)), torch.from_numpy(ids.astype(np.int32))
 
-    ex = ShardExchange(rank, world, torch.device("cpu"), local_match)
+    ex = ShardExchange(rank, world, torch.device("cpu"), local_match, merge if rank == 0 else None)
     if rank == 0:
         out = ex.step(torch.from_numpy(t.blob.copy()), torch.from_numpy(t.off.view(np.int32).copy()))
         q.put((out[0].numpy(), out[1].numpy()))
@@ -69,22 +78,6 @@ def test_shard_exchange_world2():
     wrow, wids = o.match(t.blob, t.off)
     assert np.array_equal(row.astype(np.uint64), wrow)
     assert np.array_equal(canonical(wrow, ids.astype(np.uint32)), canonical(wrow, wids))
-
-
-def test_merge_numpy_equals_torch():
-    rng = np.random.default_rng(0)
-    n, G = 500, 3
-    parts = []
-    for g in range(G):
-        c = rng.integers(0, 4, n)
-        row = np.zeros(n + 1, np.uint64)
-        row[1:] = np.cumsum(c)
-        parts.append((row, rng.integers(0, 1 << 30, int(row[-1])).astype(np.uint32)))
-    r1, i1 = merge_shard_results(parts)
-    cnt = torch.stack([torch.from_numpy(np.diff(p[0]).astype(np.int64)) for p in parts])
-    r2, i2 = merge_shard_results_torch(cnt, [torch.from_numpy(p[1].astype(np.int32)) for p in parts])
-    assert np.array_equal(r1, r2.numpy().astype(np.uint64))
-    assert np.array_equal(i1, i2.numpy().astype(np.uint32))
 
 
 def test_topic_slices_cover():

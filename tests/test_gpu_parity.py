@@ -366,7 +366,7 @@ def test_logical_shards_union(gm):
         m.close()
     gm.build(f.blob, f.off)
     whole = gm.match(t.blob, t.off, L.EGM_MODE_TRIE)
-    from emqx_amd.dist import merge_shard_results
+    from tests.shard_ref import merge_shard_results
     row, ids = merge_shard_results([(p.row_ptr, p.ids) for p in parts])
     assert np.array_equal(row, whole.row_ptr)
     assert np.array_equal(canonical(row, ids), canonical(whole.row_ptr, whole.ids))

@@ -1,0 +1,153 @@
+"""Filter-sharded layout on the GPU: the HIP merge kernel
+(egm_shard_merge) against the numpy reference merge, G logical shards on one
+MI355X merged on the device against the whole table, and ShardExchange over
+RCCL ("nccl") at world size 1 — the bench's shard step end to end."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from emqx_amd import _lib as L
+from emqx_amd import synth
+from emqx_amd.dist import ShardExchange, gpu_merge, shard_of
+from emqx_amd.engine import GpuMatcher, pack_strings
+from oracle.cpp import canonical
+from tests.shard_ref import merge_shard_results
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gm():
+    m = GpuMatcher(0)
+    yield m
+    m.close()
+
+
+def test_shard_merge_kernel_vs_numpy(gm):
+    import torch
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(7)
+    for G, n in ((1, 1), (3, 5_001), (8, 70_000), (16, 640)):
+        parts = []
+        for g in range(G):
+            c = rng.integers(0, 6, n) * (rng.random(n) < 0.7)
+            c[rng.random(n) < 0.001] = 3000          # a few long rows (several copy rounds per window)
+            row = np.zeros(n + 1, np.uint64)
+            row[1:] = np.cumsum(c)
+            parts.append((row, rng.integers(0, 1 << 31, int(row[-1]), dtype=np.uint32)))
+        want_row, want_ids = merge_shard_results(parts)
+        counts = torch.from_numpy(np.concatenate([np.diff(p[0]).astype(np.int32) for p in parts])).to(dev)
+        dids = [torch.from_numpy(p[1].view(np.int32)).to(dev) for p in parts]
+        total = int(want_row[-1])
+        out_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        out_ids = torch.zeros(total + 16, dtype=torch.int32, device=dev)
+        s = torch.cuda.current_stream().cuda_stream
+        gm.shard_merge(G, n, counts.data_ptr(), [d.data_ptr() for d in dids], total, s, out_row.data_ptr(),
+                       out_ids.data_ptr(), out_ids.numel())
+        torch.cuda.synchronize()
+        assert np.array_equal(out_row.cpu().numpy().view(np.uint64), want_row), (G, n)
+        assert np.array_equal(out_ids[:total].cpu().numpy().view(np.uint32), want_ids), (G, n)
+    with pytest.raises(L.EgmError):   # too small an output buffer is refused, nothing written
+        gm.shard_merge(1, 1, counts.data_ptr(), [dids[0].data_ptr()], 100, 0, out_row.data_ptr(),
+                       out_ids.data_ptr(), 10)
+
+
+def test_logical_shards_merged_on_device(gm):
+    """G filter shards on one GPU (each its own context and table), the same
+    batch matched by each, merged by the HIP kernel == the whole table."""
+    import torch
+    dev = torch.device("cuda:0")
+    f, t = synth.config("c0", n_topics=40_000)
+    fl = f.to_list()
+    G = 4
+    sh = shard_of(f, G)
+    d_blob = torch.from_numpy(t.blob).to(dev)
+    d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+    n = t.n
+    s = torch.cuda.current_stream().cuda_stream
+    mats, rows, idss = [], [], []
+    for g in range(G):
+        idx = np.nonzero(sh == g)[0]
+        m = GpuMatcher(0)
+        m.build(*pack_strings([fl[i] for i in idx]), idx.astype(np.uint32))
+        r = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        ids = torch.zeros(20 * n, dtype=torch.int32, device=dev)
+        m.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES, s,
+                       r.data_ptr(), ids.data_ptr(), ids.numel())
+        torch.cuda.synchronize()
+        assert m.last_stats()["overflow"] == 0
+        mats.append(m)
+        rows.append(r)
+        idss.append(ids)
+    counts = torch.cat([(r[1:] - r[:-1]).to(torch.int32) for r in rows])
+    total = int(sum(int(r[-1].item()) for r in rows))
+    out_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    out_ids = torch.zeros(total + 1, dtype=torch.int32, device=dev)
+    gm.shard_merge(G, n, counts.data_ptr(), [x.data_ptr() for x in idss], total, s, out_row.data_ptr(),
+                   out_ids.data_ptr(), out_ids.numel())
+    torch.cuda.synchronize()
+    for m in mats:
+        m.close()
+    gm.build(f.blob, f.off)
+    whole = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    row = out_row.cpu().numpy().view(np.uint64)
+    ids = out_ids[:total].cpu().numpy().view(np.uint32)
+    assert np.array_equal(row, whole.row_ptr)
+    assert np.array_equal(canonical(row, ids), canonical(whole.row_ptr, whole.ids))
+
+
+def _free_port():
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    p = so.getsockname()[1]
+    so.close()
+    return p
+
+
+def test_shard_exchange_rccl_world1(gm):
+    """ShardExchange over RCCL at world size 1 with the GPU matcher on the
+    shard-built table and the HIP merge: the bench's --mode shard step."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda:0")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        f, t = synth.config("c0", n_topics=50_000)
+        sh = shard_of(f, 1)
+        idx = np.nonzero(sh == 0)[0]
+        fl = f.to_list()
+        gm.build(*pack_strings([fl[i] for i in idx]), idx.astype(np.uint32))
+        n = t.n
+        s = torch.cuda.current_stream().cuda_stream
+        d_blob = torch.from_numpy(t.blob).to(dev)
+        d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+        d_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        d_ids = torch.zeros(4 * n, dtype=torch.int32, device=dev)
+
+        def local_match(tb, to, nn):
+            gm.match_device(tb.data_ptr(), tb.numel(), to.data_ptr(), nn, L.EGM_MODE_ROUTES, s,
+                            d_row.data_ptr(), d_ids.data_ptr(), d_ids.numel())
+            st = gm.last_stats()
+            return d_row, d_ids, int(st["n_ids"]), bool(st["overflow"])
+
+        m_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        m_ids = torch.zeros(40 * n, dtype=torch.int32, device=dev)
+        ex = ShardExchange(0, 1, dev, local_match, gpu_merge(gm, s, m_row, m_ids))
+        out = ex.step(d_blob, d_off)
+        if out is None:   # first step sized the id buffer
+            d_ids = torch.zeros(ex.last_totals[0] + 1024, dtype=torch.int32, device=dev)
+            out = ex.step(d_blob, d_off, sizes=(n, d_blob.numel()))
+        assert out is not None
+        torch.cuda.synchronize()
+        row = out[0].cpu().numpy().view(np.uint64)
+        ids = out[1].cpu().numpy().view(np.uint32)
+        gm.build(f.blob, f.off)
+        whole = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+        assert np.array_equal(row, whole.row_ptr)
+        assert np.array_equal(canonical(row, ids), canonical(whole.row_ptr, whole.ids))
+    finally:
+        dist.destroy_process_group()
