@@ -99,10 +99,11 @@ struct egm_ctx {
   std::string err;
 
   // per-batch workspace
-  DevBuf wid, lv, tfl, cnt, ids_tmp, pieces, deferred, tile_sums, stats;
+  DevBuf wid, lv, tfl, cnt, head, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats, work_desc;
   uint64_t pieces_cap = 0, ids_tmp_cap = 0;
   DevBuf in_blob, in_off, out_row, out_ids;
-  uint32_t heavy_waves = 256;
+  uint32_t heavy_waves = 64;     // waves of the heavy kernel (rare path; each owns an HBM stack)
+  uint32_t heavy_cap = 0;        // stack items per heavy wave
   uint32_t debug = 0;
   MatchStats last{};
   bool last_pending = false;
@@ -401,50 +402,59 @@ static int commit_locked(egm_ctx* c, uint64_t* epoch) {
   return EGM_OK;
 }
 
-static int ensure_work(egm_ctx* c, uint32_t n, uint64_t blob_bytes, uint64_t ids_cap) {
+// max_levels: an upper bound on the levels of any topic of the batch (the
+// heavy kernel's stack must hold the deepest one's DFS, egm_kernels.hip).
+static int ensure_work(egm_ctx* c, uint32_t n, uint64_t blob_bytes, uint64_t ids_cap, uint64_t max_levels) {
   hipError_t e;
   const uint64_t nn = (uint64_t)n + 1;
   if ((e = c->wid.ensure((blob_bytes + nn) * 4)) != hipSuccess) return c->hip_fail(e, "wid");
   if ((e = c->lv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "lv");
   if ((e = c->tfl.ensure(nn)) != hipSuccess) return c->hip_fail(e, "tfl");
   if ((e = c->cnt.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "cnt");
-  // chunk-ordered ids and their pieces, plus the slack of per-wave slabs
+  if ((e = c->head.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "head");
+  // ids in flush order and their pieces, plus the slack of per-wave slabs
   const uint64_t tcap = ids_tmp_capacity(ids_cap, n);
   if (tcap >= 0xFFFFFFF0ull) return c->fail(EGM_E_INVAL, "batch too large: > 4G matched ids (split it)");
   if ((e = c->ids_tmp.ensure(tcap * 4)) != hipSuccess) return c->hip_fail(e, "ids_tmp");
   c->ids_tmp_cap = c->ids_tmp.cap / 4;
   if ((e = c->pieces.ensure(pieces_capacity(ids_cap, n) * 16)) != hipSuccess) return c->hip_fail(e, "pieces");
-  c->pieces_cap = c->pieces.cap / 16;
+  c->pieces_cap = std::min<uint64_t>(c->pieces.cap / 16, 0xFFFFFFF0ull);
   if ((e = c->deferred.ensure((n / WALK_CHUNK + 2) * 4)) != hipSuccess) return c->hip_fail(e, "deferred");
+  const uint32_t hcap = heavy_stack_items(max_levels);
+  if ((e = c->heavy_stack.ensure((uint64_t)c->heavy_waves * hcap * 16)) != hipSuccess)
+    return c->hip_fail(e, "heavy stack");
+  c->heavy_cap = (uint32_t)std::min<uint64_t>(c->heavy_stack.cap / 16 / c->heavy_waves, 0xFFFFFFFFull);
   if ((e = c->tile_sums.ensure((scan_tiles(n) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "tile_sums");
   if ((e = c->stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "stats");
+  if ((e = c->work_desc.ensure(sizeof(MatchWork))) != hipSuccess) return c->hip_fail(e, "work descriptor");
   return EGM_OK;
 }
 
-static MatchWork work_view(egm_ctx* c, uint64_t ids_cap) {
+static MatchWork work_view(egm_ctx* c) {
   MatchWork w{};
   w.wid = c->wid.as<uint32_t>();
   w.lv = c->lv.as<uint32_t>();
   w.tfl = c->tfl.as<uint8_t>();
   w.cnt = c->cnt.as<uint32_t>();
+  w.head = c->head.as<uint32_t>();
   w.ids_tmp = c->ids_tmp.as<uint32_t>();
   w.ids_cap = c->ids_tmp_cap;   // ids_tmp entries (the output capacity is MatchOut's)
-  (void)ids_cap;
   w.pieces = c->pieces.as<uint4>();
   w.pieces_cap = c->pieces_cap;
   w.deferred = c->deferred.as<uint32_t>();
-  w.heavy_stack = nullptr;
+  w.heavy_stack = c->heavy_stack.as<uint4>();
   w.heavy_waves = c->heavy_waves;
-  w.heavy_stack_cap = 0;
+  w.heavy_cap = c->heavy_cap;
   w.tile_sums = c->tile_sums.as<uint64_t>();
   w.stats = c->stats.as<MatchStats>();
+  w.self = c->work_desc.as<MatchWork>();
   w.debug = c->debug;
   return w;
 }
 
 static int run_match(egm_ctx* c, const Epoch& ep, const uint8_t* d_blob, const uint32_t* d_off, uint32_t n,
                      int mode, hipStream_t s, uint64_t* d_row, uint32_t* d_ids, uint64_t ids_cap) {
-  MatchWork w = work_view(c, ids_cap);
+  MatchWork w = work_view(c);
   MatchOut o{d_row, d_ids, ids_cap};
   hipEvent_t evp[2] = {nullptr, nullptr};
   if (c->timing) {
@@ -505,7 +515,8 @@ int egm_open(const egm_config* cfg, egm_ctx** out) {
     delete c;
     return EGM_E_DEVICE;
   }
-  if (cfg && cfg->max_batch) ensure_work(c, cfg->max_batch, (uint64_t)cfg->max_batch * 64, (uint64_t)cfg->max_batch * 4);
+  if (cfg && cfg->max_batch)
+    ensure_work(c, cfg->max_batch, (uint64_t)cfg->max_batch * 64, (uint64_t)cfg->max_batch * 4, 1024);
   *out = c;
   return EGM_OK;
 }
@@ -610,7 +621,9 @@ int egm_match_device(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, con
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
-  int r = ensure_work(c, n, blob_bytes, ids_cap);
+  // a topic has at most (its bytes + 1) levels, and a legal one at most 65 536
+  // (emqx_topic.erl:45, 99-100): bound the device batch's depth by its blob
+  int r = ensure_work(c, n, blob_bytes, ids_cap, std::min<uint64_t>(blob_bytes, 65535) + 1);
   if (r) return r;
   std::shared_ptr<Epoch> ep = c->cur;
   r = run_match(c, *ep, d_blob, d_off, n, mode, s, d_row, d_ids, ids_cap);
@@ -698,7 +711,9 @@ int egm_match_batch(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32
   const uint32_t base0 = n ? off[0] : 0;
   const uint64_t bytes = n ? (uint64_t)off[n] - base0 : 0;
   std::vector<uint32_t> loff(n + 1);
+  uint64_t maxlen = 0;
   for (uint32_t i = 0; i <= n; ++i) loff[i] = n ? off[i] - base0 : 0;
+  for (uint32_t i = 0; i < n; ++i) maxlen = std::max<uint64_t>(maxlen, loff[i + 1] - loff[i]);
   hipError_t e;
   if ((e = c->in_blob.ensure(bytes + 16)) != hipSuccess) return c->hip_fail(e, "in_blob");
   if ((e = c->in_off.ensure(((uint64_t)n + 1) * 4)) != hipSuccess) return c->hip_fail(e, "in_off");
@@ -710,7 +725,7 @@ int egm_match_batch(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32
   std::shared_ptr<Epoch> ep = c->cur;
   uint64_t cap = std::max<uint64_t>((uint64_t)n * 4 + 1024, c->out_ids.cap / 4);
   for (int attempt = 0; attempt < 3; ++attempt) {
-    int r = ensure_work(c, n, bytes, cap);
+    int r = ensure_work(c, n, bytes, cap, maxlen + 1);
     if (r) return r;
     if ((e = c->out_row.ensure(((uint64_t)n + 1) * 8)) != hipSuccess) return c->hip_fail(e, "out_row");
     if ((e = c->out_ids.ensure((cap + 1) * 4)) != hipSuccess) return c->hip_fail(e, "out_ids");

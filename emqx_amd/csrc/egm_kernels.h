@@ -21,24 +21,24 @@ struct DevTable {                 // one epoch of the filter graph in HBM
 
 struct MatchStats {               // device-side counters, zeroed per batch
   unsigned long long cursor;      // ids_tmp entries reserved (slabs, incl. slack)
-  unsigned long long visited;     // NFA states expanded (light + heavy)
+  unsigned long long visited;     // NFA states created (light + heavy)
   unsigned long long pieces;      // pieces reserved (slabs, incl. slack)
   unsigned long long total_ids;   // matched ids in the batch (= row_ptr[n])
   unsigned int n_deferred;        // chunks handed to the heavy kernel
   unsigned int heavy_next;        // heavy work counter
   unsigned int overflow;          // bit 0: ids_tmp/pieces full, bit 1: output ids full
-  unsigned int errors;            // topics the heavy kernel could not finish
+  unsigned int errors;            // topics the heavy kernel could not walk (never for legal topics)
   unsigned long long iters;       // walk iterations (instrumentation)
   unsigned long long popped;      // items popped by the walk (lane occupancy = popped / (iters * 64))
   unsigned long long bounded;     // walk iterations whose pop was cut by the stack-room bound (DFS regime)
+  unsigned int next_chunk;        // chunk counter of the persistent walk waves
+  unsigned int pad;
 };
 
 // A piece is one flush's run of a topic's ids in ids_tmp:
-// {topic, count | HEAVY_PIECE, ids_tmp offset, offset inside the topic's row}.
-// CSR rows are assembled from pieces without atomics; light-walk pieces of a
-// topic later re-run by k_heavy are ignored; count 0 marks an unused slot.
-constexpr uint32_t HEAVY_PIECE = 0x80000000u;
-
+// {count, ids_tmp offset, offset inside the topic's row, the topic's previous
+// piece or NONE}.  head[t] is the topic's last piece, so CSR rows are
+// assembled by following the chains, without atomics.
 // Each wave reserves its output space in slabs (one device-scope atomic per
 // slab): a single shared counter bumped per flush serialises across the 8
 // XCDs at the memory side.
@@ -50,16 +50,18 @@ struct MatchWork {                // per-batch device workspace
   uint32_t* lv;                   // [n] levels
   uint8_t* tfl;                   // [n] TF_* flags
   uint32_t* cnt;                  // [n] number of ids of topic t
-  uint32_t* ids_tmp;              // [ids_cap] chunk-ordered ids
+  uint32_t* head;                 // [n] last piece of topic t (NONE: no ids)
+  uint32_t* ids_tmp;              // [ids_cap] ids in flush order
   uint64_t ids_cap;
   uint4* pieces;                  // [pieces_cap]
   uint64_t pieces_cap;
   uint32_t* deferred;             // [n / CHUNK + 1] chunk ids for the heavy kernel
-  uint2* heavy_stack;             // [heavy_waves * heavy_stack_cap]
+  uint4* heavy_stack;             // [heavy_waves * heavy_cap] work stacks of the heavy waves
   uint32_t heavy_waves;
-  uint32_t heavy_stack_cap;
+  uint32_t heavy_cap;             // items per heavy wave (>= deepest possible topic + 192)
   uint64_t* tile_sums;            // scan scratch
   MatchStats* stats;
+  MatchWork* self;                // device copy of this descriptor (written by k_setup)
   uint32_t debug;                 // DEBUG_* bits
 };
 
@@ -77,16 +79,17 @@ struct MatchOut {                 // CSR result (device)
 #endif
 constexpr int WALK_CHUNK = EGM_WALK_CHUNK;
 int walk_grid_blocks(uint32_t n_topics);
-int walk_waves_per_block();
 size_t scan_tiles(uint32_t n);
+// items of HBM stack per heavy wave for topics of up to max_levels levels
+uint32_t heavy_stack_items(uint64_t max_levels);
 // ids_tmp / pieces capacity a batch needs beyond its matched ids: slab tails
 inline uint64_t ids_tmp_capacity(uint64_t ids, uint32_t n) {
-  return ids + ids / 4 + (uint64_t)(walk_grid_blocks(n) * walk_waves_per_block() + 256) * SLAB_IDS;
+  return ids + ids / 4 + (uint64_t)(walk_grid_blocks(n) + 256) * SLAB_IDS;
 }
 inline uint64_t pieces_capacity(uint64_t ids, uint32_t n) {
   uint64_t p = 2ull * n + 4096;
   if (ids / 2 > p) p = ids / 2;
-  return p + (uint64_t)(walk_grid_blocks(n) * walk_waves_per_block() + 256) * SLAB_PIECES;
+  return p + (uint64_t)(walk_grid_blocks(n) + 256) * SLAB_PIECES;
 }
 
 // Timing hooks: when ev != nullptr, ev[0]/ev[1] bracket the walk kernel.

@@ -7,15 +7,13 @@
 //   emqx_router:match_routes/1    apps/emqx/src/emqx_router.erl:129-141  -> mode EGM_MODE_ROUTES
 //   emqx_broker:dispatch/2        apps/emqx/src/emqx_broker.erl:283-324  -> k_fanout_*
 //
-// The walk is an NFA frontier expansion over the word-level trie (egm_common.h).
-// One wavefront owns a chunk of WALK_CHUNK topics; its work items
-// (node, level, topic, flags) live in an LDS stack.  Each iteration pops up to
-// 64 items (one per lane), issues the two independent loads an item needs (the
-// node record and the literal-edge bucket), and compacts the produced matches
-// and children back into LDS with __ballot / mbcnt.  At the end of a chunk the
-// staged matches are counting-sorted by topic and written with a single
-// atomic reservation.  Chunks whose frontier or match count overflows LDS are
-// re-run by k_heavy (one topic per wave, 64 KB LDS stack, count-then-fill).
+// The walk is an NFA frontier expansion over the word-level trie (egm_common.h):
+// persistent wavefronts, each walking two chunks of 64 topics at once from an
+// LDS work stack (pop up to 64 items, issue their reads together, compact
+// children and emits back with __ballot / mbcnt), staging emits per topic
+// and flushing them as pieces chained per topic; k_compact assembles the CSR
+// rows from the chains.  Chunks with a topic deeper than the LDS stack allows
+// are walked by k_heavy (one topic per wave, stack in HBM).
 //
 // This is pointer chasing over hashed edges — HBM / latency bound; no MFMA.
 #include <hip/hip_runtime.h>
@@ -29,23 +27,6 @@ namespace egm {
 constexpr int MODE_TRIE = 0;
 constexpr int MODE_ROUTES = 1;
 
-#ifndef EGM_WALK_WAVES
-#define EGM_WALK_WAVES 1   // waves per block (LDS granularity)
-#endif
-constexpr int WALK_WAVES = EGM_WALK_WAVES;
-#ifndef EGM_WALK_STACK
-#define EGM_WALK_STACK 320   // items per wave (16 B each)
-#endif
-constexpr int WALK_STACK = EGM_WALK_STACK;
-#ifndef EGM_WALK_STAGE
-#define EGM_WALK_STAGE 320   // staged matches per flush (7 B each)
-#endif
-constexpr int WALK_STAGE = EGM_WALK_STAGE;
-#ifndef EGM_WALK_WORDS
-#define EGM_WALK_WORDS 448   // staged topic word ids per wave chunk
-#endif
-constexpr int WALK_WORDS = EGM_WALK_WORDS;
-constexpr int HEAVY_STACK = 6144;    // items (120 KB LDS) per heavy wave
 constexpr int TOK_BLOCK = 256;
 #ifndef EGM_TOK_LDS
 #define EGM_TOK_LDS 16384   // staged topic bytes per tokenise block (A/B at C2: 24 KB -> 1.09 ms, 16 KB -> 0.92, 12 KB -> 1.12)
@@ -57,7 +38,6 @@ constexpr int TOK_LDS = EGM_TOK_LDS;
 constexpr int TOK_WORDS = EGM_TOK_WORDS;
 constexpr int SCAN_TILE = 2048;      // counts per scan tile (256 threads x 8)
 
-static_assert(WALK_CHUNK <= 256 && WALK_CHUNK % 64 == 0, "chunk");
 
 // ------------------------------------------------------------ primitives ----
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
@@ -84,23 +64,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
   return x - v;
 }
 
-// item = (node, meta); meta = level[0:17) | t[17:25) | flags[25:29) | wc<<29 | exact<<30
-__device__ __forceinline__ uint32_t mk_meta(uint32_t level, uint32_t t, uint32_t fl, uint32_t wc,
-                                            uint32_t ex) {
-  return level | (t << 17) | ((fl & F_BASIC) << 25) | (wc << 29) | (ex << 30);
-}
-
 __device__ __forceinline__ uint4 ld16(const void* p) { return *(const uint4*)p; }
-
-// An empty piece {NONE, 0, 0, 0}, materialised where it is stored: as a plain
-// constant LLVM hoists it out of every loop and pins four VGPRs for the whole
-// walk kernel.
-__device__ __forceinline__ uint4 empty_piece() {
-  uint32_t x = NONE, z = 0;
-  asm volatile("" : "+v"(x), "+v"(z));
-  return make_uint4(x, z, z, z);
-}
-
 
 // ------------------------------------------------------------ dictionary ----
 __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t k) {
@@ -396,144 +360,81 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
   }
 }
 
-// ------------------------------------------------------------ NFA expand ----
-// A work item is (node, meta) plus the node's record, so expanding it needs
-// no read of its own node: meta = level[0:17) | t[17:25) | flags[25:29) |
-// wc<<29 | exact<<30, rec = {plus_child, hash_fid, term_fid}.
-struct Item {
-  uint4 a;        // {node, meta, plus_child, hash_fid}
-  uint32_t term;  // term_fid
-};
-
-__device__ __forceinline__ Item mk_item(uint32_t node, uint32_t meta, uint32_t plus, uint32_t hash,
-                                        uint32_t term) {
-  Item it;
-  it.a = make_uint4(node, meta, plus, hash);
-  it.term = term;
-  return it;
-}
-
-// Literal transition: one 128 B bucket of four 32 B slots; a slot holds the
-// edge key and a copy of the child's record.  Slots fill in probe order, so
-// the first empty slot ends the search.
-__device__ __forceinline__ bool edge_probe(const DevTable& tab, uint32_t node, uint32_t w, uint4* lo_out,
-                                           uint4* hi_out) {
-  uint32_t b = edge_bucket(node, w, tab.edge_mask);
-  for (;;) {
-    const EdgeSlot* bp = tab.edges + (size_t)b * EDGE_BUCKET;
-#pragma unroll
-    for (int k = 0; k < EDGE_BUCKET; ++k) {
-      const uint4 lo = ld16(bp + k);
-      const uint4 hi = ld16((const uint8_t*)(bp + k) + 16);
-      if (lo.x == node && lo.y == w) {
-        *lo_out = lo;
-        *hi_out = hi;
-        return true;
-      }
-      if (lo.x == NONE) return false;
-    }
-    b = (b + 1) & tab.edge_mask;
-  }
-}
-
-struct Expand {
-  uint32_t e0, e1;     // emitted filter ids ('P/#', 'P')
-  Item c0, c1;         // children (literal, '+')
-  bool h0, h1, hc0, hc1;
-};
-
-// Expand one (node, level) state of topic t.  This is match_compact/4's body
-// (emqx_trie.erl:251-266) without the string keys:
-//   'match_#'(Prefix)          -> e0 = hash_fid of node (every level <= D)
-//   recurse Prefix/Word        -> c0 = literal child
-//   recurse Prefix/'+'         -> c1 = plus child
-//   lookup_topic(Topic, IsWc)  -> e1 = term_fid at level == D if the path
-//                                 took a '+' (TRIE mode) / always (ROUTES)
-//   do_match/1's '$' rule      -> at the root of a '$' topic no '#'/'+'
-//                                 (:208-215), and the single-word probe
-//                                 lookup_topic(Prefix) -> e1 at D == 1
-// `exact` items walk a wildcard topic as a literal key (ROUTES mode only:
-// lookup_routes(Topic) of emqx_router.erl:129-134).
-// Each child costs one random read: its bucket line or its node record.
-__device__ __forceinline__ void expand(const DevTable& tab, int mode, const Item& it, uint32_t D,
-                                       uint32_t tflags, uint32_t w, Expand& x) {
-  const uint32_t node = it.a.x, meta = it.a.y;
-  const uint32_t level = meta & 0x1FFFFu;
-  const uint32_t tm = meta & (0xFFu << 17);
-  const uint32_t fl = (meta >> 25) & 0xFu, wc = (meta >> 29) & 1u, ex = (meta >> 30) & 1u;
-  const bool atend = level == D;
-  const uint32_t nmeta = (level + 1) | tm | (ex << 30);
-  x.h0 = x.h1 = x.hc0 = x.hc1 = false;
-  x.e0 = it.a.w;
-  x.e1 = it.term;
-  if (!ex) {
-    const bool rootd = (level == 0) && (tflags & TF_DOLLAR);
-    x.h0 = (fl & F_HASH) && !rootd;
-    x.h1 = atend && (fl & F_TERM) && (mode == MODE_ROUTES || wc || (D == 1 && (tflags & TF_DOLLAR)));
-    const bool want_plus = !atend && (fl & F_PLUS) && !rootd;
-    const bool want_lit = !atend && (fl & F_LIT) && w < WID_MAX;
-    uint4 prec = make_uint4(NONE, NONE, NONE, 0), lo, hi;
-    if (want_plus) prec = ld16(tab.nodes + it.a.z);
-    const bool found = want_lit && edge_probe(tab, node, w, &lo, &hi);
-    x.hc0 = found;
-    if (found) x.c0 = mk_item(lo.z, nmeta | ((lo.w & F_BASIC) << 25) | (wc << 29), hi.x, hi.y, hi.z);
-    x.hc1 = want_plus;
-    x.c1 = mk_item(it.a.z, nmeta | ((prec.w & F_BASIC) << 25) | (1u << 29), prec.x, prec.y, prec.z);
-  } else {
-    x.h1 = atend && (fl & F_TERM);
-    if (atend) return;
-    uint32_t child = NONE;
-    if (w == WID_PLUS) child = it.a.z;
-    else if (w == WID_HASH) child = tab.hash_child[node];
-    uint4 lo, hi;
-    if (child != NONE) {
-      const uint4 r = ld16(tab.nodes + child);
-      x.c0 = mk_item(child, nmeta | ((r.w & F_BASIC) << 25), r.x, r.y, r.z);
-      x.hc0 = true;
-    } else if (w < WID_MAX && edge_probe(tab, node, w, &lo, &hi)) {
-      x.c0 = mk_item(lo.z, nmeta | ((lo.w & F_BASIC) << 25), hi.x, hi.y, hi.z);
-      x.hc0 = true;
-    }
-  }
-}
-
-__device__ __forceinline__ Item root_item(const uint4& r, uint32_t t, bool exact) {
-  return mk_item(0, mk_meta(0, t, r.w, 0, exact ? 1u : 0u), r.x, r.y, r.z);
-}
-
-// ------------------------------------------------------------------ walk ----
-// A work item is 16 B (one ds_read_b128): {node, meta, plus_child, word}
-//   meta = level[0:17) | t[17:24) | flags[24:28) | wc << 28
+// -------------------------------------------------------------- NFA walk ----
+// One wavefront walks two chunks of WALK_CHUNK topics at once (128 topic
+// slots): topics are admitted into the LDS work stack as it drains, and when
+// one chunk has been admitted and its last item retired, its counts are
+// written and the next chunk (taken from a global counter) fills its slots —
+// the stack never drains between chunks, so the lanes stay busy.
+//
+// A work item is 16 B {node, meta, plus_child, word}:
+//   meta = level[0:17) | slot[17:24) | transitions to take[24:28) | took '+' << 28
 //   word = the topic's word id at `level`
 // A state is finished when it is created, from the record that created it
-// (the literal edge slot carries its child's record, the '+' child's record
-// is one 16 B read): its 'match_#' emit and, at the topic's last level, its
+// (the literal edge slot carries its child's record, the '+' child's record is
+// one 16 B read): its 'match_#' emit and, at the topic's last level, its
 // lookup_topic emit are staged at once, and only a state that still has a
-// literal or '+' transition to take is pushed.  So every popped item is at a
-// level < D and costs exactly the reads of its own transitions, issued
-// together for all the items a wave pops.
+// literal or '+' transition to take is pushed.  So a popped item costs exactly
+// the reads of its own transitions — a bucket line and a 16-B record — plus
+// the topic's next word (an L2-resident 4-B read), all issued together.
+//
+// This is match_compact/4's body (apps/emqx/src/emqx_trie.erl:251-266)
+// without string keys:
+//   'match_#'(Prefix)          -> the '#' fid of every state created
+//   recurse Prefix/Word        -> literal child: bucket probe keyed (node, word)
+//   recurse Prefix/'+'         -> '+' child: its record
+//   lookup_topic(Topic, IsWc)  -> term fid at level == D if the path took a
+//                                 '+' (TRIE mode) / always (ROUTES)
+//   do_match/1's '$' rule      -> a '$' topic's root takes no '#'/'+'
+//                                 (:208-215), and the single-word probe
+//                                 lookup_topic(Prefix) -> term fid at D == 1
 constexpr uint32_t ML_BITS = 17;
 constexpr uint32_t MT_SHIFT = 17;
 constexpr uint32_t MF_SHIFT = 24;
 constexpr uint32_t MW_SHIFT = 28;
 constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
-constexpr uint32_t T_BITS = WALK_CHUNK <= 64 ? 6 : 7;
-static_assert(WALK_CHUNK == 64, "one topic per lane in the chunk prologue");
+
+#ifndef EGM_WALK_STACK
+#define EGM_WALK_STACK 240   // items (16 B) per wave
+#endif
+#ifndef EGM_WALK_STAGE
+#define EGM_WALK_STAGE 256   // staged emits per flush (6 B each; >= 4 emits x 64 lanes)
+#endif
+constexpr uint32_t WALK_STACK = EGM_WALK_STACK;
+constexpr uint32_t WALK_STAGE = EGM_WALK_STAGE;
+constexpr uint32_t SLOTS = 2 * WALK_CHUNK;           // two chunks in flight per wave
+// The pop bound below keeps room >= dmax after every iteration and a refill
+// fills the stack to at most 64 items, so the stack cannot overflow while
+// 64 + dmax <= WALK_STACK.  Chunks with a deeper topic go to k_heavy.
+constexpr uint32_t LIGHT_DMAX = WALK_STACK - 64;
+static_assert(WALK_CHUNK == 64, "lane j loads topic j of a chunk");
+static_assert(WALK_STAGE >= 256 && WALK_STAGE <= 256, "stage: 4 emits x 64 lanes per step; u8 ranks and starts");
+static_assert(LIGHT_DMAX >= 16, "stack too small");
 
 struct alignas(16) WaveLds {
   uint4 stack[WALK_STACK];
   uint32_t stage_fid[WALK_STAGE];
-  uint16_t stage_rank[WALK_STAGE];
-  uint8_t stage_t[WALK_STAGE];
-  uint32_t words[WALK_WORDS];
-  uint32_t tinfo[WALK_CHUNK];   // D | tflags << 24
-  uint32_t tbase[WALK_CHUNK];   // word base: LDS index (staged) or wid index
-  uint32_t cnt[WALK_CHUNK];     // ids per topic, whole chunk
-  uint32_t fcnt[WALK_CHUNK];    // ids per topic in the current stage
+  uint8_t stage_t[WALK_STAGE];     // slot of the emit
+  uint8_t stage_rank[WALK_STAGE];  // rank within its slot in this flush
+  uint32_t tinfo[SLOTS];           // D | tflags << 24
+  uint32_t tbase[SLOTS];           // wid index of the topic's word 0
+  uint32_t w0[SLOTS];              // the topic's word 0
+  uint32_t cnt[SLOTS];             // ids flushed so far
+  uint32_t last[SLOTS];            // the topic's last piece (NONE: none)
+  uint16_t fcnt[SLOTS];            // ids in the current stage / start inside the flush
 };
 
-__device__ __forceinline__ uint4 mk_piece(uint32_t t, uint32_t count, uint32_t src, uint32_t row_off) {
-  return make_uint4(t, count, src, row_off);
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// The workspace pointers live in device memory (k_setup) and are re-read at
+// each rare use (chunk take, retire, flush) through a pointer the compiler
+// cannot see through: hoisted out of the loop they would pin ~30 SGPRs and
+// push the walk's wave-uniform state into VGPRs.
+typedef const __attribute__((address_space(4))) MatchWork ConstWork;   // scalar (s_load) view
+__device__ __forceinline__ ConstWork* fresh(const MatchWork* p) {
+  uint64_t v = (uint64_t)p;
+  asm volatile("" : "+s"(v));
+  return (ConstWork*)v;
 }
 
 // Per-wave output slab (uniform across the wave).
@@ -543,14 +444,9 @@ struct Slab {
 
 // Take `need` entries from the wave's slab, reserving a new slab of at least
 // `grain` entries (one device-scope atomic) when the current one is short.
-// The unused tail of an abandoned pieces slab is marked empty (count 0).
 __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, uint32_t grain,
-                                                        unsigned long long* counter, uint32_t lane,
-                                                        uint4* tail_fill, unsigned long long tail_cap) {
+                                                        unsigned long long* counter, uint32_t lane) {
   if (s.cur + need > s.end) {
-    if (tail_fill)
-      for (unsigned long long i = s.cur + lane; i < s.end && i < tail_cap; i += 64)
-        tail_fill[i] = empty_piece();
     const unsigned long long sz = need > grain ? need : grain;
     unsigned long long b = 0;
     if (lane == 0) b = atomicAdd(counter, sz);
@@ -565,69 +461,78 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
   return r;
 }
 
-// Write the stage out.  Entries are ranked within their topic by a
-// conflict-free multi-split (lanes holding the same topic find each other
-// with T_BITS ballots; one LDS add per topic per 64 entries), then scattered
-// into the wave's ids slab grouped by topic, one piece per topic present
-// carrying the topic's running count as its offset inside the CSR row.
-__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane,
-                                            const MatchWork& w, Slab& sid, Slab& spc) {
+// Write the stage out.  Entries are ranked within their slot by a
+// conflict-free multi-split (lanes holding the same slot find each other with
+// 7 ballots; the leader of each group updates the slot's count), then
+// scattered into the wave's ids slab grouped by slot.  One piece per slot
+// present: {count, ids_tmp offset, offset inside the topic's CSR row, the
+// topic's previous piece} — a topic's pieces form a chain from head[t], so
+// the compaction gathers each topic's ids without scanning all pieces.
+__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t lane, const MatchWork* wk,
+                                            Slab& sid, Slab& spc) {
+  ConstWork& w = *fresh(wk);
+#pragma unroll 1
   for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {
     const uint32_t i = i0 + lane;
     const bool act = i < nstage;
     const uint32_t tt = act ? L.stage_t[i] : 0u;
     uint64_t m = __ballot(act);
 #pragma unroll
-    for (uint32_t b = 0; b < T_BITS; ++b) {
+    for (uint32_t b = 0; b < 7; ++b) {
       const bool bit = (tt >> b) & 1u;
       const uint64_t bb = __ballot(bit);
       m &= bit ? bb : ~bb;
     }
     const uint32_t leader = act ? (uint32_t)__builtin_ctzll(m) : lane;
     uint32_t old = 0;
-    if (act && lane == leader) old = atomicAdd(&L.fcnt[tt], popc(m));
+    if (act && lane == leader) {   // one leader per slot: a plain read-modify-write
+      old = L.fcnt[tt];
+      L.fcnt[tt] = (uint16_t)(old + popc(m));
+    }
     old = __shfl(old, (int)leader, 64);
-    if (act) L.stage_rank[i] = (uint16_t)(old + mbcnt(m));
+    if (act) L.stage_rank[i] = (uint8_t)(old + mbcnt(m));
   }
   wave_sync();
-  constexpr int PER = WALK_CHUNK / 64;
-  uint32_t fl[PER];
+  uint32_t fl[2];
   uint32_t s = 0, np = 0;
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    fl[k] = L.fcnt[lane * PER + k];   // consecutive topics per lane
+  for (int k = 0; k < 2; ++k) {
+    fl[k] = L.fcnt[lane * 2 + k];   // consecutive slots per lane
     s += fl[k];
     np += fl[k] ? 1u : 0u;
   }
   uint32_t tot, ptot;
   uint32_t ex = wave_excl_scan(s, lane, &tot);
   uint32_t pex = wave_excl_scan(np, lane, &ptot);
-  const unsigned long long base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
-  const unsigned long long pbase =
-      slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
+  const unsigned long long base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane);
+  const unsigned long long pbase = slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane);
   const bool ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
   if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const uint32_t j = lane * PER + k;
-    if (fl[k] && ok) w.pieces[pbase + pex++] = mk_piece(t0 + j, fl[k], (uint32_t)(base + ex), L.cnt[j]);
-    L.fcnt[j] = ex;   // the topic's start inside this flush
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t j = lane * 2 + k;
+    if (fl[k] && ok) {
+      const uint32_t p = (uint32_t)(pbase + pex++);
+      w.pieces[p] = make_uint4(fl[k], (uint32_t)(base + ex), L.cnt[j], L.last[j]);
+      L.last[j] = p;
+    }
+    L.fcnt[j] = (uint16_t)ex;   // the slot's start inside this flush
     L.cnt[j] += fl[k];
     ex += fl[k];
   }
   wave_sync();
   if (ok) {
-    for (uint32_t i = lane; i < nstage; i += 64)
-      w.ids_tmp[base + L.fcnt[L.stage_t[i]] + L.stage_rank[i]] = L.stage_fid[i];
+    uint32_t* dst = w.ids_tmp + base;
+#pragma unroll 1
+    for (uint32_t i = lane; i < nstage; i += 64) dst[L.fcnt[L.stage_t[i]] + L.stage_rank[i]] = L.stage_fid[i];
   }
   wave_sync();
 #pragma unroll
-  for (int k = 0; k < PER; ++k) L.fcnt[lane * PER + k] = 0;
+  for (int k = 0; k < 2; ++k) L.fcnt[lane * 2 + k] = 0;
   wave_sync();
 }
 
-// Slot search continued at slot k0 of bucket b (rare: both first slots hold
-// other keys).
+// Slot search from slot k0 of bucket b on (rare: both first slots hold other keys).
 __device__ __forceinline__ bool edge_probe_from(const DevTable& tab, uint32_t b, int k0, uint32_t node, uint32_t w,
                                                 uint4* lo_out, uint4* hi_out) {
   for (;;) {
@@ -650,30 +555,17 @@ __device__ __forceinline__ bool edge_probe_from(const DevTable& tab, uint32_t b,
 // One popped item between issuing its reads and consuming them.
 struct Pend {
   uint4 it;                 // the item
-  uint32_t ti, nw;          // its topic's info, the word at level + 1
-  bool act, lit, plus;
+  uint32_t D, nw;           // its topic's depth, the word at level + 1
+  bool act, lit, plus, d1;  // d1: a one-word '$' topic (do_match/1's lookup_topic probe)
   uint4 prec, l0, h0, l1, h1;
 };
 
-// Up to four emits and two pushes per popped item.
-struct Out {
-  uint32_t f0, f1, f2, f3;  // literal child: '#', terminal; '+' child: '#', terminal
-  bool e0, e1, e2, e3;
-  uint4 c0, c1;             // children to push
-  bool p0, p1;
-  uint32_t created;         // states created (instrumentation: SURVEY §8d V_t)
-};
-
-__device__ __forceinline__ uint32_t word_at(const WaveLds& L, uint32_t tt, uint32_t level) {
-  return L.words[min(L.tbase[tt] + level, (uint32_t)WALK_WORDS - 1)];
-}
-
 // Branch-free on purpose: every lane issues its loads unconditionally (an
-// idle lane reads node 0 / bucket 0, lines every wave keeps hot).  A load
-// inside an `if` makes LLVM merge its result at the end of the block, and
-// the copy it inserts there waits for the load — the second item's reads
-// would then only be issued after the first item's had returned.
-__device__ __forceinline__ void issue(const DevTable& tab, const WaveLds& L, Pend& p) {
+// idle lane reads node 0 / bucket 0 / word 0, lines every wave keeps hot).  A
+// load inside an `if` makes LLVM merge its result at the end of the block,
+// and the copy it inserts there waits for the load.
+__device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* __restrict__ wid, uint32_t tbase,
+                                      Pend& p) {
   const uint32_t meta = p.it.y;
   const uint32_t fl = (meta >> MF_SHIFT) & 0xFu;
   p.plus = p.act && (fl & F_PLUS);
@@ -685,83 +577,85 @@ __device__ __forceinline__ void issue(const DevTable& tab, const WaveLds& L, Pen
   p.h0 = ld16(bp + 16);
   p.l1 = ld16(bp + 32);
   p.h1 = ld16(bp + 48);
-  // LDS reads overlapping the global ones: the topic's info and the next
-  // level's word (clamped; used only if level + 1 < D)
-  const uint32_t tt = (meta >> MT_SHIFT) & 0x7Fu, level = meta & LEVEL_MAX;
-  p.ti = L.tinfo[tt];
-  p.nw = word_at(L, tt, level + 1);
+  // the next level's word (clamped; used only if level + 1 < D)
+  const uint32_t level = meta & LEVEL_MAX;
+  p.nw = wid[p.act ? tbase + min(level + 1, p.D - 1) : 0u];
 }
 
-__device__ __forceinline__ void finish(const DevTable& tab, int mode, Pend& p, Out& o) {
-  o.e0 = o.e1 = o.e2 = o.e3 = o.p0 = o.p1 = false;
-  o.created = 0;
-  if (!p.act) return;
+// Children and emits of one popped item.
+struct Out {
+  uint32_t f0, f1, f2, f3;  // literal child: '#', terminal; '+' child: '#', terminal
+  bool e0, e1, e2, e3;
+  uint4 c0, c1;             // children to push
+  bool p0, p1;
+  uint32_t created;         // states created (SURVEY §8d V_t)
+};
+
+// Straight-line on purpose: every field is computed unconditionally and
+// selected by the lane's flags (conditionally assigned fields became phis
+// whose copies cost a score of VGPRs).
+__device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend& p, Out& o) {
   const uint32_t meta = p.it.y;
-  const uint32_t level = meta & LEVEL_MAX, tt = (meta >> MT_SHIFT) & 0x7Fu;
+  const uint32_t level = meta & LEVEL_MAX;
   const uint32_t wc = (meta >> MW_SHIFT) & 1u;
-  const uint32_t D = p.ti & 0xFFFFFFu, tf = p.ti >> 24;
-  const uint32_t nl = level + 1;
-  const bool leaf = nl == D;
+  const uint32_t D = p.D;
+  const bool leaf = level + 1 == D;
   const uint32_t nw = p.nw;
-  const uint32_t base_meta = nl | (tt << MT_SHIFT);
+  const uint32_t base_meta = (level + 1) | (meta & (0x7Fu << MT_SHIFT));
   // the literal probe of a child is only worth a read if its signature has
   // the next word's bit (egm_common.h)
   const uint32_t nsig = nw < WID_MAX ? sig_bit(nw) : 0u;
-  if (p.lit) {
-    // pick the matching slot's fields with masks, not a select of the two
-    // loaded slots: LLVM folds the latter into a phi of addresses into the
-    // per-item array and then keeps that array in scratch
-    const uint32_t node = p.it.x;
-    const bool m0 = p.l0.x == node && p.l0.y == p.it.w;
-    const bool z0 = p.l0.x == NONE;
-    const bool m1 = !m0 && !z0 && p.l1.x == node && p.l1.y == p.it.w;
-    const bool z1 = p.l1.x == NONE;
-    const uint32_t s1 = m1 ? 0xFFFFFFFFu : 0u;
-    uint32_t cz = (p.l0.z & ~s1) | (p.l1.z & s1), cw = (p.l0.w & ~s1) | (p.l1.w & s1);
-    uint32_t hx = (p.h0.x & ~s1) | (p.h1.x & s1), hy = (p.h0.y & ~s1) | (p.h1.y & s1);
-    uint32_t hz = (p.h0.z & ~s1) | (p.h1.z & s1);
-    bool found = m0 || m1;
-    if (!m0 && !z0 && !m1 && !z1) {   // both first slots hold other keys: keep probing
-      uint4 lo, hi;
-      found = edge_probe_from(tab, edge_bucket(node, p.it.w, tab.edge_mask), 2, node, p.it.w, &lo, &hi);
-      cz = lo.z;
-      cw = lo.w;
-      hx = hi.x;
-      hy = hi.y;
-      hz = hi.z;
-    }
-    if (found) {
-      o.created += 1;
-      o.e0 = (cw & F_HASH) != 0;
-      o.f0 = hy;
-      o.e1 = leaf && (cw & F_TERM) && (mode == MODE_ROUTES || wc || (D == 1 && (tf & TF_DOLLAR)));
-      o.f1 = hz;
-      const uint32_t go = (cw & F_PLUS) | ((cw & nsig) ? (cw & F_LIT) : 0u);
-      o.p0 = !leaf && go;
-      o.c0 = make_uint4(cz, base_meta | (go << MF_SHIFT) | (wc << MW_SHIFT), hx, nw);
-    }
+  // literal child: pick the matching slot's fields with masks, not a select
+  // of the two loaded slots (LLVM folds that into a phi of addresses into the
+  // per-item array and keeps the array in scratch)
+  const uint32_t node = p.it.x;
+  const bool m0 = p.l0.x == node && p.l0.y == p.it.w;
+  const bool z0 = p.l0.x == NONE;
+  const bool m1 = !m0 && !z0 && p.l1.x == node && p.l1.y == p.it.w;
+  const bool z1 = p.l1.x == NONE;
+  const uint32_t s1 = m1 ? 0xFFFFFFFFu : 0u;
+  uint32_t cz = (p.l0.z & ~s1) | (p.l1.z & s1), cw = (p.l0.w & ~s1) | (p.l1.w & s1);
+  uint32_t hx = (p.h0.x & ~s1) | (p.h1.x & s1), hy = (p.h0.y & ~s1) | (p.h1.y & s1);
+  uint32_t hz = (p.h0.z & ~s1) | (p.h1.z & s1);
+  bool found = p.lit && (m0 || m1);
+  if (p.lit && !m0 && !z0 && !m1 && !z1) {   // both first slots hold other keys: keep probing (rare)
+    uint4 lo, hi;
+    found = edge_probe_from(tab, edge_bucket(node, p.it.w, tab.edge_mask), 2, node, p.it.w, &lo, &hi);
+    cz = lo.z;
+    cw = lo.w;
+    hx = hi.x;
+    hy = hi.y;
+    hz = hi.z;
   }
-  if (p.plus) {
-    const uint32_t pf = p.prec.w;
-    o.created += 1;
-    o.e2 = (pf & F_HASH) != 0;
-    o.f2 = p.prec.y;
-    o.e3 = leaf && (pf & F_TERM);
-    o.f3 = p.prec.z;
-    const uint32_t go = (pf & F_PLUS) | ((pf & nsig) ? (pf & F_LIT) : 0u);
-    o.p1 = !leaf && go;
-    o.c1 = make_uint4(p.it.z, base_meta | (go << MF_SHIFT) | (1u << MW_SHIFT), p.prec.x, nw);
-  }
+  cw = found ? cw : 0u;
+  o.e0 = (cw & F_HASH) != 0;
+  o.f0 = hy;
+  o.e1 = leaf && (cw & F_TERM) && (mode == MODE_ROUTES || wc || p.d1);
+  o.f1 = hz;
+  const uint32_t go0 = (cw & F_PLUS) | ((cw & nsig) ? (cw & F_LIT) : 0u);
+  o.p0 = !leaf && go0;
+  o.c0 = make_uint4(cz, base_meta | (go0 << MF_SHIFT) | (wc << MW_SHIFT), hx, nw);
+  // '+' child
+  const uint32_t pf = p.plus ? p.prec.w : 0u;
+  o.e2 = (pf & F_HASH) != 0;
+  o.f2 = p.prec.y;
+  o.e3 = leaf && (pf & F_TERM);
+  o.f3 = p.prec.z;
+  const uint32_t go1 = (pf & F_PLUS) | ((pf & nsig) ? (pf & F_LIT) : 0u);
+  o.p1 = !leaf && go1;
+  o.c1 = make_uint4(p.it.z, base_meta | (go1 << MF_SHIFT) | (1u << MW_SHIFT), p.prec.x, nw);
+  o.created = (found ? 1u : 0u) + (p.plus ? 1u : 0u);
 }
 
 // lookup_routes(Topic) of a wildcard topic in ROUTES mode (emqx_router.erl:
 // 129-134): the topic's words walked as a literal key, '+'/'#' words taking
 // the '+'/'#' edges.  Rare (MQTT publishes never carry wildcards): one lane,
 // one dependent read per level.
-__device__ bool exact_walk(const DevTable& tab, const WaveLds& L, uint32_t j, uint32_t D, uint32_t* fid) {
+__device__ bool exact_walk(const DevTable& tab, const uint32_t* __restrict__ wid, uint32_t tbase, uint32_t D,
+                           uint32_t* fid) {
   uint32_t node = 0;
   for (uint32_t l = 0; l < D; ++l) {
-    const uint32_t wd = word_at(L, j, l);
+    const uint32_t wd = wid[tbase + l];
     uint32_t child = NONE;
     if (wd == WID_PLUS) child = tab.nodes[node].plus_child;
     else if (wd == WID_HASH) child = tab.hash_child[node];
@@ -777,229 +671,256 @@ __device__ bool exact_walk(const DevTable& tab, const WaveLds& L, uint32_t j, ui
   return (r.flags & F_TERM) != 0;
 }
 
-#ifdef EGM_WALK_MINW   // minimum waves per SIMD: caps the VGPRs (occupancy tuning)
-#define EGM_WALK_LB __launch_bounds__(64 * WALK_WAVES, EGM_WALK_MINW)
-#else
-#define EGM_WALK_LB __launch_bounds__(64 * WALK_WAVES)
-#endif
-__global__ EGM_WALK_LB void k_walk(DevTable tab, const uint32_t* __restrict__ off,
-                                                          uint32_t n, int mode, MatchWork w) {
-  __shared__ WaveLds lds_all[WALK_WAVES];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  WaveLds& L = lds_all[wave];
-  const uint32_t nwaves = gridDim.x * WALK_WAVES;
+// The root state of a topic: its '#' emit (never for a '$' topic) and the
+// transitions it has to take.
+__device__ __forceinline__ uint32_t root_flags(uint4 root, bool dollar, uint32_t w0) {
+  const uint32_t s0 = w0 < WID_MAX ? sig_bit(w0) : 0u;
+  return (dollar ? 0u : (root.w & F_PLUS)) | ((root.w & s0) ? (root.w & F_LIT) : 0u);
+}
+
+// Wave-uniform bookkeeping of one of the two chunks in flight (two named
+// instances, never an array indexed at run time: that would live in scratch).
+struct Half {
+  uint32_t chunk;   // chunk id, NONE = empty
+  uint32_t nt;      // topics in the chunk
+  uint32_t adm;     // topics admitted so far
+  uint32_t live;    // items of the chunk in the stack
+  uint32_t dm;      // deepest topic of the chunk
+};
+
+// Fill half h with the next light chunk (chunks with a topic deeper than
+// LIGHT_DMAX, or all of them under DEBUG_FORCE_HEAVY, are deferred to k_heavy).
+__device__ __forceinline__ void take_chunk(WaveLds& L, Half& H, uint32_t h, const uint32_t* __restrict__ off,
+                                           uint32_t n, uint32_t nchunks, const MatchWork* wk, uint32_t lane) {
+  ConstWork& w = *fresh(wk);
+  for (;;) {
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(&w.stats->next_chunk, 1u);
+    c = uni(__shfl(c, 0, 64));
+    if (c >= nchunks) {
+      H.chunk = NONE;
+      H.nt = H.adm = H.live = H.dm = 0;
+      return;
+    }
+    const uint32_t t0 = c * WALK_CHUNK;
+    const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
+    uint32_t D = 0, f = 0, base = 0;
+    if (lane < nt) {
+      D = w.lv[t0 + lane];
+      f = w.tfl[t0 + lane];
+      base = off[t0 + lane] + t0 + lane;
+    }
+    uint32_t dmax = D;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, d, 64));
+    dmax = uni(dmax);
+    if (dmax > LIGHT_DMAX || (w.debug & DEBUG_FORCE_HEAVY)) {
+      if (lane == 0) w.deferred[atomicAdd(&w.stats->n_deferred, 1u)] = c;
+      continue;
+    }
+    const uint32_t s = h * WALK_CHUNK + lane;
+    L.tinfo[s] = D | (f << 24);
+    L.tbase[s] = base;
+    L.w0[s] = lane < nt ? w.wid[base] : WID_NONE;
+    L.cnt[s] = 0;
+    L.last[s] = NONE;
+    L.fcnt[s] = 0;
+    H.chunk = c;
+    H.nt = nt;
+    H.adm = 0;
+    H.live = 0;
+    H.dm = dmax;
+    wave_sync();
+    return;
+  }
+}
+
+// Retire half hx once all its topics are admitted and its last item is done
+// (the stage has been flushed): write its per-topic counts and piece heads,
+// take the next chunk.
+#define WALK_RETIRE_HALF(HX, hx)                                                                        \
+  if (HX.chunk != NONE && HX.adm == HX.nt && HX.live == 0) {                                           \
+    const uint32_t t0 = HX.chunk * WALK_CHUNK;                                                         \
+    if (lane < HX.nt) {                                                                                \
+      ConstWork& w = *fresh(wk);                                                                 \
+      w.cnt[t0 + lane] = L.cnt[(hx) * WALK_CHUNK + lane];                                              \
+      w.head[t0 + lane] = L.last[(hx) * WALK_CHUNK + lane];                                            \
+    }                                                                                                  \
+    wave_sync();                                                                                       \
+    take_chunk(L, HX, hx, off, n, nchunks, wk, lane);                                                   \
+  }
+
+__global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __restrict__ wid,
+                                             const uint32_t* __restrict__ off, uint32_t n, int mode,
+                                             const MatchWork* wk) {
+  __shared__ WaveLds L;
+  const uint32_t lane = threadIdx.x;
   const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
   uint4 root = ld16(tab.nodes);   // wave-uniform: keep it in SGPRs
-  root.x = __builtin_amdgcn_readfirstlane(root.x);
-  root.y = __builtin_amdgcn_readfirstlane(root.y);
-  root.z = __builtin_amdgcn_readfirstlane(root.z);
-  root.w = __builtin_amdgcn_readfirstlane(root.w);
+  root.x = uni(root.x);
+  root.y = uni(root.y);
+  root.z = uni(root.z);
+  root.w = uni(root.w);
   uint32_t created = 0;
   unsigned long long iters = 0, popped = 0, bounded = 0;
   Slab sid{0, 0}, spc{0, 0};
+  Half A, B;   // slots 0..63 and 64..127
+  take_chunk(L, A, 0, off, n, nchunks, wk, lane);
+  take_chunk(L, B, 1, off, n, nchunks, wk, lane);
+  uint32_t sp = 0, nstage = 0;
+  bool admit_b = false;   // which half is being admitted
 
-  for (uint32_t c = blockIdx.x * WALK_WAVES + wave; c < nchunks; c += nwaves) {
-    const uint32_t t0 = c * WALK_CHUNK;
-    const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
-
-    // ---- topic info (lane j: topic t0 + j) ----
-    uint32_t dmax = 0;
+  for (;;) {
+    // ---- the one flush point of the loop top: before a retire, or when an
+    // admission's 64 root emits might not fit ----
     {
-      uint32_t D = 0, f = 0;
-      if (lane < nt) {
-        D = w.lv[t0 + lane];
-        f = w.tfl[t0 + lane];
+      const bool ra = A.chunk != NONE && A.adm == A.nt && A.live == 0;
+      const bool rb = B.chunk != NONE && B.adm == B.nt && B.live == 0;
+      if (nstage && (ra || rb || nstage + 64u > WALK_STAGE)) {
+        flush_stage(L, nstage, lane, wk, sid, spc);
+        nstage = 0;
       }
-      dmax = D;
-      L.tinfo[lane] = D | (f << 24);
-      L.cnt[lane] = 0;
-      L.fcnt[lane] = 0;
     }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, d, 64));
-    // Words are always staged in LDS as [topic][level] (finish() must not
-    // load from global memory, see issue()): a chunk of deep topics is walked
-    // as sub-chunks of S topics with S * dmax <= WALK_WORDS.  Topics deeper
-    // than WALK_WORDS levels go to the heavy kernel.
-    uint32_t S = WALK_CHUNK;
-    while (S > 1 && S * dmax > (uint32_t)WALK_WORDS) S >>= 1;
-    uint32_t sp = 0, nstage = 0;
-    bool ovf = (w.debug & DEBUG_FORCE_HEAVY) != 0 || dmax > (uint32_t)WALK_WORDS;
-    wave_sync();
-    for (uint32_t sub = 0; sub < nt && !ovf; sub += S) {
-    const uint32_t end = min(sub + S, nt);
-    if (lane < end - sub) {
-      const uint32_t j = sub + lane, D = L.tinfo[j] & 0xFFFFFFu;
-      const uint32_t* src = w.wid + off[t0 + j] + t0 + j;
-      uint32_t* dst = L.words + lane * dmax;
-      L.tbase[j] = lane * dmax;
-      uint32_t i = 0;
-      for (; i + 4 <= D; i += 4) {
-        uint32_t a0 = src[i], a1 = src[i + 1], a2 = src[i + 2], a3 = src[i + 3];
-        dst[i] = a0;
-        dst[i + 1] = a1;
-        dst[i + 2] = a2;
-        dst[i + 3] = a3;
+    // ---- retire chunks whose topics are all admitted and done ----
+    WALK_RETIRE_HALF(A, 0)
+    WALK_RETIRE_HALF(B, 1)
+    // ---- admission: new topics while the stack is short ----
+    if (sp < 64u) {
+      if (!admit_b && A.adm >= A.nt && B.adm < B.nt) admit_b = true;
+      else if (admit_b && B.adm >= B.nt && A.adm < A.nt) admit_b = false;
+      const uint32_t nt_h = admit_b ? B.nt : A.nt, adm_h = admit_b ? B.adm : A.adm;
+      if (adm_h < nt_h) {
+        // admit up to 64 - sp topics of the half: their root '#' emits
+        // (wildcard topics in ROUTES mode: one exact lookup, no push) and
+        // root items
+        const uint32_t k = min(64u - sp, nt_h - adm_h);
+        bool has = false, em = false;
+        uint32_t fid = NONE;
+        uint4 it = make_uint4(0, 0, 0, 0);
+        const uint32_t s = (admit_b ? WALK_CHUNK : 0u) + adm_h + lane;
+        if (lane < k) {
+          const uint32_t ti = L.tinfo[s], D = ti & 0xFFFFFFu, tf = ti >> 24;
+          if (tf & TF_WILDCARD) {
+            if (mode == MODE_ROUTES) em = exact_walk(tab, wid, L.tbase[s], D, &fid);
+          } else {
+            const bool dollar = (tf & TF_DOLLAR) != 0;
+            em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
+            fid = root.y;
+            created += 1;
+            const uint32_t w0 = L.w0[s];
+            const uint32_t fl = root_flags(root, dollar, w0);
+            has = fl != 0;
+            it = make_uint4(0, (s << MT_SHIFT) | (fl << MF_SHIFT), root.x, w0);
+          }
+        }
+        const uint64_t b = __ballot(has);
+        if (has) L.stack[sp + mbcnt(b)] = it;
+        const uint64_t be = __ballot(em);
+        if (em) {
+          const uint32_t q = nstage + mbcnt(be);
+          L.stage_fid[q] = fid;
+          L.stage_t[q] = (uint8_t)s;
+        }
+        const uint32_t pushed = popc(b);
+        sp += pushed;
+        nstage += popc(be);
+        if (admit_b) {
+          B.adm += k;
+          B.live += pushed;
+        } else {
+          A.adm += k;
+          A.live += pushed;
+        }
+        wave_sync();
       }
-      for (; i < D; ++i) dst[i] = src[i];
     }
-    wave_sync();
-    uint32_t next = sub;
-
-// Admit new topics while the stack is short: emit their root '#', push their
-// roots (wildcard topics in ROUTES mode: one exact lookup, no push).
-#define WALK_REFILL()                                                                                  \
-    if (sp < 64u && next < end) {                                                                      \
-      const uint32_t k = min(64u - sp, end - next);                                                    \
-      if (nstage + 64u > (uint32_t)WALK_STAGE) {                                                       \
-        flush_stage(L, nstage, t0, lane, w, sid, spc);                                                 \
-        nstage = 0;                                                                                    \
-      }                                                                                                \
-      bool has = false, em = false;                                                                    \
-      uint32_t fid = NONE;                                                                             \
-      uint4 it = make_uint4(0, 0, 0, 0);                                                               \
-      const uint32_t j = next + lane;                                                                  \
-      if (lane < k) {                                                                                  \
-        const uint32_t ti = L.tinfo[j], D = ti & 0xFFFFFFu, tf = ti >> 24;                             \
-        if (tf & TF_WILDCARD) {                                                                        \
-          if (mode == MODE_ROUTES) em = exact_walk(tab, L, j, D, &fid);                     \
-        } else if (D <= LEVEL_MAX) {                                                                   \
-          const bool dollar = (tf & TF_DOLLAR) != 0;                                                   \
-          em = (root.w & F_HASH) && !dollar; /* filter '#': never for a '$' topic */                   \
-          fid = root.y;                                                                                \
-          created += 1;                                                                                \
-          const uint32_t w0 = word_at(L, j, 0);                                             \
-          const uint32_t s0 = w0 < WID_MAX ? sig_bit(w0) : 0u;                                         \
-          const uint32_t fl = (dollar ? 0u : (root.w & F_PLUS)) | ((root.w & s0) ? (root.w & F_LIT) : 0u); \
-          has = fl != 0;                                                                               \
-          it = make_uint4(0, (j << MT_SHIFT) | (fl << MF_SHIFT), root.x, w0);                          \
-        }                                                                                              \
-      }                                                                                                \
-      const uint64_t b = __ballot(has);                                                                \
-      if (has) L.stack[sp + mbcnt(b)] = it;                                                            \
-      sp += popc(b);                                                                                   \
-      const uint64_t be = __ballot(em);                                                                \
-      if (em) {                                                                                        \
-        const uint32_t q = nstage + mbcnt(be);                                                         \
-        L.stage_fid[q] = fid;                                                                          \
-        L.stage_t[q] = (uint8_t)j;                                                                     \
-      }                                                                                                \
-      nstage += popc(be);                                                                              \
-      next += k;                                                                                       \
-      wave_sync();                                                                                     \
-    }
-
-// Pop up to 64 items (one per lane) and issue all their reads.  An item
-// pushes at most two children (net +1), so popping k <= room - dmax items
-// keeps room >= dmax afterwards; with room <= dmax the wave pops one item at a
-// time, i.e. a plain DFS, whose stack grows by at most one pending sibling per
-// level below the top item (< dmax).  So the frontier never overflows the LDS
-// stack: a deep, wide one (C3: depth 16, '+' p=.35) narrows the wave instead of
-// deferring the chunk to k_heavy.
-#define WALK_POP(P, TAKE)                                                                              \
-    {                                                                                                  \
-      const uint32_t room_ = (uint32_t)WALK_STACK - sp;                                                \
-      const uint32_t lim_ = room_ > dmax ? room_ - dmax : (room_ ? 1u : 0u);                          \
-      const uint32_t want_ = min(64u, sp), take_ = min(want_, lim_), bi_ = sp - take_;                 \
-      if (take_ == 0 && sp) ovf = true;                                                                \
-      bounded += take_ < want_ ? 1u : 0u;                                                              \
-      P.act = lane < take_;                                                                            \
-      P.it = L.stack[min(bi_ + lane, (uint32_t)WALK_STACK - 1)]; /* unconditional: see issue() */     \
-      sp = bi_;                                                                                        \
-      TAKE = take_;                                                                                    \
-      iters += take_ ? 1u : 0u;                                                                        \
-      popped += take_;                                                                                 \
-      issue(tab, L, P);                                                                    \
-    }
-
-// Consume a popped batch's reads: children -> stack (counted first: an
-// overflow abandons the chunk), emits -> stage (flushed when full).
-#define WALK_RETIRE(P)                                                                                 \
-    {                                                                                                  \
-      Out o;                                                                                           \
-      finish(tab, mode, P, o);                                                           \
-      created += o.created;                                                                            \
-      const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);                                       \
-      const uint32_t m0 = popc(c0b), nc = m0 + popc(c1b);                                              \
-      if (sp + nc > (uint32_t)WALK_STACK) {                                                            \
-        ovf = true;                                                                                    \
-      } else {                                                                                         \
-        if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;                                                     \
-        if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;                                                \
-        sp += nc;                                                                                      \
-        const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1);                                       \
-        const uint64_t b2 = __ballot(o.e2), b3 = __ballot(o.e3);                                       \
-        const uint32_t n0 = popc(b0), n1 = popc(b1), n2 = popc(b2);                                    \
-        const uint32_t ne = n0 + n1 + n2 + popc(b3);                                                   \
-        if (nstage + ne > (uint32_t)WALK_STAGE) {                                                      \
-          wave_sync();                                                                                 \
-          flush_stage(L, nstage, t0, lane, w, sid, spc);                                               \
-          nstage = 0;                                                                                  \
-        }                                                                                              \
-        const uint8_t tt = (uint8_t)((P.it.y >> MT_SHIFT) & 0x7Fu);                                    \
-        if (o.e0) {                                                                                    \
-          const uint32_t q = nstage + mbcnt(b0);                                                       \
-          L.stage_fid[q] = o.f0;                                                                       \
-          L.stage_t[q] = tt;                                                                           \
-        }                                                                                              \
-        if (o.e1) {                                                                                    \
-          const uint32_t q = nstage + n0 + mbcnt(b1);                                                  \
-          L.stage_fid[q] = o.f1;                                                                       \
-          L.stage_t[q] = tt;                                                                           \
-        }                                                                                              \
-        if (o.e2) {                                                                                    \
-          const uint32_t q = nstage + n0 + n1 + mbcnt(b2);                                             \
-          L.stage_fid[q] = o.f2;                                                                       \
-          L.stage_t[q] = tt;                                                                           \
-        }                                                                                              \
-        if (o.e3) {                                                                                    \
-          const uint32_t q = nstage + n0 + n1 + n2 + mbcnt(b3);                                        \
-          L.stage_fid[q] = o.f3;                                                                       \
-          L.stage_t[q] = tt;                                                                           \
-        }                                                                                              \
-        nstage += ne;                                                                                  \
-      }                                                                                                \
-      wave_sync();                                                                                     \
-    }
-
-    while (!ovf) {
-      WALK_REFILL();
-      if (sp == 0) {
-        if (next >= end) break;
-        continue;
-      }
-      Pend pa;
-      uint32_t ta;
-      WALK_POP(pa, ta);
-      wave_sync();
-      WALK_RETIRE(pa);
-    }
-    }  // sub-chunks
-#undef WALK_REFILL
-#undef WALK_POP
-#undef WALK_RETIRE
-    wave_sync();
-
-    if (ovf) {  // frontier exceeded the LDS stack: hand the chunk to k_heavy
-      if (lane == 0) {
-        const uint32_t d = atomicAdd(&w.stats->n_deferred, 1u);
-        w.deferred[d] = c;
-      }
-      for (uint32_t j = lane; j < nt; j += 64) w.cnt[t0 + j] = 0;
-      nstage = 0;
-      wave_sync();
+    if (sp == 0) {
+      if (A.chunk == NONE && B.chunk == NONE) break;
       continue;
     }
-    if (nstage) flush_stage(L, nstage, t0, lane, w, sid, spc);
-    for (uint32_t j = lane; j < nt; j += 64) w.cnt[t0 + j] = L.cnt[j];
+
+    // ---- pop up to 64 items and issue all their reads ----
+    // An item pushes at most two children (net +1), so popping k <= room - dmax
+    // items keeps room >= dmax afterwards; with room <= dmax the wave pops one
+    // item at a time, a plain DFS, whose stack grows by at most one pending
+    // sibling per level below the top item.  So the stack never overflows: a
+    // deep, wide frontier (C3: depth 16, '+' p=.35) narrows the wave instead.
+    const uint32_t dmax = max(A.dm, B.dm);
+    const uint32_t room = WALK_STACK - sp;
+    const uint32_t lim = room > dmax ? room - dmax : 1u;
+    const uint32_t want = min(64u, sp), take = min(want, lim), bi = sp - take;
+    bounded += take < want ? 1u : 0u;
+    iters += 1;
+    popped += take;
+    Pend p;
+    p.act = lane < take;
+    p.it = L.stack[min(bi + lane, WALK_STACK - 1)];   // unconditional: see issue()
+    sp = bi;
+    const uint32_t slot = (p.it.y >> MT_SHIFT) & 0x7Fu;
+    const uint32_t ti = L.tinfo[slot];
+    p.D = ti & 0xFFFFFFu;
+    p.d1 = p.D == 1 && ((ti >> 24) & TF_DOLLAR);
+    issue(tab, wid, L.tbase[slot], p);
+    {
+      const uint32_t n1 = popc(__ballot(p.act && slot >= WALK_CHUNK));
+      B.live -= n1;
+      A.live -= take - n1;
+    }
+    wave_sync();
+
+    // ---- consume: children -> stack, emits -> stage ----
+    Out o;
+    finish(tab, mode, p, o);
+    created += o.created;
+    const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
+    const uint32_t m0 = popc(c0b);
+    if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
+    if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;
+    const uint32_t np = m0 + popc(c1b);
+    const uint32_t n1 = popc(__ballot(o.p0 && slot >= WALK_CHUNK)) + popc(__ballot(o.p1 && slot >= WALK_CHUNK));
+    B.live += n1;
+    A.live += np - n1;
+    sp += np;
+    // emits (at most 4 per lane): the stage is flushed first if they do not fit
+    {
+      const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
+      const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
+      if (nstage + ne > WALK_STAGE) {
+        wave_sync();
+        flush_stage(L, nstage, lane, wk, sid, spc);
+        nstage = 0;
+      }
+      const uint8_t st = (uint8_t)slot;
+      if (o.e0) {
+        const uint32_t q = nstage + mbcnt(b0);
+        L.stage_fid[q] = o.f0;
+        L.stage_t[q] = st;
+      }
+      if (o.e1) {
+        const uint32_t q = nstage + n0 + mbcnt(b1);
+        L.stage_fid[q] = o.f1;
+        L.stage_t[q] = st;
+      }
+      if (o.e2) {
+        const uint32_t q = nstage + n1 + mbcnt(b2);
+        L.stage_fid[q] = o.f2;
+        L.stage_t[q] = st;
+      }
+      if (o.e3) {
+        const uint32_t q = nstage + n2 + mbcnt(b3);
+        L.stage_fid[q] = o.f3;
+        L.stage_t[q] = st;
+      }
+      nstage += ne;
+    }
     wave_sync();
   }
-  for (unsigned long long i = spc.cur + lane; i < spc.end && i < w.pieces_cap; i += 64)
-    w.pieces[i] = empty_piece();   // unused tail of the last pieces slab
+#undef WALK_RETIRE_HALF
   unsigned long long v = created;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
   if (lane == 0) {
+    ConstWork& w = *fresh(wk);
     if (v) atomicAdd(&w.stats->visited, v);
     atomicAdd(&w.stats->iters, iters);
     atomicAdd(&w.stats->popped, popped);
@@ -1008,115 +929,149 @@ __global__ EGM_WALK_LB void k_walk(DevTable tab, const uint32_t* __restrict__ of
 }
 
 // ----------------------------------------------------------------- heavy ----
-// Topics of deferred chunks: one wave per topic, LDS stack of HEAVY_STACK
-// items, two passes (count, then fill at a reserved offset) so the output
-// needs no staging.
-__global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __restrict__ off, uint32_t n,
-                                              int mode, MatchWork w) {
-  __shared__ uint4 stk_a[HEAVY_STACK];
-  __shared__ uint32_t stk_t[HEAVY_STACK];
+// Topics of deferred chunks (a topic deeper than LIGHT_DMAX, or every chunk
+// under DEBUG_FORCE_HEAVY): one wave per topic, the same states and pop bound
+// as k_walk, but the stack lives in HBM — heavy_cap items per wave, sized by
+// the host to at least the batch's deepest possible topic + 192, so by the
+// pop-bound argument no legal topic (<= 65 535 bytes, emqx_topic.erl:45,
+// 99-100) can overflow it.  Two passes: count, then fill at a reserved offset
+// (one piece per topic).
+__device__ __forceinline__ void heavy_fence() {
+  // the wave's own stack stores must be visible to its next loads of them
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+
+__global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __restrict__ off, uint32_t n, int mode,
+                                              MatchWork w) {
   const uint32_t lane = threadIdx.x;
-  const uint4 rootr = ld16(tab.nodes);
+  uint4 root = ld16(tab.nodes);
+  root.x = uni(root.x);
+  root.y = uni(root.y);
+  root.z = uni(root.z);
+  root.w = uni(root.w);
   const uint32_t total = w.stats->n_deferred * (uint32_t)WALK_CHUNK;
-  uint64_t visited = 0;
+  uint4* stk = w.heavy_stack + (uint64_t)blockIdx.x * w.heavy_cap;
+  const uint32_t cap = w.heavy_cap;
+  unsigned long long created = 0;
   for (;;) {
     uint32_t idx = 0;
     if (lane == 0) idx = atomicAdd(&w.stats->heavy_next, 1u);
-    idx = __shfl(idx, 0, 64);
+    idx = uni(__shfl(idx, 0, 64));
     if (idx >= total) break;
     const uint32_t t = w.deferred[idx / WALK_CHUNK] * WALK_CHUNK + idx % WALK_CHUNK;
     if (t >= n) continue;
-    const uint32_t D = w.lv[t], tf = w.tfl[t], gb = off[t] + t;
-    if ((tf & TF_WILDCARD) && mode == MODE_TRIE) {
+    const uint32_t D = uni(w.lv[t]), tf = uni(w.tfl[t]), tb = uni(off[t] + t);
+    if (tf & TF_WILDCARD) {   // no trie walk: TRIE mode matches nothing, ROUTES mode one exact lookup
+      uint32_t fid = NONE;
+      const bool em = mode == MODE_ROUTES && exact_walk(tab, w.wid, tb, D, &fid);
       if (lane == 0) {
-        w.cnt[t] = 0;
+        uint32_t pc = NONE;
+        if (em) {
+          const unsigned long long base = atomicAdd(&w.stats->cursor, 1ull);
+          const unsigned long long p = atomicAdd(&w.stats->pieces, 1ull);
+          if (base < w.ids_cap && p < w.pieces_cap) {
+            w.ids_tmp[base] = fid;
+            w.pieces[p] = make_uint4(1, (uint32_t)base, 0, NONE);
+            pc = (uint32_t)p;
+          } else {
+            atomicOr(&w.stats->overflow, 1u);
+          }
+        }
+        w.cnt[t] = em ? 1u : 0u;
+        w.head[t] = pc;
         w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
       }
       continue;
     }
-    const Item root = root_item(rootr, 0, (tf & TF_WILDCARD) != 0);
-    unsigned long long base = 0, pbase = 0;
-    uint32_t count = 0;
-    bool err = false, fits = true;
-    for (int pass = 0; pass < 2 && !err; ++pass) {
-      uint32_t sp = 1, k = 0;
+    if (D + 192u > cap) {   // cannot happen for a legal topic (the host sizes cap from the batch)
       if (lane == 0) {
-        stk_a[0] = root.a;
-        stk_t[0] = root.term;
-      }
-      wave_sync();
-      while (sp) {
-        const uint32_t take = min(64u, sp), bi = sp - take;
-        const bool act = lane < take;
-        Item it;
-        it.a = make_uint4(0, 0, 0, 0);
-        it.term = NONE;
-        if (act) {
-          it.a = stk_a[bi + lane];
-          it.term = stk_t[bi + lane];
-        }
-        sp = bi;
-        wave_sync();
-        Expand x;
-        x.h0 = x.h1 = x.hc0 = x.hc1 = false;
-        if (act) {
-          const uint32_t level = it.a.y & 0x1FFFFu;
-          const uint32_t wd = level < D ? w.wid[gb + level] : WID_NONE;
-          expand(tab, mode, it, D, tf, wd, x);
-        }
-        const uint64_t b0 = __ballot(x.h0), b1 = __ballot(x.h1);
-        const uint32_t n0 = popc(b0);
-        if (pass == 1 && fits) {
-          if (x.h0) w.ids_tmp[base + k + mbcnt(b0)] = x.e0;
-          if (x.h1) w.ids_tmp[base + k + n0 + mbcnt(b1)] = x.e1;
-        }
-        k += n0 + popc(b1);
-        const uint64_t c0 = __ballot(x.hc0), c1 = __ballot(x.hc1);
-        const uint32_t m0 = popc(c0), nc = m0 + popc(c1);
-        if (sp + nc > (uint32_t)HEAVY_STACK) {
-          err = true;
-          break;
-        }
-        if (x.hc0) {
-          const uint32_t p = sp + mbcnt(c0);
-          stk_a[p] = x.c0.a;
-          stk_t[p] = x.c0.term;
-        }
-        if (x.hc1) {
-          const uint32_t p = sp + m0 + mbcnt(c1);
-          stk_a[p] = x.c1.a;
-          stk_t[p] = x.c1.term;
-        }
-        sp += nc;
-        if (pass == 0) visited += take;
-        wave_sync();
-      }
-      wave_sync();
-      if (pass == 0 && !err) {
-        count = k;
-        if (lane == 0 && count) {
-          base = atomicAdd(&w.stats->cursor, (unsigned long long)count);
-          pbase = atomicAdd(&w.stats->pieces, 1ull);
-        }
-        base = __shfl(base, 0, 64);
-        pbase = __shfl(pbase, 0, 64);
-        fits = base + count <= w.ids_cap && pbase < w.pieces_cap;
-        if (!fits && lane == 0) atomicOr(&w.stats->overflow, 1u);
-      }
-    }
-    if (lane == 0) {
-      if (err) {
         atomicAdd(&w.stats->errors, 1u);
         w.cnt[t] = 0;
+        w.head[t] = NONE;
         w.tfl[t] = (uint8_t)(tf | TF_HEAVY | TF_ERROR);
-      } else {
-        w.cnt[t] = count;
-        if (count && fits) w.pieces[pbase] = mk_piece(t, count | HEAVY_PIECE, (uint32_t)base, 0);
-        w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
+      }
+      continue;
+    }
+    const bool dollar = (tf & TF_DOLLAR) != 0;
+    const uint32_t w0 = uni(w.wid[tb]);
+    const uint32_t rfl = root_flags(root, dollar, w0);
+    const bool rem = (root.w & F_HASH) && !dollar;
+    unsigned long long base = 0;
+    uint32_t count = 0;
+    bool fits = true;
+    for (int pass = 0; pass < 2; ++pass) {
+      uint32_t sp = 0, k = 0;
+      if (rem) {
+        if (pass == 1 && fits && lane == 0) w.ids_tmp[base] = root.y;
+        k = 1;
+      }
+      if (rfl) {
+        if (lane == 0) stk[0] = make_uint4(0, rfl << MF_SHIFT, root.x, w0);
+        sp = 1;
+      }
+      if (pass == 0 && lane == 0) created += 1;
+      heavy_fence();
+      while (sp) {
+        const uint32_t room = cap - sp;
+        const uint32_t lim = room > D ? room - D : 1u;
+        const uint32_t take = min(min(64u, sp), lim), bi = sp - take;
+        Pend p;
+        p.act = lane < take;
+        p.it = stk[p.act ? bi + lane : 0u];
+        p.D = D;
+        p.d1 = D == 1 && (tf & TF_DOLLAR);
+        issue(tab, w.wid, tb, p);
+        sp = bi;
+        Out o;
+        finish(tab, mode, p, o);
+        if (pass == 0) created += o.created;
+        const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
+        const uint32_t m0 = popc(c0b);
+        if (sp + m0 + popc(c1b) > cap) {   // guard only: the pop bound keeps sp + pushes <= cap
+          count = 0;
+          fits = false;
+          if (lane == 0) atomicOr(&w.stats->overflow, 4u);
+          break;
+        }
+        heavy_fence();   // every lane's pop load is done before the pushes overwrite those entries
+        if (o.p0) stk[sp + mbcnt(c0b)] = o.c0;
+        if (o.p1) stk[sp + m0 + mbcnt(c1b)] = o.c1;
+        sp += m0 + popc(c1b);
+        const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
+        const uint32_t n0 = popc(b0), n1 = popc(b1), n2 = popc(b2);
+        if (pass == 1 && fits) {
+          if (o.e0) w.ids_tmp[base + k + mbcnt(b0)] = o.f0;
+          if (o.e1) w.ids_tmp[base + k + n0 + mbcnt(b1)] = o.f1;
+          if (o.e2) w.ids_tmp[base + k + n0 + n1 + mbcnt(b2)] = o.f2;
+          if (o.e3) w.ids_tmp[base + k + n0 + n1 + n2 + mbcnt(b3)] = o.f3;
+        }
+        k += n0 + n1 + n2 + popc(b3);
+        heavy_fence();
+      }
+      if (pass == 0) {
+        count = k;
+        unsigned long long pb = 0;
+        if (lane == 0 && count) {
+          base = atomicAdd(&w.stats->cursor, (unsigned long long)count);
+          pb = atomicAdd(&w.stats->pieces, 1ull);
+        }
+        base = __shfl(base, 0, 64);
+        pb = __shfl(pb, 0, 64);
+        fits = count == 0 || (base + count <= w.ids_cap && pb < w.pieces_cap);
+        if (lane == 0) {
+          if (!fits) atomicOr(&w.stats->overflow, 1u);
+          w.cnt[t] = count;
+          w.head[t] = (count && fits) ? (uint32_t)pb : NONE;
+          if (count && fits) w.pieces[pb] = make_uint4(count, (uint32_t)base, 0, NONE);
+          w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
+        }
+        if (!count || !fits) break;
       }
     }
   }
-  if (lane == 0 && visited) atomicAdd(&w.stats->visited, (unsigned long long)visited);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) created += __shfl_xor(created, d, 64);
+  if (lane == 0 && created) atomicAdd(&w.stats->visited, created);
 }
 
 // ------------------------------------------------------------------ scan ----
@@ -1195,31 +1150,25 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
   if (blockIdx.x == 0 && threadIdx.x == 0) row_ptr[n] = tile_sums[ntiles];
 }
 
-// pieces -> CSR rows, no atomics: a piece knows its offset inside the row.
-// One wave per window of 64 pieces: lane k loads piece k and its row start,
-// a wave scan lays the window's ids out as one run [0, tot), and the lanes
-// copy that run with consecutive lanes on consecutive ids (a binary search
-// over the window's 64 scan values finds each id's piece).  The pieces of one
-// flush have contiguous sources and topics of one chunk, so the reads and the
-// row_ptr loads coalesce.  Light pieces of topics re-run by k_heavy and unused
-// slab slots (count 0) are skipped.
+// Pieces -> CSR rows, no atomics.  One wave per window of 64 topics: lane k
+// follows topic k's piece chain (head[t] -> prev ...; usually one or two
+// pieces), and in each round the wave lays the window's current pieces out as
+// one run [0, tot) by a scan and copies it with consecutive lanes on
+// consecutive ids (a binary search over the 64 scan values finds each id's
+// piece).  Every output line of the window's rows [row_ptr[t0],
+// row_ptr[t0 + 64]) is written by this one wave within a few rounds, so the
+// L2 merges the partial writes into whole lines.
 #ifndef EGM_COMPACT_WAVES
 #define EGM_COMPACT_WAVES 4
 #endif
-#ifndef EGM_COMPACT_BLOCKS
-#define EGM_COMPACT_BLOCKS 65536   // grid cap; A/B at C2: 8192 -> 2.07 ms, 32768 -> 1.80, 65536 -> 1.74
-#endif
 constexpr int COMPACT_WAVES = EGM_COMPACT_WAVES;
-#ifndef EGM_COMPACT_IPL
-#define EGM_COMPACT_IPL 8   // 8: 2.06 -> 1.91 ms at C2 (A/B, rocprof)
-#endif
-constexpr int COMPACT_IPL = EGM_COMPACT_IPL;
-__global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __restrict__ pieces,
-                                                                const uint8_t* __restrict__ tfl,
+constexpr int COMPACT_IPL = 8;   // ids per lane per copy round in flight
+__global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint32_t* __restrict__ head,
+                                                                const uint4* __restrict__ pieces,
                                                                 const uint32_t* __restrict__ ids_tmp, uint32_t n,
                                                                 const uint64_t* __restrict__ row_ptr,
                                                                 uint32_t* __restrict__ ids, uint64_t ids_cap,
-                                                                uint64_t pieces_cap, MatchStats* stats) {
+                                                                MatchStats* stats) {
   __shared__ uint32_t s_scan[COMPACT_WAVES][64];
   __shared__ uint32_t s_src[COMPACT_WAVES][64];
   __shared__ uint64_t s_dst[COMPACT_WAVES][64];
@@ -1231,64 +1180,73 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
     return;
   }
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t np = min((uint64_t)stats->pieces, pieces_cap);
-  const bool any_heavy = stats->n_deferred != 0;   // else no light piece can be stale
-  // a contiguous range of windows per wave (not a grid stride): the flushes
-  // of one chunk sit next to each other in pieces[], so one wave completes
-  // the cache lines of a chunk's rows
-  const uint64_t nwin = (np + 63) / 64, nw = (uint64_t)gridDim.x * COMPACT_WAVES;
-  const uint64_t per = (nwin + nw - 1) / nw, me = (uint64_t)blockIdx.x * COMPACT_WAVES + wave;
-  const uint64_t wend = min(nwin, (me + 1) * per) * 64;
-  uint64_t w0 = me * per * 64;
-  uint4 pc = pieces[min(w0 + lane, np - 1)];   // unconditional (a load under a branch is waited for at once)
-  for (; w0 < wend; w0 += 64) {
-    const uint64_t i = w0 + lane;
-    uint32_t c = i < np ? (pc.y & ~HEAVY_PIECE) : 0u;
-    const uint64_t rp = row_ptr[c ? pc.x : 0u];
-    if (any_heavy && c && (tfl[pc.x] & TF_HEAVY) && !(pc.y & HEAVY_PIECE)) c = 0;
-    uint32_t tot;
-    const uint32_t ex = wave_excl_scan(c, lane, &tot);
-    s_scan[wave][lane] = ex;
-    s_src[wave][lane] = pc.z;
-    s_dst[wave][lane] = rp + pc.w;
-    wave_sync();
-    pc = pieces[min(i + 64, np - 1)];   // the next window's piece, in flight during the copy
-    // COMPACT_IPL ids per lane per round: their searches, loads and stores overlap
-    for (uint32_t q0 = lane; q0 < tot; q0 += 64 * COMPACT_IPL) {
-      uint32_t v[COMPACT_IPL];
-      uint64_t d[COMPACT_IPL];
+  const uint32_t nwin = (n + 63) / 64;
+  for (uint32_t win = blockIdx.x * COMPACT_WAVES + wave; win < nwin; win += gridDim.x * COMPACT_WAVES) {
+    const uint32_t t = win * 64 + lane;
+    uint32_t p = t < n ? head[t] : NONE;
+    const uint64_t rs = row_ptr[min(t, n)];
+    while (__ballot(p != NONE)) {
+      const uint4 pc = pieces[p != NONE ? p : 0u];   // unconditional (a load under a branch is waited for at once)
+      const uint32_t c = p != NONE ? pc.x : 0u;
+      uint32_t tot;
+      const uint32_t ex = wave_excl_scan(c, lane, &tot);
+      s_scan[wave][lane] = ex;
+      s_src[wave][lane] = pc.y;
+      s_dst[wave][lane] = rs + pc.z;
+      wave_sync();
+      for (uint32_t q0 = lane; q0 < tot; q0 += 64 * COMPACT_IPL) {
+        uint32_t v[COMPACT_IPL];
+        uint64_t d[COMPACT_IPL];
 #pragma unroll
-      for (int r = 0; r < COMPACT_IPL; ++r) {
-        const uint32_t q = min(q0 + 64u * r, tot - 1);
-        uint32_t k = 0;
+        for (int r = 0; r < COMPACT_IPL; ++r) {
+          const uint32_t q = min(q0 + 64u * r, tot - 1);
+          uint32_t k = 0;
 #pragma unroll
-        for (uint32_t step = 32; step >= 1; step >>= 1)
-          if (s_scan[wave][k + step] <= q) k += step;
-        const uint32_t o = q - s_scan[wave][k];
-        d[r] = s_dst[wave][k] + o;
-        v[r] = ids_tmp[s_src[wave][k] + o];
-      }
-#pragma unroll
-      for (int r = 0; r < COMPACT_IPL; ++r)
-        if (q0 + 64u * r < tot) {
-          ids[d[r]] = v[r];   // plain stores: nontemporal ones measured 2x slower here
+          for (uint32_t step = 32; step >= 1; step >>= 1)
+            if (s_scan[wave][k + step] <= q) k += step;
+          const uint32_t o = q - s_scan[wave][k];
+          d[r] = s_dst[wave][k] + o;
+          v[r] = ids_tmp[s_src[wave][k] + o];
         }
+#pragma unroll
+        for (int r = 0; r < COMPACT_IPL; ++r)
+          if (q0 + 64u * r < tot) ids[d[r]] = v[r];
+      }
+      wave_sync();
+      p = p != NONE ? pc.w : NONE;
     }
-    wave_sync();
   }
 }
 
+// The walk's workspace descriptor, written to device memory in stream order.
+__global__ void k_setup(MatchWork w, MatchWork* out) {
+  if (threadIdx.x == 0) *out = w;
+}
+
 // ------------------------------------------------------------- launchers ----
+// The walk runs persistent waves (one per block) that take chunks from a
+// global counter: as many as the GPU holds at once, fewer for a small batch.
+static uint32_t walk_resident_waves() {
+  static uint32_t cached = 0;
+  if (!cached) {
+    int dev = 0, cus = 256, per = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_walk, 64, 0) != hipSuccess || per <= 0) per = 16;
+    cached = (uint32_t)(cus * per);
+  }
+  return cached;
+}
+
 int walk_grid_blocks(uint32_t n) {
   const uint32_t chunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
-  uint32_t blocks = (chunks + WALK_WAVES - 1) / WALK_WAVES;
-  const uint32_t cap = 256 * 32 / WALK_WAVES;  // grid-stride beyond 32 waves per CU
+  uint32_t blocks = (chunks + 1) / 2;   // two chunks in flight per wave
+  const uint32_t cap = walk_resident_waves();
   if (blocks > cap) blocks = cap;
-  blocks = (blocks + 7) & ~7u;                 // a multiple of the 8 XCDs
   return blocks ? (int)blocks : 1;
 }
 
-int walk_waves_per_block() { return WALK_WAVES; }
+uint32_t heavy_stack_items(uint64_t max_levels) { return (uint32_t)(max_levels + 256); }
 
 size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
@@ -1312,15 +1270,16 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   hipLaunchKernelGGL(k_tokenise, dim3((n + TOK_BLOCK - 1) / TOK_BLOCK), dim3(TOK_BLOCK), 0, s, tab, blob,
                      off, n, w.wid, w.lv, w.tfl);
   if (ev_walk) hipEventRecord(ev_walk[0], s);
-  hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64 * WALK_WAVES), 0, s, tab, off, n, mode, w);
+  hipLaunchKernelGGL(k_setup, dim3(1), dim3(64), 0, s, w, w.self);
+  hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64), 0, s, tab, (const uint32_t*)w.wid, off, n, mode,
+                     (const MatchWork*)w.self);
   if (ev_walk) hipEventRecord(ev_walk[1], s);
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
   scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);
-  // shorter window ranges per wave keep more copies in flight; small batches
-  // get a small grid (the piece count is only known on the device)
-  const uint32_t cblocks = (uint32_t)std::min<uint64_t>(EGM_COMPACT_BLOCKS, std::max<uint64_t>(256, ((uint64_t)n + 63) / 64));
-  hipLaunchKernelGGL(k_compact, dim3(cblocks), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.tfl, w.ids_tmp, n, out.row_ptr, out.ids,
-                     out.ids_cap, w.pieces_cap, w.stats);
+  const uint32_t nwin = (n + 63) / 64;
+  const uint32_t cblocks = std::min<uint32_t>(65536, (nwin + COMPACT_WAVES - 1) / COMPACT_WAVES);
+  hipLaunchKernelGGL(k_compact, dim3(cblocks ? cblocks : 1), dim3(64 * COMPACT_WAVES), 0, s, w.head, w.pieces,
+                     w.ids_tmp, n, out.row_ptr, out.ids, out.ids_cap, w.stats);
   return hipGetLastError();
 }
 
