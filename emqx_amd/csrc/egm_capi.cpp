@@ -15,6 +15,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/emqx_gpu_match.h"
@@ -99,7 +100,7 @@ struct egm_ctx {
   std::string err;
 
   // per-batch workspace
-  DevBuf wid, lv, tfl, cnt, head, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats, work_desc;
+  DevBuf wid, lv, tfl, cnt, head, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats;
   uint64_t pieces_cap = 0, ids_tmp_cap = 0;
   DevBuf in_blob, in_off, out_row, out_ids;
   uint32_t heavy_waves = 64;     // waves of the heavy kernel (rare path; each owns an HBM stack)
@@ -123,6 +124,24 @@ struct egm_ctx {
   std::vector<hipEvent_t> ev_free;
   double walk_ms = 0, fan_ms = 0;
   uint64_t walk_n = 0, fan_n = 0;
+
+  // The per-context workspaces (match, fan-out, merge) are shared by every
+  // launch, whatever stream the caller gives: a launch on a new stream first
+  // waits for the last launch that used them (one event, recorded after each).
+  hipEvent_t work_ev = nullptr;
+  hipStream_t work_stream = nullptr;
+  void work_begin(hipStream_t s) {
+    if (work_stream && work_stream != s && work_ev) hipStreamWaitEvent(s, work_ev, 0);
+  }
+  void work_end(hipStream_t s) {
+    if (!work_ev && hipEventCreateWithFlags(&work_ev, hipEventDisableTiming) != hipSuccess) work_ev = nullptr;
+    if (work_ev) hipEventRecord(work_ev, s);
+    work_stream = s;
+  }
+  // last fan-out (egm_last_fanout)
+  const uint64_t* fan_drow = nullptr;
+  uint32_t fan_topics = 0;
+  hipStream_t fan_stream = nullptr;
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -318,6 +337,20 @@ static int commit_locked(egm_ctx* c, uint64_t* epoch) {
   c->last_commit = CommitStats{};
   const HostTable& t = c->table;
   DirtyLog d = c->table.take_dirty();
+  // on any failure below, the changes go back into the table's log, so the
+  // next commit publishes them (the half-written slot stays invalid)
+  struct Restore {
+    egm_ctx* c;
+    const DirtyLog& d;
+    bool armed = true;
+    ~Restore() {
+      if (armed) c->table.restore_dirty(d);
+    }
+  } restore{c, d};
+  if (c->debug & EGM_DEBUG_FAIL_COMMIT) {   // test hook: a commit that fails after taking the log (one shot)
+    c->debug &= ~EGM_DEBUG_FAIL_COMMIT;
+    return c->fail(EGM_E_DEVICE, "commit: injected failure");
+  }
   const int x = c->cur_slot < 0 ? 0 : 1 - c->cur_slot;
   Slot& S = c->slots[x];
   Slot* C = c->cur_slot < 0 ? nullptr : &c->slots[c->cur_slot];
@@ -375,6 +408,7 @@ static int commit_locked(egm_ctx* c, uint64_t* epoch) {
     c->last_commit.patched = np;
   }
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "commit: sync");
+  restore.armed = false;
   S.valid = true;
   S.pending.clear();
   if (C) C->pending.merge(d);   // the previous epoch's slot now lacks this commit's changes
@@ -426,7 +460,6 @@ static int ensure_work(egm_ctx* c, uint32_t n, uint64_t blob_bytes, uint64_t ids
   c->heavy_cap = (uint32_t)std::min<uint64_t>(c->heavy_stack.cap / 16 / c->heavy_waves, 0xFFFFFFFFull);
   if ((e = c->tile_sums.ensure((scan_tiles(n) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "tile_sums");
   if ((e = c->stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "stats");
-  if ((e = c->work_desc.ensure(sizeof(MatchWork))) != hipSuccess) return c->hip_fail(e, "work descriptor");
   return EGM_OK;
 }
 
@@ -447,7 +480,6 @@ static MatchWork work_view(egm_ctx* c) {
   w.heavy_cap = c->heavy_cap;
   w.tile_sums = c->tile_sums.as<uint64_t>();
   w.stats = c->stats.as<MatchStats>();
-  w.self = c->work_desc.as<MatchWork>();
   w.debug = c->debug;
   return w;
 }
@@ -461,7 +493,9 @@ static int run_match(egm_ctx* c, const Epoch& ep, const uint8_t* d_blob, const u
     evp[0] = c->take_event();
     evp[1] = c->take_event();
   }
+  c->work_begin(s);
   hipError_t e = launch_match(ep.view, d_blob, d_off, n, mode, w, o, s, c->timing ? evp : nullptr);
+  c->work_end(s);
   note_use(c, ep.slot, s);   // a later commit must not overwrite this slot before the walk is done
   if (c->timing) {
     c->ev_walk.push_back(evp[0]);
@@ -487,6 +521,33 @@ static bool valid_offsets(const uint32_t* off, uint32_t n) {
   if (!off) return false;
   for (uint32_t i = 0; i < n; ++i)
     if (off[i + 1] < off[i]) return false;
+  return true;
+}
+
+// Check a batch of inserts against the table before changing anything (the
+// reference applies route changes in all-or-nothing mnesia transactions,
+// emqx_router.erl:252-303): every new filter's id must be < WID_MAX, unused by
+// a live filter (deletes of the same delta apply after the inserts) and not
+// claimed twice in the batch.  Filters already present (or repeated in the
+// batch) are idempotent no-ops (emqx_trie.erl:84-86).
+static bool validate_inserts(const HostTable& t, const uint8_t* blob, const uint32_t* off, uint32_t n,
+                             const uint32_t* ids, bool from_empty, std::string* why) {
+  if (!ids) return true;   // ids assigned by the table
+  std::unordered_set<std::string> seen_bytes;
+  std::unordered_set<uint32_t> seen_ids;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t* p = blob + off[i];
+    const uint32_t len = off[i + 1] - off[i];
+    std::string key((const char*)p, len);
+    if (!from_empty && t.lookup(p, len) != NONE) continue;
+    if (!seen_bytes.insert(key).second) continue;
+    const uint32_t id = ids[i];
+    if (id == NONE) continue;
+    if (id >= WID_MAX || (!from_empty && t.id_in_use(id)) || !seen_ids.insert(id).second) {
+      *why = "bad or duplicate filter id at index " + std::to_string(i);
+      return false;
+    }
+  }
   return true;
 }
 
@@ -534,6 +595,8 @@ void egm_close(egm_ctx* c) {
     drain_slot(c->slots[1]);
     if (c->patch_host) hipHostFree(c->patch_host);
     c->patch_host = nullptr;
+    if (c->work_ev) hipEventDestroy(c->work_ev);
+    c->work_ev = nullptr;
   }
   hipStreamDestroy(c->stream);
   delete c;
@@ -545,6 +608,8 @@ int egm_table_build(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32
   if (!c || (n && (!blob || !valid_offsets(off, n)))) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
+  std::string why;
+  if (!validate_inserts(c->table, blob, off, n, ids, true, &why)) return c->fail(EGM_E_INVAL, why);
   c->table.clear();
   for (uint32_t i = 0; i < n; ++i) {
     int r = c->table.insert(blob + off[i], off[i + 1] - off[i], ids ? ids[i] : i, nullptr);
@@ -559,6 +624,9 @@ int egm_table_apply_delta(egm_ctx* c, const egm_delta* ins, const egm_delta* del
   if (ins && ins->n && (!ins->blob || !valid_offsets(ins->offsets, ins->n))) return EGM_E_INVAL;
   if (del && del->n && (!del->blob || !valid_offsets(del->offsets, del->n))) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
+  std::string why;
+  if (ins && !validate_inserts(c->table, ins->blob, ins->offsets, ins->n, ins->ids, false, &why))
+    return c->fail(EGM_E_INVAL, why);   // nothing staged
   if (ins)
     for (uint32_t i = 0; i < ins->n; ++i) {
       int r = c->table.insert(ins->blob + ins->offsets[i], ins->offsets[i + 1] - ins->offsets[i],
@@ -827,6 +895,7 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
     evp[0] = c->take_event();
     evp[1] = c->take_event();
   }
+  c->work_begin(s);
   e = launch_fanout(st, d_mrow, d_mids, n, nids, d_drow, d_fid, d_sub, cap, c->f_dc.as<uint32_t>(),
                     c->f_ds0.as<uint64_t>(), c->f_dpos.as<uint64_t>(), c->f_tiles.as<uint64_t>(), c->f_ovf.as<unsigned int>(), s,
                     c->timing ? evp : nullptr);
@@ -834,6 +903,10 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
     c->ev_fan.push_back(evp[0]);
     c->ev_fan.push_back(evp[1]);
   }
+  c->work_end(s);
+  c->fan_drow = d_drow;
+  c->fan_topics = n;
+  c->fan_stream = s;
   if (e != hipSuccess) return c->hip_fail(e, "launch_fanout");
   if (total) {
     unsigned int ovf = 0;
@@ -925,9 +998,28 @@ int egm_shard_merge(egm_ctx* c, uint32_t n_shards, uint32_t n, const uint32_t* d
   if ((e = c->m_tot.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "merge tot");
   ShardIds src{};
   for (uint32_t k = 0; k < n_shards; ++k) src.ids[k] = d_shard_ids[k];
+  c->work_begin(s);
   e = launch_shard_merge(d_counts, n_shards, n, src, c->m_srow.as<uint64_t>(),
                          c->m_tiles.as<uint64_t>(), c->m_tot.as<uint32_t>(), d_row, d_ids, ids_cap, s);
+  c->work_end(s);
   if (e != hipSuccess) return c->hip_fail(e, "launch_shard_merge");
+  return EGM_OK;
+}
+
+int egm_last_fanout(egm_ctx* c, uint64_t* n_deliveries, uint32_t* overflow) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (!c->fan_drow) return c->fail(EGM_E_STATE, "no fan-out launched");
+  if (set_device(c)) return EGM_E_DEVICE;
+  uint64_t tot = 0;
+  unsigned int ovf = 0;
+  hipError_t e;
+  if ((e = hipStreamSynchronize(c->fan_stream)) != hipSuccess ||
+      (e = hipMemcpy(&tot, c->fan_drow + c->fan_topics, 8, hipMemcpyDeviceToHost)) != hipSuccess ||
+      (e = hipMemcpy(&ovf, c->f_ovf.p, 4, hipMemcpyDeviceToHost)) != hipSuccess)
+    return c->hip_fail(e, "fan-out readback");
+  if (n_deliveries) *n_deliveries = tot;
+  if (overflow) *overflow = ovf;
   return EGM_OK;
 }
 

@@ -61,7 +61,6 @@ struct MatchWork {                // per-batch device workspace
   uint32_t heavy_cap;             // items per heavy wave (>= deepest possible topic + 192)
   uint64_t* tile_sums;            // scan scratch
   MatchStats* stats;
-  MatchWork* self;                // device copy of this descriptor (written by k_setup)
   uint32_t debug;                 // DEBUG_* bits
 };
 

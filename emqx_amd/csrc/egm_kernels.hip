@@ -426,13 +426,14 @@ struct alignas(16) WaveLds {
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// The workspace pointers live in device memory (k_setup) and are re-read at
-// each rare use (chunk take, retire, flush) through a pointer the compiler
-// cannot see through: hoisted out of the loop they would pin ~30 SGPRs and
-// push the walk's wave-uniform state into VGPRs.
+// The workspace descriptor is k_walk's first kernel argument, so it sits at
+// offset 0 of the kernarg segment.  It is re-read at each rare use (chunk
+// take, retire, flush) through a pointer the compiler cannot see through:
+// hoisted out of the loop its fields would pin ~30 SGPRs and push the walk's
+// wave-uniform state into VGPRs.
 typedef const __attribute__((address_space(4))) MatchWork ConstWork;   // scalar (s_load) view
-__device__ __forceinline__ ConstWork* fresh(const MatchWork* p) {
-  uint64_t v = (uint64_t)p;
+__device__ __forceinline__ ConstWork* fresh() {
+  uint64_t v = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(v));
   return (ConstWork*)v;
 }
@@ -468,9 +469,8 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
 // present: {count, ids_tmp offset, offset inside the topic's CSR row, the
 // topic's previous piece} — a topic's pieces form a chain from head[t], so
 // the compaction gathers each topic's ids without scanning all pieces.
-__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t lane, const MatchWork* wk,
-                                            Slab& sid, Slab& spc) {
-  ConstWork& w = *fresh(wk);
+__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t lane, Slab& sid, Slab& spc) {
+  ConstWork& w = *fresh();
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {
     const uint32_t i = i0 + lane;
@@ -691,8 +691,8 @@ struct Half {
 // Fill half h with the next light chunk (chunks with a topic deeper than
 // LIGHT_DMAX, or all of them under DEBUG_FORCE_HEAVY, are deferred to k_heavy).
 __device__ __forceinline__ void take_chunk(WaveLds& L, Half& H, uint32_t h, const uint32_t* __restrict__ off,
-                                           uint32_t n, uint32_t nchunks, const MatchWork* wk, uint32_t lane) {
-  ConstWork& w = *fresh(wk);
+                                           uint32_t n, uint32_t nchunks, uint32_t lane) {
+  ConstWork& w = *fresh();
   for (;;) {
     uint32_t c = 0;
     if (lane == 0) c = atomicAdd(&w.stats->next_chunk, 1u);
@@ -721,8 +721,13 @@ __device__ __forceinline__ void take_chunk(WaveLds& L, Half& H, uint32_t h, cons
     const uint32_t s = h * WALK_CHUNK + lane;
     L.tinfo[s] = D | (f << 24);
     L.tbase[s] = base;
-    L.w0[s] = lane < nt ? w.wid[base] : WID_NONE;
-    L.cnt[s] = 0;
+    uint32_t w0 = WID_NONE, wl = 0;
+    if (lane < nt) {   // word 0, and a touch of the last word: the topic's word lines come into L2 for the walk's pops
+      w0 = w.wid[base];
+      wl = w.wid[base + D - 1];
+    }
+    L.w0[s] = w0;
+    L.cnt[s] = wl == 0xFFFFFFFEu ? 1u : 0u;   // 0: no word id is TOMB (the compare keeps the touch load alive)
     L.last[s] = NONE;
     L.fcnt[s] = 0;
     H.chunk = c;
@@ -742,17 +747,16 @@ __device__ __forceinline__ void take_chunk(WaveLds& L, Half& H, uint32_t h, cons
   if (HX.chunk != NONE && HX.adm == HX.nt && HX.live == 0) {                                           \
     const uint32_t t0 = HX.chunk * WALK_CHUNK;                                                         \
     if (lane < HX.nt) {                                                                                \
-      ConstWork& w = *fresh(wk);                                                                 \
+      ConstWork& w = *fresh();                                                                 \
       w.cnt[t0 + lane] = L.cnt[(hx) * WALK_CHUNK + lane];                                              \
       w.head[t0 + lane] = L.last[(hx) * WALK_CHUNK + lane];                                            \
     }                                                                                                  \
     wave_sync();                                                                                       \
-    take_chunk(L, HX, hx, off, n, nchunks, wk, lane);                                                   \
+    take_chunk(L, HX, hx, off, n, nchunks, lane);                                                   \
   }
 
-__global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __restrict__ wid,
-                                             const uint32_t* __restrict__ off, uint32_t n, int mode,
-                                             const MatchWork* wk) {
+__global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const uint32_t* __restrict__ wid,
+                                             const uint32_t* __restrict__ off, uint32_t n, int mode) {
   __shared__ WaveLds L;
   const uint32_t lane = threadIdx.x;
   const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
@@ -765,8 +769,8 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
   unsigned long long iters = 0, popped = 0, bounded = 0;
   Slab sid{0, 0}, spc{0, 0};
   Half A, B;   // slots 0..63 and 64..127
-  take_chunk(L, A, 0, off, n, nchunks, wk, lane);
-  take_chunk(L, B, 1, off, n, nchunks, wk, lane);
+  take_chunk(L, A, 0, off, n, nchunks, lane);
+  take_chunk(L, B, 1, off, n, nchunks, lane);
   uint32_t sp = 0, nstage = 0;
   bool admit_b = false;   // which half is being admitted
 
@@ -777,7 +781,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
       const bool ra = A.chunk != NONE && A.adm == A.nt && A.live == 0;
       const bool rb = B.chunk != NONE && B.adm == B.nt && B.live == 0;
       if (nstage && (ra || rb || nstage + 64u > WALK_STAGE)) {
-        flush_stage(L, nstage, lane, wk, sid, spc);
+        flush_stage(L, nstage, lane, sid, spc);
         nstage = 0;
       }
     }
@@ -887,7 +891,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
       const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
       if (nstage + ne > WALK_STAGE) {
         wave_sync();
-        flush_stage(L, nstage, lane, wk, sid, spc);
+        flush_stage(L, nstage, lane, sid, spc);
         nstage = 0;
       }
       const uint8_t st = (uint8_t)slot;
@@ -920,7 +924,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
   if (lane == 0) {
-    ConstWork& w = *fresh(wk);
+    ConstWork& w = *fresh();
     if (v) atomicAdd(&w.stats->visited, v);
     atomicAdd(&w.stats->iters, iters);
     atomicAdd(&w.stats->popped, popped);
@@ -1218,11 +1222,6 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint32_t* 
   }
 }
 
-// The walk's workspace descriptor, written to device memory in stream order.
-__global__ void k_setup(MatchWork w, MatchWork* out) {
-  if (threadIdx.x == 0) *out = w;
-}
-
 // ------------------------------------------------------------- launchers ----
 // The walk runs persistent waves (one per block) that take chunks from a
 // global counter: as many as the GPU holds at once, fewer for a small batch.
@@ -1270,9 +1269,8 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   hipLaunchKernelGGL(k_tokenise, dim3((n + TOK_BLOCK - 1) / TOK_BLOCK), dim3(TOK_BLOCK), 0, s, tab, blob,
                      off, n, w.wid, w.lv, w.tfl);
   if (ev_walk) hipEventRecord(ev_walk[0], s);
-  hipLaunchKernelGGL(k_setup, dim3(1), dim3(64), 0, s, w, w.self);
-  hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64), 0, s, tab, (const uint32_t*)w.wid, off, n, mode,
-                     (const MatchWork*)w.self);
+  hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64), 0, s, w, tab, (const uint32_t*)w.wid, off, n,
+                     mode);
   if (ev_walk) hipEventRecord(ev_walk[1], s);
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
   scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);

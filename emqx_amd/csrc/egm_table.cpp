@@ -324,6 +324,10 @@ uint32_t HostTable::lookup(const uint8_t* p, uint32_t len) const {
   return li == NONE ? NONE : ffid_[li];
 }
 
+bool HostTable::id_in_use(uint32_t fid) const {
+  return by_fid_.find(mix64(fid), [&](uint32_t x) { return falive_[x] && ffid_[x] == fid; }) != NONE;
+}
+
 const uint8_t* HostTable::filter_bytes(uint32_t fid, uint32_t* len) const {
   uint32_t li = by_fid_.find(mix64(fid), [&](uint32_t x) { return falive_[x] && ffid_[x] == fid; });
   if (li == NONE) return nullptr;

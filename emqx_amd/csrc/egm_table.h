@@ -69,6 +69,8 @@ class HostTable {
   uint32_t lookup(const uint8_t* p, uint32_t len) const;
   // bytes of a filter id (nullptr if unknown)
   const uint8_t* filter_bytes(uint32_t fid, uint32_t* len) const;
+  // whether a live filter holds this id
+  bool id_in_use(uint32_t fid) const;
 
   void relayout();          // BFS renumbering of nodes + edge table rebuild
   void clear();
@@ -94,6 +96,8 @@ class HostTable {
 
   // changes since the previous call (see DirtyLog)
   DirtyLog take_dirty();
+  // hand a taken log back (a commit that failed after taking it)
+  void restore_dirty(const DirtyLog& d) { dirty_.merge(d); }
   const DirtyLog& dirty() const { return dirty_; }
 
  private:

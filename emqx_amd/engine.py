@@ -159,9 +159,9 @@ class GpuMatcher:
         n = len(off) - 1
         res = C.POINTER(L.egm_result)()
         rc = self.lib.egm_match_batch(self.ctx, _ptr(blob), _ptr(off), n, mode, C.byref(res))
-        if rc == L.EGM_E_OVERFLOW and allow_error and res:
-            pass
-        else:
+        if rc != 0 and not (rc == L.EGM_E_OVERFLOW and allow_error and res):
+            if res:   # the library may hand back a result with an error: release it
+                self.lib.egm_result_free(res)
             self._check(rc, "egm_match_batch")
         try:
             r = res.contents
@@ -240,6 +240,12 @@ class GpuMatcher:
                       d_sub: int, cap: int):
         self._check(self.lib.egm_fanout_device(self.ctx, d_mrow, d_mids, mids_len, n, stream or None, d_drow,
                                                d_fid, d_sub, cap), "egm_fanout_device")
+
+    def last_fanout(self) -> dict:
+        """Delivery total of the last fan-out and whether its buffers were too small."""
+        tot, ovf = C.c_uint64(), C.c_uint32()
+        self._check(self.lib.egm_last_fanout(self.ctx, C.byref(tot), C.byref(ovf)), "egm_last_fanout")
+        return {"deliveries": tot.value, "overflow": ovf.value}
 
 
     # -- multi-GPU filter shards --------------------------------------------------

@@ -24,6 +24,12 @@
  * duration of the call; results are library-allocated and released with
  * egm_result_free().  One context = one HIP device; calls on a context are
  * serialised internally (a dirty-scheduler NIF may call from any thread).
+ * The device entry points may be given any HIP stream: launches that share
+ * the context's workspaces are ordered across streams by the library (a
+ * launch on a new stream waits for the previous one), and a table commit
+ * waits for every launch still reading the epoch it overwrites.
+ * Table changes are all-or-nothing: a delta or build with an invalid id
+ * leaves the staged table unchanged.
  */
 #ifndef EMQX_GPU_MATCH_H
 #define EMQX_GPU_MATCH_H
@@ -150,8 +156,11 @@ int egm_last_walk_counters(egm_ctx* ctx, uint64_t* iters, uint64_t* popped, uint
 /* Enable per-kernel timing with HIP events on the launch stream (0/1) and read
    the accumulated walk-kernel time (ms) and launch count. */
 int egm_set_timing(egm_ctx* ctx, int enable);
-/* Test hooks: bit 0 routes every chunk through the overflow (heavy) kernel. */
+/* Test hooks: bit 0 routes every chunk through the heavy kernel; bit 1 makes
+   the next table commit fail after it has taken the staged changes (they must
+   survive into the following commit). */
 #define EGM_DEBUG_FORCE_HEAVY 1u
+#define EGM_DEBUG_FAIL_COMMIT 2u
 int egm_set_debug(egm_ctx* ctx, uint32_t flags);
 int egm_get_timing(egm_ctx* ctx, double* walk_ms, uint64_t* walk_launches, double* fanout_ms,
                    uint64_t* fanout_launches);
@@ -166,6 +175,10 @@ int egm_fanout_batch(egm_ctx* ctx, const egm_result* matched, egm_delivery** out
 int egm_fanout_device(egm_ctx* ctx, const uint64_t* d_match_row, const uint32_t* d_match_ids,
                       uint64_t match_ids_len, uint32_t n_topics, void* hip_stream, uint64_t* d_deliv_row, uint32_t* d_fid,
                       uint32_t* d_sub, uint64_t deliv_cap);
+/* Synchronises the last fan-out and reports its delivery total and whether
+   deliv_cap was too small (overflow != 0: d_fid/d_sub were not written;
+   rerun with deliv_cap >= n_deliveries). */
+int egm_last_fanout(egm_ctx* ctx, uint64_t* n_deliveries, uint32_t* overflow);
 
 /* ---- multi-GPU filter sharding ----
    Merge the match results of one topic batch against n_shards disjoint filter

@@ -1,0 +1,173 @@
+"""Failure behaviour of the C-ABI and the heavy path's no-overflow
+guarantee, on the GPU.
+
+* a delta or build with an invalid id changes nothing (the reference's route
+  changes are all-or-nothing mnesia transactions, emqx_router.erl:252-303);
+* a commit that fails after taking the staged changes publishes them with the
+  next commit (EGM_DEBUG_FAIL_COMMIT);
+* device batches on different streams share the context's workspaces safely;
+* a fan-out into too small a buffer reports its overflow (egm_last_fanout);
+* no legal topic (<= 65 535 bytes, emqx_topic.erl:45, 99-100) overflows: a
+  7 000-level chain set and a 2^14-wide combination set, against the oracle.
+"""
+import numpy as np
+import pytest
+
+from emqx_amd import _lib as L
+from emqx_amd import synth
+from emqx_amd.engine import GpuMatcher
+from oracle import trie_ref as R
+from oracle.cpp import OracleTrie, canonical
+
+pytestmark = pytest.mark.gpu
+DEBUG_FAIL_COMMIT = 2
+
+
+@pytest.fixture(scope="module")
+def gm():
+    m = GpuMatcher(0)
+    yield m
+    m.close()
+
+
+def sets(res):
+    return [sorted(res.row(i).tolist()) for i in range(len(res.row_ptr) - 1)]
+
+
+def test_invalid_delta_changes_nothing(gm):
+    gm.build_strings([b"a/+", b"b/#"], ids=[10, 11])
+    topics = [b"a/x", b"b/y/z", b"c/d"]
+    before = sets(gm.match_strings(topics))
+    with pytest.raises(L.EgmError):   # id 10 is taken by a/+: the whole delta is refused
+        gm.apply(inserts=[b"c/+", b"d/+"], insert_ids=[12, 10], deletes=[b"a/+"])
+    with pytest.raises(L.EgmError):   # the same new id twice
+        gm.apply(inserts=[b"c/+", b"d/+"], insert_ids=[13, 13])
+    gm.commit()
+    assert sets(gm.match_strings(topics)) == before
+    assert gm.filter_id(b"c/+") is None
+    with pytest.raises(L.EgmError):   # a failed build leaves the old table
+        gm.build_strings([b"x/#", b"y/#"], ids=[1, 1])
+    assert sets(gm.match_strings(topics)) == before
+    gm.apply(inserts=[b"c/+"], insert_ids=[12])   # a valid delta still goes through
+    gm.commit()
+    assert sets(gm.match_strings(topics))[2] == [12]
+
+
+def test_failed_commit_keeps_its_changes(gm):
+    f, t = synth.config("c0", n_filters=6_000, n_topics=20_000)
+    fl = f.to_list()
+    gm.build(f.blob, f.off)
+    gm.apply(deletes=fl[:2000])
+    gm.set_debug(DEBUG_FAIL_COMMIT)
+    with pytest.raises(L.EgmError):
+        gm.commit()
+    gm.set_debug(0)
+    gm.apply(deletes=fl[2000:2500])
+    gm.commit()                      # publishes both deltas
+    res = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    o = OracleTrie(True, L.EGM_MODE_ROUTES)
+    o.add(f.blob, f.off)
+    from emqx_amd.engine import pack_strings
+    o.remove(*pack_strings(fl[:2500]))
+    row, ids = o.match(t.blob, t.off, threads=8)
+    assert np.array_equal(res.row_ptr, row)
+    assert np.array_equal(canonical(res.row_ptr, res.ids), canonical(row, ids))
+
+
+def test_batches_on_two_streams(gm):
+    import torch
+    f, t = synth.config("c0", n_topics=60_000)
+    gm.build(f.blob, f.off)
+    want = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    dev = torch.device("cuda:0")
+    d_blob = torch.from_numpy(t.blob).to(dev)
+    d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+    n, cap = t.n, len(want.ids) + 1024
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for s in (s1, s2, s1, s2):   # back to back on alternating streams, no host sync in between
+        r = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        i = torch.zeros(cap, dtype=torch.int32, device=dev)
+        gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES,
+                        s.cuda_stream, r.data_ptr(), i.data_ptr(), cap)
+        outs.append((s, r, i))
+    torch.cuda.synchronize()
+    for s, r, i in outs:
+        row = r.cpu().numpy().view(np.uint64)
+        ids = i.cpu().numpy().view(np.uint32)[: len(want.ids)]
+        assert np.array_equal(row, want.row_ptr)
+        assert np.array_equal(canonical(row, ids), canonical(want.row_ptr, want.ids))
+
+
+def test_fanout_overflow_is_reported(gm):
+    import torch
+    f, t = synth.config("c1", n_filters=20_000, n_topics=5_000)
+    gm.build(f.blob, f.off)
+    srow, subs = synth.subscribers(f.n, p_big=0.01, n_big=500, p_share=0.1)
+    gm.subs_build(srow, subs)
+    host = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    mrow = torch.from_numpy(host.row_ptr.view(np.int64)).to(dev)
+    mids = torch.from_numpy(host.ids.view(np.int32)).to(dev)
+    n = t.n
+    drow = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    fid = torch.zeros(100, dtype=torch.int32, device=dev)
+    sub = torch.zeros(100, dtype=torch.int32, device=dev)
+    gm.fanout_device(mrow.data_ptr(), mids.data_ptr(), len(host.ids), n, s, drow.data_ptr(), fid.data_ptr(),
+                     sub.data_ptr(), 100)
+    st = gm.last_fanout()
+    total = int(sum(int(srow[x + 1] - srow[x]) for x in host.ids.tolist()))
+    assert st["deliveries"] == total > 100 and st["overflow"] == 1
+    fid = torch.zeros(total, dtype=torch.int32, device=dev)
+    sub = torch.zeros(total, dtype=torch.int32, device=dev)
+    gm.fanout_device(mrow.data_ptr(), mids.data_ptr(), len(host.ids), n, s, drow.data_ptr(), fid.data_ptr(),
+                     sub.data_ptr(), total)
+    assert gm.last_fanout() == {"deliveries": total, "overflow": 0}
+
+
+def test_no_overflow_7000_level_chains(gm):
+    """Topics of 7 000 levels (far deeper than the LDS walk takes: k_heavy with
+    its HBM stack) against filter chains that keep a literal and a '+'
+    alternative pending at every level, plus the long-topic edge of 65 535
+    bytes."""
+    D = 7000
+    deep = [b"l%d" % (i % 7) for i in range(D)]
+    filters = [b"/".join(deep), b"/".join(deep[:-1]) + b"/+", b"/".join([b"+"] * D),
+               b"/".join(b"+" if i % 2 else deep[i] for i in range(D)),
+               b"/".join(deep[:3500]) + b"/#", b"#", b"l0/#"]
+    topics = [b"/".join(deep), b"/".join(deep[:-1]) + b"/zz", b"/".join(deep[:3500]), b"x" * 65_535,
+              b"/" * 65_534, b"l0/l1"]
+    gm.build_strings(filters)
+    for mode in (L.EGM_MODE_TRIE, L.EGM_MODE_ROUTES):
+        res = gm.match_strings(topics, mode)
+        assert res.n_error == 0
+        for i, tp in enumerate(topics):
+            want = R.trie_semantics(tp, filters) if mode == 0 else R.routes_semantics(tp, filters)
+            got = sorted(filters[x] for x in res.row(i).tolist())
+            assert got == sorted(want), (mode, i)
+
+
+def test_no_overflow_2_14_wide_frontier(gm):
+    """Every filter of depth 14 over {'+', 'k<l>'}: the matching topic's
+    frontier holds 2^14 states; the light walk narrows to depth-first instead
+    of overflowing, and the heavy path (forced) agrees."""
+    D = 14
+    filters = [b"/".join(b"+" if (m >> l) & 1 else b"k%d" % l for l in range(D)) for m in range(1 << D)]
+    filters += [b"#"]
+    gm.build_strings(filters)
+    topics = [b"/".join(b"k%d" % l for l in range(D)), b"/".join(b"k%d" % l for l in range(D - 1)) + b"/q"] + \
+        [b"k0/zz"] * 100
+    res = gm.match_strings(topics, L.EGM_MODE_TRIE)
+    assert res.n_error == 0
+    got = sets(res)
+    assert len(got[0]) == (1 << D) - 1 + 1   # all but the all-literal filter, + '#'
+    assert len(got[1]) == (1 << (D - 1)) + 1  # last level must be '+', + '#'
+    gm.set_debug(1)
+    try:
+        hv = gm.match_strings(topics, L.EGM_MODE_TRIE)
+    finally:
+        gm.set_debug(0)
+    assert hv.n_error == 0 and sets(hv) == got
+    for i in (0, 1):
+        assert sorted(filters[x] for x in got[i]) == sorted(R.trie_semantics(topics[i], filters))

@@ -13,6 +13,7 @@
 #   sq         SQ wait/active counters + TCC hit/miss over the C2 bench
 #   host       host-visible path (egm_match_batch, pinned staging) bench
 #   smoke      __graft_entry__.smoke()
+#   ab_V       the C2 bench on variant V (emqx_amd/libemqx_gpu_match_V.so, tools/build_variant.py)
 # An ordinary failure (exit 1..5) moves on; a fault, abort or timeout ends the job.
 set -u
 TAG=$1; shift
@@ -53,6 +54,9 @@ for step in "$@"; do
       run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off ;;
     host) run host 600 python tools/bench_host.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    ab_*)   # A/B variant built by tools/build_variant.py: C2 bench under rocprof stats
+      v=${step#ab_}
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$v" -o run --output-format csv -- $B --steps 10 --warmup 2 --cpu-baseline off ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
