@@ -26,7 +26,8 @@ struct MatchStats {               // device-side counters, zeroed per batch
   unsigned long long total_ids;   // matched ids in the batch (= row_ptr[n])
   unsigned int n_deferred;        // chunks handed to the heavy kernel
   unsigned int heavy_next;        // heavy work counter
-  unsigned int overflow;          // bit 0: ids_tmp/pieces full, bit 1: output ids full
+  unsigned int overflow;          // bit 0: ids_tmp/pieces full, bit 1: output ids full, bit 2: heavy stack,
+                                  // bit 3: a loop guard fired (a bug: reported, never a hung GPU)
   unsigned int errors;            // topics the heavy kernel could not walk (never for legal topics)
   unsigned long long iters;       // walk iterations (instrumentation)
   unsigned long long popped;      // items popped by the walk (lane occupancy = popped / (iters * 64))

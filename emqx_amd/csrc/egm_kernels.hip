@@ -18,6 +18,9 @@
 // This is pointer chasing over hashed edges — HBM / latency bound; no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "egm_kernels.h"
@@ -424,7 +427,12 @@ struct alignas(16) WaveLds {
   uint16_t fcnt[SLOTS];            // ids in the current stage / start inside the flush
 };
 
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+// readfirstlane returns int: widen each half as unsigned (a sign-extended low
+// half would set the high word of a pointer whose bit 31 is set)
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | (uint64_t)uni((uint32_t)v);
+}
 
 // The workspace descriptor is k_walk's first kernel argument, so it sits at
 // offset 0 of the kernarg segment.  It is re-read at each rare use (chunk
@@ -435,7 +443,10 @@ typedef const __attribute__((address_space(4))) MatchWork ConstWork;   // scalar
 __device__ __forceinline__ ConstWork* fresh() {
   uint64_t v = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(v));
-  return (ConstWork*)v;
+  // an asm result counts as divergent: without readfirstlane every value read
+  // through it, and the whole loop's control flow, would be treated as
+  // per-lane (exec-masked branches, uniform state in VGPRs)
+  return (ConstWork*)uni64(v);
 }
 
 // Per-wave output slab (uniform across the wave).
@@ -452,8 +463,7 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
     unsigned long long b = 0;
     if (lane == 0) b = atomicAdd(counter, sz);
     b = __shfl(b, 0, 64);
-    b = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
-        __builtin_amdgcn_readfirstlane((uint32_t)b);   // wave-uniform: keep it in SGPRs
+    b = uni64(b);   // wave-uniform: keep it in SGPRs
     s.cur = b;
     s.end = b + sz;
   }
@@ -579,7 +589,11 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* __res
   p.h1 = ld16(bp + 48);
   // the next level's word (clamped; used only if level + 1 < D)
   const uint32_t level = meta & LEVEL_MAX;
+#ifdef EGM_AB_FAKE_NW   // A/B only (wrong results): the cost of the next-word reads
+  p.nw = p.it.w ^ level;
+#else
   p.nw = wid[p.act ? tbase + min(level + 1, p.D - 1) : 0u];
+#endif
 }
 
 // Children and emits of one popped item.
@@ -769,12 +783,21 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
   unsigned long long iters = 0, popped = 0, bounded = 0;
   Slab sid{0, 0}, spc{0, 0};
   Half A, B;   // slots 0..63 and 64..127
+  // a flush reads the stage counts of all 128 slots: a half that never gets a
+  // chunk must read zeros
+  L.fcnt[lane] = 0;
+  L.fcnt[lane + WALK_CHUNK] = 0;
   take_chunk(L, A, 0, off, n, nchunks, lane);
   take_chunk(L, B, 1, off, n, nchunks, lane);
   uint32_t sp = 0, nstage = 0;
   bool admit_b = false;   // which half is being admitted
 
+  uint32_t guard = 0;   // every loop of the kernel is bounded: a bug reports, it never hangs the GPU
   for (;;) {
+    if (++guard > (1u << 22)) {
+      if (lane == 0) atomicOr(&fresh()->stats->overflow, 8u);
+      break;
+    }
     // ---- the one flush point of the loop top: before a retire, or when an
     // admission's 64 root emits might not fit ----
     {
@@ -941,8 +964,16 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
 // 99-100) can overflow it.  Two passes: count, then fill at a reserved offset
 // (one piece per topic).
 __device__ __forceinline__ void heavy_fence() {
-  // the wave's own stack stores must be visible to its next loads of them
+  // the wave's own stack stores must have reached L2 before its next loads of them
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+
+// Stack reads bypass the CU's L1 (a nontemporal load is served by L2): the
+// L1 may still hold a line of the stack from before the wave's own stores to it.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16_l2(const uint4* p) {
+  const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
 }
 
 __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __restrict__ off, uint32_t n, int mode,
@@ -1015,13 +1046,18 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
       }
       if (pass == 0 && lane == 0) created += 1;
       heavy_fence();
+      uint32_t guard = 0;
       while (sp) {
+        if (++guard > (1u << 22)) {
+          if (lane == 0) atomicOr(&w.stats->overflow, 8u);
+          break;
+        }
         const uint32_t room = cap - sp;
         const uint32_t lim = room > D ? room - D : 1u;
         const uint32_t take = min(min(64u, sp), lim), bi = sp - take;
         Pend p;
         p.act = lane < take;
-        p.it = stk[p.act ? bi + lane : 0u];
+        p.it = ld16_l2(stk + (p.act ? bi + lane : 0u));
         p.D = D;
         p.d1 = D == 1 && (tf & TF_DOLLAR);
         issue(tab, w.wid, tb, p);
@@ -1189,7 +1225,12 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint32_t* 
     const uint32_t t = win * 64 + lane;
     uint32_t p = t < n ? head[t] : NONE;
     const uint64_t rs = row_ptr[min(t, n)];
+    uint32_t guard = 0;
     while (__ballot(p != NONE)) {
+      if (++guard > (1u << 22)) {
+        if (lane == 0) atomicOr(&stats->overflow, 8u);
+        break;
+      }
       const uint4 pc = pieces[p != NONE ? p : 0u];   // unconditional (a load under a branch is waited for at once)
       const uint32_t c = p != NONE ? pc.x : 0u;
       uint32_t tot;
@@ -1258,6 +1299,23 @@ static void scan_counts(const uint32_t* cnt, uint32_t n, uint64_t* tile_sums, ui
                      copy);
 }
 
+// EGM_TRACE_KERNELS=1: synchronise after every kernel of a batch and name it
+// on stderr (diagnostics: which kernel of a batch does not return).
+static bool trace_kernels() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("EGM_TRACE_KERNELS");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+static void trace(hipStream_t s, const char* what) {
+  if (!trace_kernels()) return;
+  fprintf(stderr, "[egm] %s ...", what);
+  const hipError_t e = hipStreamSynchronize(s);
+  fprintf(stderr, " %s\n", hipGetErrorString(e));
+}
+
 hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n,
                         int mode, const MatchWork& w, const MatchOut& out, hipStream_t s,
                         hipEvent_t* ev_walk) {
@@ -1268,16 +1326,21 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   }
   hipLaunchKernelGGL(k_tokenise, dim3((n + TOK_BLOCK - 1) / TOK_BLOCK), dim3(TOK_BLOCK), 0, s, tab, blob,
                      off, n, w.wid, w.lv, w.tfl);
+  trace(s, "k_tokenise");
   if (ev_walk) hipEventRecord(ev_walk[0], s);
   hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64), 0, s, w, tab, (const uint32_t*)w.wid, off, n,
                      mode);
   if (ev_walk) hipEventRecord(ev_walk[1], s);
+  trace(s, "k_walk");
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
+  trace(s, "k_heavy");
   scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);
+  trace(s, "scan");
   const uint32_t nwin = (n + 63) / 64;
   const uint32_t cblocks = std::min<uint32_t>(65536, (nwin + COMPACT_WAVES - 1) / COMPACT_WAVES);
   hipLaunchKernelGGL(k_compact, dim3(cblocks ? cblocks : 1), dim3(64 * COMPACT_WAVES), 0, s, w.head, w.pieces,
                      w.ids_tmp, n, out.row_ptr, out.ids, out.ids_cap, w.stats);
+  trace(s, "k_compact");
   return hipGetLastError();
 }
 
