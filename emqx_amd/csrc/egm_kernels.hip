@@ -396,6 +396,9 @@ constexpr uint32_t MT_SHIFT = 17;
 constexpr uint32_t MF_SHIFT = 24;
 constexpr uint32_t MW_SHIFT = 28;
 constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
+#ifndef EGM_GUARD_BITS
+#define EGM_GUARD_BITS 22   // loop guards: iterations a wave may spend in one loop before reporting a bug
+#endif
 
 #ifndef EGM_WALK_STACK
 #define EGM_WALK_STACK 240   // items (16 B) per wave
@@ -707,15 +710,16 @@ struct Half {
 __device__ __forceinline__ void take_chunk(WaveLds& L, Half& H, uint32_t h, const uint32_t* __restrict__ off,
                                            uint32_t n, uint32_t nchunks, uint32_t lane) {
   ConstWork& w = *fresh();
-  for (;;) {
+  // Straight-line loop with wave-uniform flags only (no return/continue from
+  // inside lane-conditional code: that pattern made the structurizer give
+  // the lanes different exits and the wave a chunk per lane).
+  bool taken = false;
+  uint32_t guard = 0;
+  while (!taken && ++guard < (1u << EGM_GUARD_BITS)) {
     uint32_t c = 0;
     if (lane == 0) c = atomicAdd(&w.stats->next_chunk, 1u);
     c = uni(__shfl(c, 0, 64));
-    if (c >= nchunks) {
-      H.chunk = NONE;
-      H.nt = H.adm = H.live = H.dm = 0;
-      return;
-    }
+    if (c >= nchunks) break;
     const uint32_t t0 = c * WALK_CHUNK;
     const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
     uint32_t D = 0, f = 0, base = 0;
@@ -728,30 +732,39 @@ __device__ __forceinline__ void take_chunk(WaveLds& L, Half& H, uint32_t h, cons
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, d, 64));
     dmax = uni(dmax);
-    if (dmax > LIGHT_DMAX || (w.debug & DEBUG_FORCE_HEAVY)) {
-      if (lane == 0) w.deferred[atomicAdd(&w.stats->n_deferred, 1u)] = c;
-      continue;
+    const bool heavy = dmax > LIGHT_DMAX || (uni(w.debug) & DEBUG_FORCE_HEAVY);
+    if (heavy) {   // deferred to k_heavy
+      uint32_t d = 0;
+      if (lane == 0) d = atomicAdd(&w.stats->n_deferred, 1u);
+      d = uni(__shfl(d, 0, 64));
+      if (lane == 0) w.deferred[d] = c;
+    } else {
+      const uint32_t s = h * WALK_CHUNK + lane;
+      uint32_t w0 = WID_NONE, wl = 0;
+      if (lane < nt) {   // word 0, and a touch of the last word: the topic's word lines come into L2 for the pops
+        w0 = w.wid[base];
+        wl = w.wid[base + D - 1];
+      }
+      L.tinfo[s] = D | (f << 24);
+      L.tbase[s] = base;
+      L.w0[s] = w0;
+      L.cnt[s] = wl == 0xFFFFFFFEu ? 1u : 0u;   // 0: no word id is TOMB (the compare keeps the touch load alive)
+      L.last[s] = NONE;
+      L.fcnt[s] = 0;
+      H.chunk = c;
+      H.nt = nt;
+      H.dm = dmax;
+      taken = true;
     }
-    const uint32_t s = h * WALK_CHUNK + lane;
-    L.tinfo[s] = D | (f << 24);
-    L.tbase[s] = base;
-    uint32_t w0 = WID_NONE, wl = 0;
-    if (lane < nt) {   // word 0, and a touch of the last word: the topic's word lines come into L2 for the walk's pops
-      w0 = w.wid[base];
-      wl = w.wid[base + D - 1];
-    }
-    L.w0[s] = w0;
-    L.cnt[s] = wl == 0xFFFFFFFEu ? 1u : 0u;   // 0: no word id is TOMB (the compare keeps the touch load alive)
-    L.last[s] = NONE;
-    L.fcnt[s] = 0;
-    H.chunk = c;
-    H.nt = nt;
-    H.adm = 0;
-    H.live = 0;
-    H.dm = dmax;
-    wave_sync();
-    return;
   }
+  if (!taken) {
+    H.chunk = NONE;
+    H.nt = 0;
+    H.dm = 0;
+  }
+  H.adm = 0;
+  H.live = 0;
+  wave_sync();
 }
 
 // Retire half hx once all its topics are admitted and its last item is done
@@ -794,7 +807,7 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
 
   uint32_t guard = 0;   // every loop of the kernel is bounded: a bug reports, it never hangs the GPU
   for (;;) {
-    if (++guard > (1u << 22)) {
+    if (++guard > (1u << EGM_GUARD_BITS)) {
       if (lane == 0) atomicOr(&fresh()->stats->overflow, 8u);
       break;
     }
@@ -1048,7 +1061,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
       heavy_fence();
       uint32_t guard = 0;
       while (sp) {
-        if (++guard > (1u << 22)) {
+        if (++guard > (1u << EGM_GUARD_BITS)) {
           if (lane == 0) atomicOr(&w.stats->overflow, 8u);
           break;
         }
@@ -1227,7 +1240,7 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint32_t* 
     const uint64_t rs = row_ptr[min(t, n)];
     uint32_t guard = 0;
     while (__ballot(p != NONE)) {
-      if (++guard > (1u << 22)) {
+      if (++guard > (1u << EGM_GUARD_BITS)) {
         if (lane == 0) atomicOr(&stats->overflow, 8u);
         break;
       }

@@ -22,6 +22,6 @@ for mode in (0, 1):
                      allow_error=True) if False else None
         try:
             r = gm.match_strings(ts, mode)
-            print("  ok", time.time() - t0, r.row_ptr[-1], gm.last_stats(), flush=True)
+            print("  ok", time.time() - t0, r.row_ptr[-1], gm.last_stats(), gm.walk_counters(), flush=True)
         except Exception as e:  # noqa: BLE001
             print("  error", e, gm.last_stats(), flush=True)
