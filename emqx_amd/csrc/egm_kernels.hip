@@ -401,19 +401,25 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #endif
 
 #ifndef EGM_WALK_STACK
-#define EGM_WALK_STACK 240   // items (16 B) per wave
+#define EGM_WALK_STACK 216   // items (16 B) per wave
 #endif
+#ifndef EGM_WALK_WPS
+#define EGM_WALK_WPS 8       // words per topic staged in LDS (deeper levels are read from HBM)
+#endif
+constexpr uint32_t WPS = EGM_WALK_WPS;
 #ifndef EGM_WALK_STAGE
 #define EGM_WALK_STAGE 256   // staged emits per flush (6 B each; >= 4 emits x 64 lanes)
 #endif
 constexpr uint32_t WALK_STACK = EGM_WALK_STACK;
 constexpr uint32_t WALK_STAGE = EGM_WALK_STAGE;
 constexpr uint32_t SLOTS = 2 * WALK_CHUNK;           // two chunks in flight per wave
+constexpr uint32_t SLOT_BITS = 6;
 // The pop bound below keeps room >= dmax after every iteration and a refill
 // fills the stack to at most 64 items, so the stack cannot overflow while
 // 64 + dmax <= WALK_STACK.  Chunks with a deeper topic go to k_heavy.
 constexpr uint32_t LIGHT_DMAX = WALK_STACK - 64;
-static_assert(WALK_CHUNK == 64, "lane j loads topic j of a chunk");
+static_assert(SLOTS == 64 && (1u << SLOT_BITS) == SLOTS, "one slot per lane");
+static_assert(WPS % 2 == 0 && WPS >= 2, "two lanes stage a topic's words");
 static_assert(WALK_STAGE >= 256 && WALK_STAGE <= 256, "stage: 4 emits x 64 lanes per step; u8 ranks and starts");
 static_assert(LIGHT_DMAX >= 16, "stack too small");
 
@@ -424,10 +430,10 @@ struct alignas(16) WaveLds {
   uint8_t stage_rank[WALK_STAGE];  // rank within its slot in this flush
   uint32_t tinfo[SLOTS];           // D | tflags << 24
   uint32_t tbase[SLOTS];           // wid index of the topic's word 0
-  uint32_t w0[SLOTS];              // the topic's word 0
   uint32_t cnt[SLOTS];             // ids flushed so far
   uint32_t last[SLOTS];            // the topic's last piece (NONE: none)
   uint16_t fcnt[SLOTS];            // ids in the current stage / start inside the flush
+  uint32_t words[SLOTS * WPS];     // the topic's first WPS word ids
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
@@ -491,7 +497,7 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
     const uint32_t tt = act ? L.stage_t[i] : 0u;
     uint64_t m = __ballot(act);
 #pragma unroll
-    for (uint32_t b = 0; b < 7; ++b) {
+    for (uint32_t b = 0; b < SLOT_BITS; ++b) {
       const bool bit = (tt >> b) & 1u;
       const uint64_t bb = __ballot(bit);
       m &= bit ? bb : ~bb;
@@ -506,33 +512,21 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
     if (act) L.stage_rank[i] = (uint8_t)(old + mbcnt(m));
   }
   wave_sync();
-  uint32_t fl[2];
-  uint32_t s = 0, np = 0;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    fl[k] = L.fcnt[lane * 2 + k];   // consecutive slots per lane
-    s += fl[k];
-    np += fl[k] ? 1u : 0u;
-  }
+  const uint32_t fl = L.fcnt[lane];   // slot = lane
   uint32_t tot, ptot;
-  uint32_t ex = wave_excl_scan(s, lane, &tot);
-  uint32_t pex = wave_excl_scan(np, lane, &ptot);
+  const uint32_t ex = wave_excl_scan(fl, lane, &tot);
+  const uint32_t pex = wave_excl_scan(fl ? 1u : 0u, lane, &ptot);
   const unsigned long long base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane);
   const unsigned long long pbase = slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane);
   const bool ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
   if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const uint32_t j = lane * 2 + k;
-    if (fl[k] && ok) {
-      const uint32_t p = (uint32_t)(pbase + pex++);
-      w.pieces[p] = make_uint4(fl[k], (uint32_t)(base + ex), L.cnt[j], L.last[j]);
-      L.last[j] = p;
-    }
-    L.fcnt[j] = (uint16_t)ex;   // the slot's start inside this flush
-    L.cnt[j] += fl[k];
-    ex += fl[k];
+  if (fl && ok) {
+    const uint32_t p = (uint32_t)(pbase + pex);
+    w.pieces[p] = make_uint4(fl, (uint32_t)(base + ex), L.cnt[lane], L.last[lane]);
+    L.last[lane] = p;
   }
+  L.fcnt[lane] = (uint16_t)ex;   // the slot's start inside this flush
+  L.cnt[lane] += fl;
   wave_sync();
   if (ok) {
     uint32_t* dst = w.ids_tmp + base;
@@ -540,8 +534,7 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
     for (uint32_t i = lane; i < nstage; i += 64) dst[L.fcnt[L.stage_t[i]] + L.stage_rank[i]] = L.stage_fid[i];
   }
   wave_sync();
-#pragma unroll
-  for (int k = 0; k < 2; ++k) L.fcnt[lane * 2 + k] = 0;
+  L.fcnt[lane] = 0;
   wave_sync();
 }
 
@@ -578,7 +571,7 @@ struct Pend {
 // load inside an `if` makes LLVM merge its result at the end of the block,
 // and the copy it inserts there waits for the load.
 __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* __restrict__ wid, uint32_t tbase,
-                                      Pend& p) {
+                                      const uint32_t* wlds, Pend& p) {
   const uint32_t meta = p.it.y;
   const uint32_t fl = (meta >> MF_SHIFT) & 0xFu;
   p.plus = p.act && (fl & F_PLUS);
@@ -592,11 +585,13 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* __res
   p.h1 = ld16(bp + 48);
   // the next level's word (clamped; used only if level + 1 < D)
   const uint32_t level = meta & LEVEL_MAX;
-#ifdef EGM_AB_FAKE_NW   // A/B only (wrong results): the cost of the next-word reads
-  p.nw = p.it.w ^ level;
-#else
-  p.nw = wid[p.act ? tbase + min(level + 1, p.D - 1) : 0u];
-#endif
+  // from the LDS stage for the first WPS levels, else from HBM (deep topics;
+  // the other lanes read word 0, one hot line)
+  const uint32_t nl = min(level + 1, p.D - 1);
+  const bool far = p.act && nl >= WPS;
+  const uint32_t wg = wid[far ? tbase + nl : 0u];
+  const uint32_t wl = wlds ? wlds[min(nl, WPS - 1)] : 0u;
+  p.nw = (far || !wlds) ? wg : wl;
 }
 
 // Children and emits of one popped item.
@@ -739,18 +734,24 @@ __device__ __forceinline__ void take_chunk(WaveLds& L, Half& H, uint32_t h, cons
       d = uni(__shfl(d, 0, 64));
       if (lane == 0) w.deferred[d] = c;
     } else {
-      const uint32_t s = h * WALK_CHUNK + lane;
-      uint32_t w0 = WID_NONE, wl = 0;
-      if (lane < nt) {   // word 0, and a touch of the last word: the topic's word lines come into L2 for the pops
-        w0 = w.wid[base];
-        wl = w.wid[base + D - 1];
+      if (lane < nt) {
+        const uint32_t s = h * WALK_CHUNK + lane;
+        L.tinfo[s] = D | (f << 24);
+        L.tbase[s] = base;
+        L.cnt[s] = 0;
+        L.last[s] = NONE;
       }
-      L.tinfo[s] = D | (f << 24);
-      L.tbase[s] = base;
-      L.w0[s] = w0;
-      L.cnt[s] = wl == 0xFFFFFFFEu ? 1u : 0u;   // 0: no word id is TOMB (the compare keeps the touch load alive)
-      L.last[s] = NONE;
-      L.fcnt[s] = 0;
+      // the first WPS words of each topic: two lanes per topic, WPS / 2 words each
+      const uint32_t jt = lane >> 1, part = lane & 1;
+      const uint32_t Dt = (uint32_t)__shfl(D, (int)jt, 64), bt = (uint32_t)__shfl(base, (int)jt, 64);
+      uint32_t wv[WPS / 2];
+#pragma unroll
+      for (uint32_t r = 0; r < WPS / 2; ++r) {
+        const uint32_t l = part * (WPS / 2) + r;
+        wv[r] = w.wid[(jt < nt && l < Dt) ? bt + l : 0u];
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < WPS / 2; ++r) L.words[(h * WALK_CHUNK + jt) * WPS + part * (WPS / 2) + r] = wv[r];
       H.chunk = c;
       H.nt = nt;
       H.dm = dmax;
@@ -798,8 +799,7 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
   Half A, B;   // slots 0..63 and 64..127
   // a flush reads the stage counts of all 128 slots: a half that never gets a
   // chunk must read zeros
-  L.fcnt[lane] = 0;
-  L.fcnt[lane + WALK_CHUNK] = 0;
+  L.fcnt[lane] = 0;   // slot = lane
   take_chunk(L, A, 0, off, n, nchunks, lane);
   take_chunk(L, B, 1, off, n, nchunks, lane);
   uint32_t sp = 0, nstage = 0;
@@ -847,7 +847,7 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
             em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
             fid = root.y;
             created += 1;
-            const uint32_t w0 = L.w0[s];
+            const uint32_t w0 = L.words[s * WPS];
             const uint32_t fl = root_flags(root, dollar, w0);
             has = fl != 0;
             it = make_uint4(0, (s << MT_SHIFT) | (fl << MF_SHIFT), root.x, w0);
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
     const uint32_t ti = L.tinfo[slot];
     p.D = ti & 0xFFFFFFu;
     p.d1 = p.D == 1 && ((ti >> 24) & TF_DOLLAR);
-    issue(tab, wid, L.tbase[slot], p);
+    issue(tab, wid, L.tbase[slot], L.words + slot * WPS, p);
     {
       const uint32_t n1 = popc(__ballot(p.act && slot >= WALK_CHUNK));
       B.live -= n1;
@@ -1073,7 +1073,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
         p.it = ld16_l2(stk + (p.act ? bi + lane : 0u));
         p.D = D;
         p.d1 = D == 1 && (tf & TF_DOLLAR);
-        issue(tab, w.wid, tb, p);
+        issue(tab, w.wid, tb, nullptr, p);
         sp = bi;
         Out o;
         finish(tab, mode, p, o);
