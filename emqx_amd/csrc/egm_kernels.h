@@ -75,7 +75,7 @@ struct MatchOut {                 // CSR result (device)
 
 // launch sizing shared with the host (egm_capi.cpp)
 #ifndef EGM_WALK_CHUNK
-#define EGM_WALK_CHUNK 32   // topics per walk chunk (a wave holds two)
+#define EGM_WALK_CHUNK 64   // topics per chunk taken by a walk wave (and deferred to k_heavy)
 #endif
 constexpr int WALK_CHUNK = EGM_WALK_CHUNK;
 int walk_grid_blocks(uint32_t n_topics);

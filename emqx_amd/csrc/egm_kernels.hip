@@ -401,7 +401,7 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #endif
 
 #ifndef EGM_WALK_STACK
-#define EGM_WALK_STACK 216   // items (16 B) per wave
+#define EGM_WALK_STACK 176   // items (16 B) per wave
 #endif
 #ifndef EGM_WALK_WPS
 #define EGM_WALK_WPS 8       // words per topic staged in LDS (deeper levels are read from HBM)
@@ -412,14 +412,13 @@ constexpr uint32_t WPS = EGM_WALK_WPS;
 #endif
 constexpr uint32_t WALK_STACK = EGM_WALK_STACK;
 constexpr uint32_t WALK_STAGE = EGM_WALK_STAGE;
-constexpr uint32_t SLOTS = 2 * WALK_CHUNK;           // two chunks in flight per wave
+constexpr uint32_t SLOTS = 64;                       // topics in flight per wave (slot = lane)
 constexpr uint32_t SLOT_BITS = 6;
 // The pop bound below keeps room >= dmax after every iteration and a refill
 // fills the stack to at most 64 items, so the stack cannot overflow while
 // 64 + dmax <= WALK_STACK.  Chunks with a deeper topic go to k_heavy.
 constexpr uint32_t LIGHT_DMAX = WALK_STACK - 64;
-static_assert(SLOTS == 64 && (1u << SLOT_BITS) == SLOTS, "one slot per lane");
-static_assert(WPS % 2 == 0 && WPS >= 2, "two lanes stage a topic's words");
+static_assert(SLOTS == 64 && (1u << SLOT_BITS) == SLOTS && WALK_CHUNK == 64, "one slot, one prefetched topic per lane");
 static_assert(WALK_STAGE >= 256 && WALK_STAGE <= 256, "stage: 4 emits x 64 lanes per step; u8 ranks and starts");
 static_assert(LIGHT_DMAX >= 16, "stack too small");
 
@@ -434,6 +433,9 @@ struct alignas(16) WaveLds {
   uint32_t last[SLOTS];            // the topic's last piece (NONE: none)
   uint16_t fcnt[SLOTS];            // ids in the current stage / start inside the flush
   uint32_t words[SLOTS * WPS];     // the topic's first WPS word ids
+  uint32_t live[SLOTS];            // the topic's items in the stack (or being expanded)
+  uint32_t tid[SLOTS];             // the topic's index in the batch
+  uint32_t finmask[2];             // slots whose topic finished this iteration
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
@@ -588,10 +590,10 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* __res
   // from the LDS stage for the first WPS levels, else from HBM (deep topics;
   // the other lanes read word 0, one hot line)
   const uint32_t nl = min(level + 1, p.D - 1);
-  const bool far = p.act && nl >= WPS;
+  const bool far = p.act && (nl >= WPS || !wlds);   // k_heavy stages no words
   const uint32_t wg = wid[far ? tbase + nl : 0u];
   const uint32_t wl = wlds ? wlds[min(nl, WPS - 1)] : 0u;
-  p.nw = (far || !wlds) ? wg : wl;
+  p.nw = far ? wg : wl;
 }
 
 // Children and emits of one popped item.
@@ -690,27 +692,25 @@ __device__ __forceinline__ uint32_t root_flags(uint4 root, bool dollar, uint32_t
   return (dollar ? 0u : (root.w & F_PLUS)) | ((root.w & s0) ? (root.w & F_LIT) : 0u);
 }
 
-// Wave-uniform bookkeeping of one of the two chunks in flight (two named
-// instances, never an array indexed at run time: that would live in scratch).
-struct Half {
-  uint32_t chunk;   // chunk id, NONE = empty
-  uint32_t nt;      // topics in the chunk
-  uint32_t adm;     // topics admitted so far
-  uint32_t live;    // items of the chunk in the stack
-  uint32_t dm;      // deepest topic of the chunk
+// The next topics of a wave, prefetched into registers: lane j (< nt) holds
+// topic t0 + j's depth, flags, wid base and first WPS words.  Chunks come from
+// a global counter; a chunk with a topic deeper than LIGHT_DMAX (or every
+// chunk under DEBUG_FORCE_HEAVY) is deferred to k_heavy.  Straight-line loop
+// with wave-uniform flags only (a return from lane-conditional code inside
+// such a loop made the structurizer give the lanes different exits).
+struct Prefetch {
+  uint32_t t0, nt, next;    // wave-uniform: first topic, topics, next to admit
+  uint32_t D, f, base;      // lane j: topic t0 + j
+  uint32_t wv[WPS];
 };
 
-// Fill half h with the next light chunk (chunks with a topic deeper than
-// LIGHT_DMAX, or all of them under DEBUG_FORCE_HEAVY, are deferred to k_heavy).
-__device__ __forceinline__ void take_chunk(WaveLds& L, Half& H, uint32_t h, const uint32_t* __restrict__ off,
-                                           uint32_t n, uint32_t nchunks, uint32_t lane) {
+__device__ __forceinline__ void prefetch_chunk(Prefetch& P, const uint32_t* __restrict__ off,
+                                               const uint32_t* __restrict__ wid, uint32_t n, uint32_t nchunks,
+                                               uint32_t lane) {
   ConstWork& w = *fresh();
-  // Straight-line loop with wave-uniform flags only (no return/continue from
-  // inside lane-conditional code: that pattern made the structurizer give
-  // the lanes different exits and the wave a chunk per lane).
-  bool taken = false;
+  P.t0 = P.nt = P.next = 0;
   uint32_t guard = 0;
-  while (!taken && ++guard < (1u << EGM_GUARD_BITS)) {
+  while (++guard < (1u << EGM_GUARD_BITS)) {
     uint32_t c = 0;
     if (lane == 0) c = atomicAdd(&w.stats->next_chunk, 1u);
     c = uni(__shfl(c, 0, 64));
@@ -727,62 +727,38 @@ __device__ __forceinline__ void take_chunk(WaveLds& L, Half& H, uint32_t h, cons
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, d, 64));
     dmax = uni(dmax);
-    const bool heavy = dmax > LIGHT_DMAX || (uni(w.debug) & DEBUG_FORCE_HEAVY);
-    if (heavy) {   // deferred to k_heavy
+    if (dmax > LIGHT_DMAX || (uni(w.debug) & DEBUG_FORCE_HEAVY)) {   // deferred to k_heavy
       uint32_t d = 0;
       if (lane == 0) d = atomicAdd(&w.stats->n_deferred, 1u);
       d = uni(__shfl(d, 0, 64));
       if (lane == 0) w.deferred[d] = c;
     } else {
-      if (lane < nt) {
-        const uint32_t s = h * WALK_CHUNK + lane;
-        L.tinfo[s] = D | (f << 24);
-        L.tbase[s] = base;
-        L.cnt[s] = 0;
-        L.last[s] = NONE;
-      }
-      // the first WPS words of each topic: two lanes per topic, WPS / 2 words each
-      const uint32_t jt = lane >> 1, part = lane & 1;
-      const uint32_t Dt = (uint32_t)__shfl(D, (int)jt, 64), bt = (uint32_t)__shfl(base, (int)jt, 64);
-      uint32_t wv[WPS / 2];
+      P.t0 = t0;
+      P.nt = nt;
+      P.D = D;
+      P.f = f;
+      P.base = base;
 #pragma unroll
-      for (uint32_t r = 0; r < WPS / 2; ++r) {
-        const uint32_t l = part * (WPS / 2) + r;
-        wv[r] = w.wid[(jt < nt && l < Dt) ? bt + l : 0u];
-      }
-#pragma unroll
-      for (uint32_t r = 0; r < WPS / 2; ++r) L.words[(h * WALK_CHUNK + jt) * WPS + part * (WPS / 2) + r] = wv[r];
-      H.chunk = c;
-      H.nt = nt;
-      H.dm = dmax;
-      taken = true;
+      for (uint32_t r = 0; r < WPS; ++r) P.wv[r] = wid[(lane < nt && r < D) ? base + r : 0u];
+      break;
     }
   }
-  if (!taken) {
-    H.chunk = NONE;
-    H.nt = 0;
-    H.dm = 0;
-  }
-  H.adm = 0;
-  H.live = 0;
-  wave_sync();
 }
 
-// Retire half hx once all its topics are admitted and its last item is done
-// (the stage has been flushed): write its per-topic counts and piece heads,
-// take the next chunk.
-#define WALK_RETIRE_HALF(HX, hx)                                                                        \
-  if (HX.chunk != NONE && HX.adm == HX.nt && HX.live == 0) {                                           \
-    const uint32_t t0 = HX.chunk * WALK_CHUNK;                                                         \
-    if (lane < HX.nt) {                                                                                \
-      ConstWork& w = *fresh();                                                                 \
-      w.cnt[t0 + lane] = L.cnt[(hx) * WALK_CHUNK + lane];                                              \
-      w.head[t0 + lane] = L.last[(hx) * WALK_CHUNK + lane];                                            \
-    }                                                                                                  \
-    wave_sync();                                                                                       \
-    take_chunk(L, HX, hx, off, n, nchunks, lane);                                                   \
-  }
+// Deepest topic held in the wave's slots (the pop bound needs it).
+__device__ __forceinline__ uint32_t slots_dmax(const WaveLds& L, uint64_t held, uint32_t lane) {
+  uint32_t d = ((held >> lane) & 1) ? (L.tinfo[lane] & 0xFFFFFFu) : 0u;
+#pragma unroll
+  for (int k = 32; k >= 1; k >>= 1) d = max(d, (uint32_t)__shfl_xor(d, k, 64));
+  return uni(d);
+}
 
+// One wave walks up to 64 topics at once, one per slot (slot = lane for the
+// per-slot bookkeeping).  A topic enters a free slot when the stack runs
+// short, its live item count is kept in LDS, and a slot whose topic has no
+// item left (and none of whose emits is still staged) is retired — counts
+// and piece head written — and refilled at once: the stack never drains
+// between topics or chunks.
 __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const uint32_t* __restrict__ wid,
                                              const uint32_t* __restrict__ off, uint32_t n, int mode) {
   __shared__ WaveLds L;
@@ -796,86 +772,103 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
   uint32_t created = 0;
   unsigned long long iters = 0, popped = 0, bounded = 0;
   Slab sid{0, 0}, spc{0, 0};
-  Half A, B;   // slots 0..63 and 64..127
-  // a flush reads the stage counts of all 128 slots: a half that never gets a
-  // chunk must read zeros
   L.fcnt[lane] = 0;   // slot = lane
-  take_chunk(L, A, 0, off, n, nchunks, lane);
-  take_chunk(L, B, 1, off, n, nchunks, lane);
-  uint32_t sp = 0, nstage = 0;
-  bool admit_b = false;   // which half is being admitted
-
+  L.live[lane] = 0;
+  if (lane < 2) L.finmask[lane] = 0;
+  Prefetch P;
+  prefetch_chunk(P, off, wid, n, nchunks, lane);
+  uint64_t freem = ~0ull, donem = 0;   // slots: free; done (no item left) but not yet retired
+  uint32_t sp = 0, nstage = 0, dmax = 0;
   uint32_t guard = 0;   // every loop of the kernel is bounded: a bug reports, it never hangs the GPU
   for (;;) {
     if (++guard > (1u << EGM_GUARD_BITS)) {
       if (lane == 0) atomicOr(&fresh()->stats->overflow, 8u);
       break;
     }
-    // ---- the one flush point of the loop top: before a retire, or when an
-    // admission's 64 root emits might not fit ----
+    const bool more = P.next < P.nt;
+    // ---- the one flush point of the loop top: room for 64 root emits, done
+    // slots to recycle, or the end ----
+    if (nstage && (nstage + 64u > WALK_STAGE || (donem && (!freem || (sp == 0 && !more))) ||
+                   (donem && sp < 64u && popc(freem) < 8u))) {
+      flush_stage(L, nstage, lane, sid, spc);
+      nstage = 0;
+    }
+    // ---- retire done slots with nothing staged ----
     {
-      const bool ra = A.chunk != NONE && A.adm == A.nt && A.live == 0;
-      const bool rb = B.chunk != NONE && B.adm == B.nt && B.live == 0;
-      if (nstage && (ra || rb || nstage + 64u > WALK_STAGE)) {
-        flush_stage(L, nstage, lane, sid, spc);
-        nstage = 0;
+      const uint64_t rm = __ballot(((donem >> lane) & 1) && L.fcnt[lane] == 0);
+      if (rm) {
+        if ((rm >> lane) & 1) {
+          ConstWork& w = *fresh();
+          const uint32_t t = L.tid[lane];
+          w.cnt[t] = L.cnt[lane];
+          w.head[t] = L.last[lane];
+        }
+        donem &= ~rm;
+        freem |= rm;
+        dmax = slots_dmax(L, ~freem, lane);
       }
     }
-    // ---- retire chunks whose topics are all admitted and done ----
-    WALK_RETIRE_HALF(A, 0)
-    WALK_RETIRE_HALF(B, 1)
-    // ---- admission: new topics while the stack is short ----
-    if (sp < 64u) {
-      if (!admit_b && A.adm >= A.nt && B.adm < B.nt) admit_b = true;
-      else if (admit_b && B.adm >= B.nt && A.adm < A.nt) admit_b = false;
-      const uint32_t nt_h = admit_b ? B.nt : A.nt, adm_h = admit_b ? B.adm : A.adm;
-      if (adm_h < nt_h) {
-        // admit up to 64 - sp topics of the half: their root '#' emits
-        // (wildcard topics in ROUTES mode: one exact lookup, no push) and
-        // root items
-        const uint32_t k = min(64u - sp, nt_h - adm_h);
-        bool has = false, em = false;
-        uint32_t fid = NONE;
-        uint4 it = make_uint4(0, 0, 0, 0);
-        const uint32_t s = (admit_b ? WALK_CHUNK : 0u) + adm_h + lane;
-        if (lane < k) {
-          const uint32_t ti = L.tinfo[s], D = ti & 0xFFFFFFu, tf = ti >> 24;
-          if (tf & TF_WILDCARD) {
-            if (mode == MODE_ROUTES) em = exact_walk(tab, wid, L.tbase[s], D, &fid);
-          } else {
-            const bool dollar = (tf & TF_DOLLAR) != 0;
-            em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
-            fid = root.y;
-            created += 1;
-            const uint32_t w0 = L.words[s * WPS];
-            const uint32_t fl = root_flags(root, dollar, w0);
-            has = fl != 0;
-            it = make_uint4(0, (s << MT_SHIFT) | (fl << MF_SHIFT), root.x, w0);
-          }
-        }
-        const uint64_t b = __ballot(has);
-        if (has) L.stack[sp + mbcnt(b)] = it;
-        const uint64_t be = __ballot(em);
-        if (em) {
-          const uint32_t q = nstage + mbcnt(be);
-          L.stage_fid[q] = fid;
-          L.stage_t[q] = (uint8_t)s;
-        }
-        const uint32_t pushed = popc(b);
-        sp += pushed;
-        nstage += popc(be);
-        if (admit_b) {
-          B.adm += k;
-          B.live += pushed;
+    // ---- admission: new topics into free slots while the stack is short ----
+    if (sp < 64u && freem && more) {
+      const uint32_t k = min(min(64u - sp, popc(freem)), P.nt - P.next);
+      const bool fr = (freem >> lane) & 1;
+      const uint32_t r = mbcnt(freem);               // rank of this free slot
+      const bool tk = fr && r < k;                   // slot `lane` takes prefetched topic P.next + r
+      const uint32_t src = P.next + (tk ? r : 0u);
+      const uint32_t D = (uint32_t)__shfl(P.D, (int)src, 64), f = (uint32_t)__shfl(P.f, (int)src, 64);
+      const uint32_t base = (uint32_t)__shfl(P.base, (int)src, 64);
+      uint32_t wv[WPS];
+#pragma unroll
+      for (uint32_t q = 0; q < WPS; ++q) wv[q] = (uint32_t)__shfl(P.wv[q], (int)src, 64);
+      bool has = false, em = false;
+      uint32_t fid = NONE;
+      uint4 it = make_uint4(0, 0, 0, 0);
+      if (tk) {
+        L.tinfo[lane] = D | (f << 24);
+        L.tbase[lane] = base;
+        L.tid[lane] = P.t0 + src;
+        L.cnt[lane] = 0;
+        L.last[lane] = NONE;
+#pragma unroll
+        for (uint32_t q = 0; q < WPS; ++q) L.words[lane * WPS + q] = wv[q];
+        if (f & TF_WILDCARD) {
+          if (mode == MODE_ROUTES) em = exact_walk(tab, wid, base, D, &fid);
         } else {
-          A.adm += k;
-          A.live += pushed;
+          const bool dollar = (f & TF_DOLLAR) != 0;
+          em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
+          fid = root.y;
+          created += 1;
+          const uint32_t fl = root_flags(root, dollar, wv[0]);
+          has = fl != 0;
+          it = make_uint4(0, (lane << MT_SHIFT) | (fl << MF_SHIFT), root.x, wv[0]);
         }
-        wave_sync();
+        L.live[lane] = has ? 1u : 0u;
       }
+      const uint64_t b = __ballot(has);
+      if (has) L.stack[sp + mbcnt(b)] = it;
+      sp += popc(b);
+      const uint64_t be = __ballot(em);
+      if (em) {
+        const uint32_t q = nstage + mbcnt(be);
+        L.stage_fid[q] = fid;
+        L.stage_t[q] = (uint8_t)lane;
+      }
+      nstage += popc(be);
+      const uint64_t tkm = __ballot(tk);
+      freem &= ~tkm;
+      donem |= tkm & ~b;   // a topic with no item is done at once
+      {
+        uint32_t dm = tk ? D : 0u;
+#pragma unroll
+        for (int d2 = 32; d2 >= 1; d2 >>= 1) dm = max(dm, (uint32_t)__shfl_xor(dm, d2, 64));
+        dmax = max(dmax, uni(dm));
+      }
+      P.next += k;
+      wave_sync();
+      if (P.next >= P.nt) prefetch_chunk(P, off, wid, n, nchunks, lane);
     }
     if (sp == 0) {
-      if (A.chunk == NONE && B.chunk == NONE) break;
+      if (!(P.next < P.nt) && !donem) break;   // no topic left, every slot retired
       continue;
     }
 
@@ -885,7 +878,6 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
     // item at a time, a plain DFS, whose stack grows by at most one pending
     // sibling per level below the top item.  So the stack never overflows: a
     // deep, wide frontier (C3: depth 16, '+' p=.35) narrows the wave instead.
-    const uint32_t dmax = max(A.dm, B.dm);
     const uint32_t room = WALK_STACK - sp;
     const uint32_t lim = room > dmax ? room - dmax : 1u;
     const uint32_t want = min(64u, sp), take = min(want, lim), bi = sp - take;
@@ -896,16 +888,11 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
     p.act = lane < take;
     p.it = L.stack[min(bi + lane, WALK_STACK - 1)];   // unconditional: see issue()
     sp = bi;
-    const uint32_t slot = (p.it.y >> MT_SHIFT) & 0x7Fu;
+    const uint32_t slot = (p.it.y >> MT_SHIFT) & (SLOTS - 1);
     const uint32_t ti = L.tinfo[slot];
     p.D = ti & 0xFFFFFFu;
     p.d1 = p.D == 1 && ((ti >> 24) & TF_DOLLAR);
     issue(tab, wid, L.tbase[slot], L.words + slot * WPS, p);
-    {
-      const uint32_t n1 = popc(__ballot(p.act && slot >= WALK_CHUNK));
-      B.live -= n1;
-      A.live -= take - n1;
-    }
     wave_sync();
 
     // ---- consume: children -> stack, emits -> stage ----
@@ -916,11 +903,13 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
     const uint32_t m0 = popc(c0b);
     if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
     if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;
-    const uint32_t np = m0 + popc(c1b);
-    const uint32_t n1 = popc(__ballot(o.p0 && slot >= WALK_CHUNK)) + popc(__ballot(o.p1 && slot >= WALK_CHUNK));
-    B.live += n1;
-    A.live += np - n1;
-    sp += np;
+    sp += m0 + popc(c1b);
+    // live items per topic: children first, then the popped item, so the lane
+    // that takes a topic's count to zero is the last one
+    const uint32_t pushes = (o.p0 ? 1u : 0u) + (o.p1 ? 1u : 0u);
+    if (pushes) atomicAdd(&L.live[slot], pushes);
+    wave_sync();
+    if (p.act && atomicSub(&L.live[slot], 1u) == 1u) atomicOr(&L.finmask[slot >> 5], 1u << (slot & 31));
     // emits (at most 4 per lane): the stage is flushed first if they do not fit
     {
       const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
@@ -954,8 +943,14 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
       nstage += ne;
     }
     wave_sync();
+    {   // topics that finished this iteration
+      const uint64_t fin = ((uint64_t)uni(L.finmask[1]) << 32) | uni(L.finmask[0]);
+      donem |= fin;
+      wave_sync();
+      if (lane < 2) L.finmask[lane] = 0;
+      wave_sync();
+    }
   }
-#undef WALK_RETIRE_HALF
   unsigned long long v = created;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -1293,7 +1288,7 @@ static uint32_t walk_resident_waves() {
 
 int walk_grid_blocks(uint32_t n) {
   const uint32_t chunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
-  uint32_t blocks = (chunks + 1) / 2;   // two chunks in flight per wave
+  uint32_t blocks = chunks;   // waves keep taking chunks until none is left
   const uint32_t cap = walk_resident_waves();
   if (blocks > cap) blocks = cap;
   return blocks ? (int)blocks : 1;
