@@ -87,6 +87,8 @@ SIGNATURES = {
     "egm_filter_id": (C.c_int, [_P, _P, C.c_uint32, _u32p]),
     "egm_filter_bytes": (C.c_int, [_P, C.c_uint32, C.POINTER(_u8p), _u32p]),
     "egm_match_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_int, C.POINTER(C.POINTER(egm_result))]),
+    "egm_match_submit": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_int, _u64p]),
+    "egm_match_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(C.POINTER(egm_result))]),
     "egm_match_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, _P, _P, C.c_uint64, _P]),
     "egm_last_stats": (C.c_int, [_P, _u64p, _u64p, _u32p, _u32p, _u32p]),
     "egm_last_walk_counters": (C.c_int, [_P, _u64p, _u64p, _u64p]),

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/emqx_gpu_match.h"
+#include "egm_alloc.h"
 #include "egm_kernels.h"
 #include "egm_table.h"
 
@@ -53,6 +54,53 @@ struct DevBuf {
   template <class T>
   T* as() const { return (T*)p; }
 };
+
+// Pinned host memory (page-locked: DMA at full PCIe rate, asynchronous copies).
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  PinBuf() = default;
+  PinBuf(const PinBuf&) = delete;
+  PinBuf& operator=(const PinBuf&) = delete;
+  ~PinBuf() { release(); }
+  void release() {
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    release();
+    const size_t b = bytes + bytes / 4 + 4096;   // grow with headroom: pinning is slow
+    hipError_t e = hipHostMalloc(&p, b, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = b;
+    return hipSuccess;
+  }
+};
+
+// One batch of the host pipeline (egm_match_submit / egm_match_wait): its
+// pinned input copy, device input and output, and the pinned result the
+// caller reads until egm_result_free.
+struct PipeSlot {
+  bool busy = false;     // submitted, not yet waited for
+  bool held = false;     // its result is with the caller
+  uint32_t n = 0;
+  int mode = 0;
+  uint64_t bytes = 0, maxlen = 0, cap = 0;
+  PinBuf h_in, h_out, h_stats;
+  DevBuf d_blob, d_off, d_row, d_ids, d_flags;
+  hipEvent_t ev_in = nullptr, ev_done = nullptr;
+  uint64_t epoch = 0;
+  ~PipeSlot() {
+    if (ev_in) hipEventDestroy(ev_in);
+    if (ev_done) hipEventDestroy(ev_done);
+  }
+};
+constexpr size_t PIPE_MAX_SLOTS = 8;
 
 // One device copy of the table image.  Two slots alternate: a commit writes
 // the slot that is NOT current, so batches still reading the current epoch are
@@ -138,6 +186,9 @@ struct egm_ctx {
     if (work_ev) hipEventRecord(work_ev, s);
     work_stream = s;
   }
+  // host pipeline (egm_match_submit / egm_match_wait)
+  std::vector<std::unique_ptr<PipeSlot>> pipe;
+  hipStream_t copy_stream = nullptr;
   // last fan-out (egm_last_fanout)
   const uint64_t* fan_drow = nullptr;
   uint32_t fan_topics = 0;
@@ -597,6 +648,10 @@ void egm_close(egm_ctx* c) {
     c->patch_host = nullptr;
     if (c->work_ev) hipEventDestroy(c->work_ev);
     c->work_ev = nullptr;
+    if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
+    c->pipe.clear();
+    if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+    c->copy_stream = nullptr;
   }
   hipStreamDestroy(c->stream);
   delete c;
@@ -767,91 +822,197 @@ int egm_get_timing(egm_ctx* c, double* walk_ms, uint64_t* walk_n, double* fan_ms
   return EGM_OK;
 }
 
-int egm_match_batch(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, int mode,
-                    egm_result** out) {
-  if (!c || !out || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES)) return EGM_E_INVAL;
+// Copy n bytes with up to 8 threads (large batches: one host core moves
+// ~10 GB/s, the PCIe link ~50).
+static void par_copy(void* dst, const void* src, size_t bytes) {
+  const size_t chunk = 64u << 20;
+  if (bytes <= chunk) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  const unsigned nt = (unsigned)std::min<size_t>(8, (bytes + chunk - 1) / chunk);
+  std::vector<std::thread> th;
+  const size_t per = (bytes + nt - 1) / nt;
+  for (unsigned k = 0; k < nt; ++k) {
+    const size_t lo = k * per, hi = std::min(bytes, lo + per);
+    if (lo < hi) th.emplace_back([=] { memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, hi - lo); });
+  }
+  for (auto& x : th) x.join();
+}
+
+// Enqueue one staged batch of slot S: H2D on the copy stream, the match on
+// the context stream once the input is in, then the batch's flags and
+// counters copied out in stream order (the next batch reuses the workspace).
+static int pipe_launch(egm_ctx* c, PipeSlot& S) {
+  hipError_t e;
+  hipStream_t s = c->stream;
+  const uint64_t n = S.n;
+  std::shared_ptr<Epoch> ep = c->cur;
+  S.epoch = ep->id;
+  int r = ensure_work(c, S.n, S.bytes, S.cap, S.maxlen + 1);
+  if (r) return r;
+  if ((e = S.d_row.ensure((n + 1) * 8)) != hipSuccess) return c->hip_fail(e, "pipe row");
+  if ((e = S.d_ids.ensure((S.cap + 1) * 4)) != hipSuccess) return c->hip_fail(e, "pipe ids");
+  if ((e = S.d_flags.ensure(n + 8)) != hipSuccess) return c->hip_fail(e, "pipe flags");
+  if ((e = S.h_stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "pipe stats");
+  if ((e = hipStreamWaitEvent(s, S.ev_in, 0)) != hipSuccess) return c->hip_fail(e, "pipe wait input");
+  r = run_match(c, *ep, S.d_blob.as<uint8_t>(), S.d_off.as<uint32_t>(), S.n, S.mode, s, S.d_row.as<uint64_t>(),
+                S.d_ids.as<uint32_t>(), S.cap);
+  if (r) return r;
+  c->last_pending = false;   // this batch's counters travel with the slot
+  if ((n && (e = hipMemcpyAsync(S.d_flags.p, c->tfl.p, n, hipMemcpyDeviceToDevice, s)) != hipSuccess) ||
+      (e = hipMemcpyAsync(S.h_stats.p, c->stats.p, sizeof(MatchStats), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipEventRecord(S.ev_done, s)) != hipSuccess)
+    return c->hip_fail(e, "pipe epilogue");
+  return EGM_OK;
+}
+
+int egm_match_submit(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, int mode, uint64_t* ticket) {
+  if (!c || !ticket || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES)) return EGM_E_INVAL;
   if (n && (!off || !valid_offsets(off, n) || (!blob && off[n] > off[0]))) return EGM_E_INVAL;
-  *out = nullptr;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
-  hipStream_t s = c->stream;
-  // stage inputs (rebased so offsets start at 0)
+  hipError_t e;
+  if (!c->copy_stream && (e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking)) != hipSuccess)
+    return c->hip_fail(e, "copy stream");
+  size_t k = 0;
+  while (k < c->pipe.size() && (c->pipe[k]->busy || c->pipe[k]->held)) ++k;
+  if (k == c->pipe.size()) {
+    if (k == PIPE_MAX_SLOTS) return c->fail(EGM_E_STATE, "pipeline full: wait for a ticket or free its result");
+    c->pipe.emplace_back(new PipeSlot());
+    PipeSlot& N = *c->pipe.back();
+    if (hipEventCreateWithFlags(&N.ev_in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&N.ev_done, hipEventDisableTiming) != hipSuccess)
+      return c->fail(EGM_E_DEVICE, "pipe events");
+  }
+  PipeSlot& S = *c->pipe[k];
+  // stage the caller's (borrowed) batch in pinned memory, offsets rebased to 0
   const uint32_t base0 = n ? off[0] : 0;
   const uint64_t bytes = n ? (uint64_t)off[n] - base0 : 0;
-  std::vector<uint32_t> loff(n + 1);
+  const uint64_t o_off = (bytes + 15) & ~15ull, in_sz = o_off + ((uint64_t)n + 1) * 4;
+  if ((e = S.h_in.ensure(in_sz)) != hipSuccess) return c->hip_fail(e, "pipe pinned input");
+  // the previous use of this slot's staging must be finished (its H2D)
+  if ((e = hipEventSynchronize(S.ev_in)) != hipSuccess) return c->hip_fail(e, "pipe input reuse");
+  uint8_t* hin = (uint8_t*)S.h_in.p;
+  if (bytes) par_copy(hin, blob + base0, bytes);
+  uint32_t* hoff = (uint32_t*)(hin + o_off);
   uint64_t maxlen = 0;
-  for (uint32_t i = 0; i <= n; ++i) loff[i] = n ? off[i] - base0 : 0;
-  for (uint32_t i = 0; i < n; ++i) maxlen = std::max<uint64_t>(maxlen, loff[i + 1] - loff[i]);
+  for (uint32_t i = 0; i <= n; ++i) hoff[i] = n ? off[i] - base0 : 0;
+  for (uint32_t i = 0; i < n; ++i) maxlen = std::max<uint64_t>(maxlen, hoff[i + 1] - hoff[i]);
+  S.n = n;
+  S.mode = mode;
+  S.bytes = bytes;
+  S.maxlen = maxlen;
+  S.cap = std::max<uint64_t>(std::max<uint64_t>((uint64_t)n * 4 + 1024, S.cap), c->out_ids.cap / 4);
+  if ((e = S.d_blob.ensure(bytes + 16)) != hipSuccess) return c->hip_fail(e, "pipe blob");
+  if ((e = S.d_off.ensure(((uint64_t)n + 1) * 4)) != hipSuccess) return c->hip_fail(e, "pipe offsets");
+  if ((bytes && (e = hipMemcpyAsync(S.d_blob.p, hin, bytes, hipMemcpyHostToDevice, c->copy_stream)) != hipSuccess) ||
+      (e = hipMemcpyAsync(S.d_off.p, hoff, ((uint64_t)n + 1) * 4, hipMemcpyHostToDevice, c->copy_stream)) !=
+          hipSuccess ||
+      (e = hipEventRecord(S.ev_in, c->copy_stream)) != hipSuccess)
+    return c->hip_fail(e, "pipe H2D");
+  int r = pipe_launch(c, S);
+  if (r) return r;
+  S.busy = true;
+  *ticket = (uint64_t)k + 1;
+  return EGM_OK;
+}
+
+int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
+  if (!c || !out || ticket == 0) return EGM_E_INVAL;
+  *out = nullptr;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (ticket > c->pipe.size() || !c->pipe[ticket - 1]->busy) return c->fail(EGM_E_STATE, "unknown ticket");
+  if (set_device(c)) return EGM_E_DEVICE;
+  PipeSlot& S = *c->pipe[ticket - 1];
   hipError_t e;
-  if ((e = c->in_blob.ensure(bytes + 16)) != hipSuccess) return c->hip_fail(e, "in_blob");
-  if ((e = c->in_off.ensure(((uint64_t)n + 1) * 4)) != hipSuccess) return c->hip_fail(e, "in_off");
-  if (bytes && (e = hipMemcpyAsync(c->in_blob.p, blob + base0, bytes, hipMemcpyHostToDevice, s)) != hipSuccess)
-    return c->hip_fail(e, "H2D blob");
-  if ((e = hipMemcpyAsync(c->in_off.p, loff.data(), ((uint64_t)n + 1) * 4, hipMemcpyHostToDevice, s)) !=
-      hipSuccess)
-    return c->hip_fail(e, "H2D offsets");
-  std::shared_ptr<Epoch> ep = c->cur;
-  uint64_t cap = std::max<uint64_t>((uint64_t)n * 4 + 1024, c->out_ids.cap / 4);
-  for (int attempt = 0; attempt < 3; ++attempt) {
-    int r = ensure_work(c, n, bytes, cap, maxlen + 1);
-    if (r) return r;
-    if ((e = c->out_row.ensure(((uint64_t)n + 1) * 8)) != hipSuccess) return c->hip_fail(e, "out_row");
-    if ((e = c->out_ids.ensure((cap + 1) * 4)) != hipSuccess) return c->hip_fail(e, "out_ids");
-    r = run_match(c, *ep, c->in_blob.as<uint8_t>(), c->in_off.as<uint32_t>(), n, mode, s,
-                  c->out_row.as<uint64_t>(), c->out_ids.as<uint32_t>(), cap);
-    if (r) return r;
-    r = sync_last(c);
-    if (r) return r;
-    if (!c->last.overflow) break;
-    cap = c->last.total_ids + c->last.total_ids / 8 + 1024;   // exact total is known even on overflow
-    if (attempt == 2) return c->fail(EGM_E_NOMEM, "ids capacity");
+  MatchStats st{};
+  for (int attempt = 0;; ++attempt) {
+    if ((e = hipEventSynchronize(S.ev_done)) != hipSuccess) return c->hip_fail(e, "pipe wait");
+    st = *(const MatchStats*)S.h_stats.p;
+    if (!st.overflow) break;
+    if (attempt == 2 || (st.overflow & ~3u)) {
+      S.busy = false;
+      return c->fail(EGM_E_NOMEM, "ids capacity");
+    }
+    // the exact total is known even on overflow: rerun the staged batch once with room for it
+    S.cap = st.total_ids + st.total_ids / 8 + 1024;
+    int r = pipe_launch(c, S);
+    if (r) {
+      S.busy = false;
+      return r;
+    }
   }
-  const uint64_t nids = c->last.total_ids;
-  // one allocation: struct + arrays (egm_result_free == free)
-  size_t sz = sizeof(egm_result);
-  size_t o_counts = sz;
-  sz += ((uint64_t)n * 4 + 7) & ~7ull;
-  size_t o_row = sz;
-  sz += ((uint64_t)n + 1) * 8;
-  size_t o_ids = sz;
-  sz += ((nids * 4) + 7) & ~7ull;
-  size_t o_flags = sz;
-  sz += n + 8;
-  uint8_t* mem = (uint8_t*)malloc(sz);
-  if (!mem) return c->fail(EGM_E_NOMEM, "result");
-  egm_result* res = (egm_result*)mem;
+  c->last = st;   // egm_last_stats reports the waited batch
+  const uint64_t n = S.n, nids = st.total_ids;
+  // result: header + struct + counts + row_ptr + ids + flags, in the slot's pinned memory
+  const size_t o_res = sizeof(ResultHdr), o_cnt = (o_res + sizeof(egm_result) + 15) & ~(size_t)15,
+               o_row = (o_cnt + n * 4 + 15) & ~(size_t)15, o_ids = o_row + (n + 1) * 8,
+               o_fl = (o_ids + nids * 4 + 15) & ~(size_t)15, total = o_fl + n + 16;
+  if ((e = S.h_out.ensure(total)) != hipSuccess) {
+    S.busy = false;
+    return c->hip_fail(e, "pipe pinned result");
+  }
+  uint8_t* h = (uint8_t*)S.h_out.p;
+  ResultHdr* hdr = (ResultHdr*)h;
+  egm_result* res = (egm_result*)(h + o_res);
   memset(res, 0, sizeof(*res));
-  res->n_topics = n;
+  res->n_topics = S.n;
   res->n_ids = nids;
-  res->counts = (uint32_t*)(mem + o_counts);
-  res->row_ptr = (uint64_t*)(mem + o_row);
-  res->ids = (uint32_t*)(mem + o_ids);
-  res->flags = (uint8_t*)(mem + o_flags);
-  res->epoch = ep->id;
-  res->visited = c->last.visited;
-  res->n_error = c->last.errors;
-  if ((e = hipMemcpy(res->row_ptr, c->out_row.p, ((uint64_t)n + 1) * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
-      (nids && (e = hipMemcpy(res->ids, c->out_ids.p, nids * 4, hipMemcpyDeviceToHost)) != hipSuccess) ||
-      (n && (e = hipMemcpy(res->flags, c->tfl.p, n, hipMemcpyDeviceToHost)) != hipSuccess)) {
-    free(mem);
-    return c->hip_fail(e, "D2H result");
+  res->counts = (uint32_t*)(h + o_cnt);
+  res->row_ptr = (uint64_t*)(h + o_row);
+  res->ids = (uint32_t*)(h + o_ids);
+  res->flags = (uint8_t*)(h + o_fl);
+  res->epoch = S.epoch;
+  res->visited = st.visited;
+  res->n_error = st.errors;
+  if ((e = hipMemcpyAsync(res->row_ptr, S.d_row.p, (n + 1) * 8, hipMemcpyDeviceToHost, c->copy_stream)) !=
+          hipSuccess ||
+      (nids && (e = hipMemcpyAsync(res->ids, S.d_ids.p, nids * 4, hipMemcpyDeviceToHost, c->copy_stream)) !=
+                   hipSuccess) ||
+      (n && (e = hipMemcpyAsync(res->flags, S.d_flags.p, n, hipMemcpyDeviceToHost, c->copy_stream)) != hipSuccess) ||
+      (e = hipStreamSynchronize(c->copy_stream)) != hipSuccess) {
+    S.busy = false;
+    return c->hip_fail(e, "pipe D2H");
   }
-  if (res->row_ptr[n] != nids) {
-    free(mem);
-    return c->fail(EGM_E_DEVICE, "row_ptr total mismatch");
-  }
+  S.busy = false;
+  if (res->row_ptr[n] != nids) return c->fail(EGM_E_DEVICE, "row_ptr total mismatch");
   uint32_t heavy = 0;
-  for (uint32_t i = 0; i < n; ++i) {
+  for (uint64_t i = 0; i < n; ++i) {
     res->counts[i] = (uint32_t)(res->row_ptr[i + 1] - res->row_ptr[i]);
     heavy += (res->flags[i] & TF_HEAVY) ? 1 : 0;
   }
   res->n_heavy = heavy;
+  hdr->magic = RES_PIPE;
+  hdr->owner = c;
+  hdr->slot = ticket - 1;
+  S.held = true;
   *out = res;
   if (res->n_error) {
-    c->err = "some topics exceeded the heavy-path frontier stack (flag EGM_TF_ERROR)";
+    c->err = "some topics could not be walked (flag EGM_TF_ERROR)";
     return EGM_E_OVERFLOW;
   }
   return EGM_OK;
+}
+
+// One synchronous batch: the pipeline with a single ticket.  Host buffers are
+// staged in pinned memory and the result is read in place from pinned memory
+// (released by egm_result_free).
+int egm_match_batch(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, int mode,
+                    egm_result** out) {
+  if (!c || !out) return EGM_E_INVAL;
+  *out = nullptr;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  uint64_t t = 0;
+  int r = egm_match_submit(c, blob, off, n, mode, &t);
+  if (r) return r;
+  return egm_match_wait(c, t, out);
+}
+
+// egm_result_free for a pipeline result: the slot's pinned memory is free again.
+static void pipe_release(egm_ctx* c, uint64_t slot) {
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (slot < c->pipe.size()) c->pipe[slot]->held = false;
 }
 
 // ---------------------------------------------------------------- fan-out --
@@ -962,7 +1123,7 @@ int egm_fanout_batch(egm_ctx* c, const egm_result* m, egm_delivery** out) {
   sz += (total * 4 + 7) & ~7ull;
   size_t o_sub = sz;
   sz += (total * 4 + 7) & ~7ull;
-  uint8_t* mem = (uint8_t*)malloc(sz);
+  uint8_t* mem = (uint8_t*)result_alloc(sz);
   if (!mem) return c->fail(EGM_E_NOMEM, "delivery");
   egm_delivery* d = (egm_delivery*)mem;
   d->n_topics = n;
@@ -973,7 +1134,7 @@ int egm_fanout_batch(egm_ctx* c, const egm_result* m, egm_delivery** out) {
   if ((e = hipMemcpy(d->row_ptr, c->f_drow.p, ((uint64_t)n + 1) * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
       (total && (e = hipMemcpy(d->fid, c->f_dfid.p, total * 4, hipMemcpyDeviceToHost)) != hipSuccess) ||
       (total && (e = hipMemcpy(d->sub, c->f_dsub.p, total * 4, hipMemcpyDeviceToHost)) != hipSuccess)) {
-    free(mem);
+    result_discard(mem);
     return c->hip_fail(e, "D2H deliveries");
   }
   *out = d;
@@ -1023,7 +1184,12 @@ int egm_last_fanout(egm_ctx* c, uint64_t* n_deliveries, uint32_t* overflow) {
   return EGM_OK;
 }
 
-void egm_result_free(void* r) { free(r); }
+void egm_result_free(void* r) {
+  if (!r) return;
+  ResultHdr* h = (ResultHdr*)r - 1;
+  if (h->magic == RES_PIPE) pipe_release((egm_ctx*)h->owner, h->slot);
+  else result_discard(r);
+}
 
 // ---------------------------------------------------- host-only image API --
 struct egm_image {

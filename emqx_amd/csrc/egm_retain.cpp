@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/emqx_gpu_match.h"
+#include "egm_alloc.h"
 #include "egm_kernels.h"
 
 using namespace egm;
@@ -479,7 +480,7 @@ int egm_rstore_match(egm_rstore* r, const uint8_t* blob, const uint32_t* off, ui
   sz += (total * 4 + 7) & ~7ull;
   const size_t o_flags = sz;
   sz += n + 8;
-  uint8_t* mem = (uint8_t*)malloc(sz);
+  uint8_t* mem = (uint8_t*)result_alloc(sz);
   if (!mem) return r->fail(EGM_E_NOMEM, "result");
   egm_result* res = (egm_result*)mem;
   memset(res, 0, sizeof(*res));
@@ -493,7 +494,7 @@ int egm_rstore_match(egm_rstore* r, const uint8_t* blob, const uint32_t* off, ui
       (total && (e = hipMemcpyAsync(res->ids, r->ids.p, total * 4, hipMemcpyDeviceToHost, s))) ||
       (n && (e = hipMemcpyAsync(res->flags, r->tfl.p, n, hipMemcpyDeviceToHost, s))) ||
       (e = hipStreamSynchronize(s))) {
-    free(mem);
+    result_discard(mem);
     return r->hip_fail(e, "D2H result");
   }
   for (uint32_t i = 0; i < n; ++i) res->counts[i] = (uint32_t)(res->row_ptr[i + 1] - res->row_ptr[i]);

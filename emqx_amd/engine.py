@@ -173,6 +173,35 @@ class GpuMatcher:
         finally:
             self.lib.egm_result_free(res)
 
+    def submit(self, blob: np.ndarray, off: np.ndarray, mode: int = L.EGM_MODE_TRIE) -> int:
+        """Queue a host batch on the pipeline (staged in pinned memory at once)."""
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        t = C.c_uint64()
+        self._check(self.lib.egm_match_submit(self.ctx, _ptr(blob), _ptr(off), len(off) - 1, mode, C.byref(t)),
+                    "egm_match_submit")
+        return t.value
+
+    def wait(self, ticket: int, copy: bool = True) -> Optional[MatchResult]:
+        """Result of a submitted batch (copied out, pinned memory released);
+        copy=False releases it unread (throughput measurement)."""
+        res = C.POINTER(L.egm_result)()
+        rc = self.lib.egm_match_wait(self.ctx, ticket, C.byref(res))
+        if rc != 0:
+            if res:
+                self.lib.egm_result_free(res)
+            self._check(rc, "egm_match_wait")
+        try:
+            if not copy:
+                return None
+            r = res.contents
+            n, nid = int(r.n_topics), int(r.n_ids)
+            row = np.ctypeslib.as_array(r.row_ptr, shape=(n + 1,)).copy()
+            ids = np.ctypeslib.as_array(r.ids, shape=(nid,)).copy() if nid else np.zeros(0, np.uint32)
+            fl = np.ctypeslib.as_array(r.flags, shape=(n,)).copy() if n else np.zeros(0, np.uint8)
+            return MatchResult(row, ids, fl, int(r.epoch), int(r.visited), int(r.n_heavy), int(r.n_error))
+        finally:
+            self.lib.egm_result_free(res)
+
     def match_strings(self, topics: Sequence[bytes], mode: int = L.EGM_MODE_TRIE) -> MatchResult:
         blob, off = pack_strings(topics)
         return self.match(blob, off, mode)

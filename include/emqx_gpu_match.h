@@ -137,6 +137,20 @@ int egm_filter_bytes(egm_ctx* ctx, uint32_t id, const uint8_t** bytes, uint32_t*
 int egm_match_batch(egm_ctx* ctx, const uint8_t* topics_blob, const uint32_t* topic_offsets,
                     uint32_t n_topics, int mode, egm_result** out);
 
+/* Pipelined host batches (the drop-in's NIF path; SURVEY §8b ownership):
+   egm_match_submit copies the caller's borrowed batch into pinned staging at
+   once (the caller may reuse its buffers when it returns), queues the
+   host->device copy on a copy stream and the match on the context stream, and
+   hands back a ticket; egm_match_wait blocks for that ticket and returns the
+   CSR result in pinned memory (no extra host copy), valid until
+   egm_result_free.  With two tickets in flight, batch k's device->host copy
+   overlaps batch k+1's match.  At most 8 tickets or unreleased results per
+   context (EGM_E_STATE beyond); free pipeline results before egm_close.
+   egm_match_batch is submit + wait. */
+int egm_match_submit(egm_ctx* ctx, const uint8_t* topics_blob, const uint32_t* topic_offsets, uint32_t n_topics,
+                     int mode, uint64_t* ticket);
+int egm_match_wait(egm_ctx* ctx, uint64_t ticket, egm_result** out);
+
 /* Device-resident variant: d_blob (4-byte aligned, blob_bytes >= d_offsets[n])
    and d_offsets are device pointers (d_offsets[0] == 0); results stay in device buffers owned by the caller
    (d_row_ptr[n+1], d_ids[ids_cap], d_flags[n] may be NULL).  Asynchronous on

@@ -171,3 +171,39 @@ def test_no_overflow_2_14_wide_frontier(gm):
     assert hv.n_error == 0 and sets(hv) == got
     for i in (0, 1):
         assert sorted(filters[x] for x in got[i]) == sorted(R.trie_semantics(topics[i], filters))
+
+
+def test_pipeline_submit_wait(gm):
+    """egm_match_submit / egm_match_wait: batches staged in pinned memory and
+    overlapped, results equal to one-by-one matching, the caller's buffers
+    reusable as soon as submit returns, and the ticket limit enforced."""
+    f, t = synth.config("c0", n_topics=60_000)
+    gm.build(f.blob, f.off)
+    parts = [t.subset(np.arange(a, b)) for a, b in ((0, 20_000), (20_000, 20_001), (20_001, 20_001),
+                                                      (20_001, 60_000))]
+    want = [gm.match(p.blob, p.off, L.EGM_MODE_ROUTES) for p in parts]
+    tickets = []
+    for p in parts:
+        blob, off = p.blob.copy(), p.off.copy()
+        tickets.append(gm.submit(blob, off, L.EGM_MODE_ROUTES))
+        blob[:] = 0   # the library staged its own copy
+        off[:] = 0
+    for tk, w in zip(tickets, want):
+        got = gm.wait(tk)
+        assert np.array_equal(got.row_ptr, w.row_ptr)
+        assert np.array_equal(canonical(got.row_ptr, got.ids), canonical(w.row_ptr, w.ids))
+        assert np.array_equal(got.flags, w.flags)
+    # results held by the caller block their slots: at most 8 outstanding
+    import ctypes as C
+    held = []
+    for _ in range(8):
+        tk = gm.submit(parts[0].blob, parts[0].off, L.EGM_MODE_ROUTES)
+        r = C.POINTER(L.egm_result)()
+        assert gm.lib.egm_match_wait(gm.ctx, tk, C.byref(r)) == 0
+        held.append(r)
+    with pytest.raises(L.EgmError):
+        gm.submit(parts[0].blob, parts[0].off, L.EGM_MODE_ROUTES)
+    for r in held:
+        gm.lib.egm_result_free(r)
+    again = gm.wait(gm.submit(parts[3].blob, parts[3].off, L.EGM_MODE_ROUTES))
+    assert np.array_equal(again.row_ptr, want[3].row_ptr)

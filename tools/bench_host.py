@@ -1,0 +1,66 @@
+"""Host-visible throughput of the drop-in path: topics/s
+from a host topic blob to a host CSR result, through egm_match_submit /
+egm_match_wait (pinned staging, H2D on a copy stream, match, D2H), with two
+batches in flight — the PCIe-inclusive rate the NIF sees, never bench.py's
+`value`.
+
+    python tools/bench_host.py [--config c2] [--batch 1000000] [--batches 20]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--filters", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=1_000_000)
+    ap.add_argument("--batches", type=int, default=20)
+    a = ap.parse_args()
+    from emqx_amd import _lib as L
+    from emqx_amd import synth
+    from emqx_amd.engine import GpuMatcher
+    import numpy as np
+    c = synth.CONFIGS[a.config]
+    seed = synth.SEED_BASE + synth.CONFIG_INDEX[a.config]
+    f = synth.filters(a.filters or c["n_filters"], c["dmin"], c["dmax"], c["wc"], c["p_plus"], c["p_hash"],
+                      seed=seed)
+    t = synth.topics(a.batch * 2, f, c["dmin"], c["dmax"], seed=seed)
+    halves = [t.subset(np.arange(0, a.batch)), t.subset(np.arange(a.batch, 2 * a.batch))]
+    gm = GpuMatcher(0, max_batch=a.batch)
+    gm.build(f.blob, f.off)
+    mode = L.EGM_MODE_ROUTES
+    for h in halves:   # warm up: size the buffers
+        gm.wait(gm.submit(h.blob, h.off, mode), copy=False)
+    out = {}
+    for depth in (1, 2):
+        ids = 0
+        t0 = time.perf_counter()
+        inflight = []
+        for k in range(a.batches):
+            inflight.append(gm.submit(halves[k % 2].blob, halves[k % 2].off, mode))
+            if len(inflight) == depth:
+                gm.wait(inflight.pop(0), copy=False)
+                ids += gm.last_stats()["n_ids"]
+        while inflight:
+            gm.wait(inflight.pop(0), copy=False)
+            ids += gm.last_stats()["n_ids"]
+        dt = time.perf_counter() - t0
+        out[f"in_flight_{depth}"] = {"topics_per_s": a.batch * a.batches / dt, "ms_per_batch": dt / a.batches * 1e3,
+                                     "ids_per_batch": ids / a.batches,
+                                     "result_bytes_per_batch": ids / a.batches * 4 + (a.batch + 1) * 8 + a.batch,
+                                     "input_bytes_per_batch": int(halves[0].off[-1]) + 4 * (a.batch + 1)}
+    gm.close()
+    line = {"what": "host_e2e: host topic blob -> host CSR (egm_match_submit/egm_match_wait, pinned staging)",
+            "config": a.config, "filters": f.n, "batch": a.batch, "batches": a.batches, **out}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
