@@ -14,6 +14,14 @@
  *   match_batch/3   -> egm_match_batch     (emqx_trie:match/1 and the filter set of
  *                      emqx_router:match_routes/1 — emqx_router.erl:129-141 — for a
  *                      list of publish topics; returns [[FilterId]])
+ *   submit/3, wait/2 -> egm_match_submit / egm_match_wait (the batcher's pipeline:
+ *                      submit returns a ticket at once, wait blocks for its rows)
+ *   subs_build/2    -> egm_subs_build      (filter id -> subscriber ids: the
+ *                      emqx_subscriber bag flattened, emqx_broker.erl:116-162)
+ *   publish_batch/2 -> egm_match_batch (routes mode) + egm_fanout_batch: the
+ *                      match_routes/1 + dispatch/2 expansion of emqx_broker:publish/1
+ *                      (emqx_broker.erl:200-209, 283-308) for a list of topics;
+ *                      returns [{[FilterId], [{FilterId, Sub}]}]
  *
  * Threading: match_batch and apply_delta run on dirty CPU schedulers
  * (ERL_NIF_DIRTY_JOB_CPU_BOUND) — a batch takes well over 1 ms.  The library
@@ -171,6 +179,18 @@ static ERL_NIF_TERM nif_apply_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM
   return enif_make_tuple2(env, ATOM_OK, enif_make_uint64(env, epoch));
 }
 
+/* Rows of a CSR as [[Id]] (shared by match_batch and wait). */
+static ERL_NIF_TERM rows_term(ErlNifEnv* env, const egm_result* res) {
+  ERL_NIF_TERM rows = enif_make_list(env, 0);
+  for (uint32_t i = res->n_topics; i-- > 0;) {
+    ERL_NIF_TERM row = enif_make_list(env, 0);
+    for (uint64_t k = res->row_ptr[i + 1]; k-- > res->row_ptr[i];)
+      row = enif_make_list_cell(env, enif_make_uint(env, res->ids[k]), row);
+    rows = enif_make_list_cell(env, row, rows);
+  }
+  return rows;
+}
+
 /* match_batch(Ctx, [Topic :: binary()], Mode :: 0 | 1) -> {ok, [[Id]]} | {error, _} */
 static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   egm_res_t* r;
@@ -185,16 +205,126 @@ static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM
   free(blob);
   free(off);
   if (rc && !res) return error_tuple(env, r->ctx, rc);
-  ERL_NIF_TERM rows = enif_make_list(env, 0);
+  if (rc) {
+    egm_result_free(res);
+    return error_tuple(env, r->ctx, rc);
+  }
+  ERL_NIF_TERM rows = rows_term(env, res);
+  egm_result_free(res);
+  return enif_make_tuple2(env, ATOM_OK, rows);
+}
+
+/* submit(Ctx, [Topic], Mode) -> {ok, Ticket} | {error, _}: the topics are
+   staged in pinned memory before it returns. */
+static ERL_NIF_TERM nif_submit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  egm_res_t* r;
+  int mode;
+  uint8_t* blob;
+  uint32_t *off, n;
+  if (argc != 3 || !get_ctx(env, argv[0], &r) || !enif_get_int(env, argv[2], &mode) ||
+      (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES) || !pack_list(env, argv[1], &blob, &off, &n))
+    return enif_make_badarg(env);
+  uint64_t ticket = 0;
+  int rc = egm_match_submit(r->ctx, blob, off, n, mode, &ticket);
+  free(blob);
+  free(off);
+  if (rc) return error_tuple(env, r->ctx, rc);
+  return enif_make_tuple2(env, ATOM_OK, enif_make_uint64(env, ticket));
+}
+
+/* wait(Ctx, Ticket) -> {ok, [[Id]]} | {error, _} */
+static ERL_NIF_TERM nif_wait(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  egm_res_t* r;
+  ErlNifUInt64 ticket;
+  if (argc != 2 || !get_ctx(env, argv[0], &r) || !enif_get_uint64(env, argv[1], &ticket))
+    return enif_make_badarg(env);
+  egm_result* res = NULL;
+  int rc = egm_match_wait(r->ctx, ticket, &res);
+  if (rc) {
+    if (res) egm_result_free(res);
+    return error_tuple(env, r->ctx, rc);
+  }
+  ERL_NIF_TERM rows = rows_term(env, res);
+  egm_result_free(res);
+  return enif_make_tuple2(env, ATOM_OK, rows);
+}
+
+/* subs_build(Ctx, [[Sub]]) -> ok | {error, _}: list position = filter id; a
+   shared group is the integer GroupId bor 16#80000000. */
+static ERL_NIF_TERM nif_subs_build(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  egm_res_t* r;
+  unsigned nf;
+  if (argc != 2 || !get_ctx(env, argv[0], &r) || !enif_get_list_length(env, argv[1], &nf))
+    return enif_make_badarg(env);
+  uint64_t* row = (uint64_t*)malloc(((size_t)nf + 1) * sizeof(uint64_t));
+  if (!row) return enif_make_badarg(env);
+  ERL_NIF_TERM head, tail = argv[1];
+  row[0] = 0;
+  for (unsigned i = 0; i < nf; ++i) {
+    unsigned len;
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_list_length(env, head, &len)) {
+      free(row);
+      return enif_make_badarg(env);
+    }
+    row[i + 1] = row[i] + len;
+  }
+  uint32_t* subs = (uint32_t*)malloc((size_t)(row[nf] ? row[nf] : 1) * sizeof(uint32_t));
+  if (!subs) {
+    free(row);
+    return enif_make_badarg(env);
+  }
+  tail = argv[1];
+  for (unsigned i = 0; i < nf; ++i) {
+    ERL_NIF_TERM h2, t2;
+    enif_get_list_cell(env, tail, &head, &tail);
+    t2 = head;
+    for (uint64_t k = row[i]; k < row[i + 1]; ++k) {
+      unsigned v;
+      if (!enif_get_list_cell(env, t2, &h2, &t2) || !enif_get_uint(env, h2, &v)) {
+        free(row);
+        free(subs);
+        return enif_make_badarg(env);
+      }
+      subs[k] = v;
+    }
+  }
+  int rc = egm_subs_build(r->ctx, row, nf, subs);
+  free(row);
+  free(subs);
+  return rc ? error_tuple(env, r->ctx, rc) : ATOM_OK;
+}
+
+/* publish_batch(Ctx, [Topic]) -> {ok, [{[FilterId], [{FilterId, Sub}]}]} | {error, _} */
+static ERL_NIF_TERM nif_publish_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  egm_res_t* r;
+  uint8_t* blob;
+  uint32_t *off, n;
+  if (argc != 2 || !get_ctx(env, argv[0], &r) || !pack_list(env, argv[1], &blob, &off, &n))
+    return enif_make_badarg(env);
+  egm_result* res = NULL;
+  egm_delivery* dl = NULL;
+  int rc = egm_match_batch(r->ctx, blob, off, n, EGM_MODE_ROUTES, &res);
+  free(blob);
+  free(off);
+  if (!rc) rc = egm_fanout_batch(r->ctx, res, &dl);
+  if (rc) {
+    if (res) egm_result_free(res);
+    if (dl) egm_result_free(dl);
+    return error_tuple(env, r->ctx, rc);
+  }
+  ERL_NIF_TERM out = enif_make_list(env, 0);
   for (uint32_t i = n; i-- > 0;) {
-    ERL_NIF_TERM row = enif_make_list(env, 0);
+    ERL_NIF_TERM ids = enif_make_list(env, 0), dv = enif_make_list(env, 0);
     for (uint64_t k = res->row_ptr[i + 1]; k-- > res->row_ptr[i];)
-      row = enif_make_list_cell(env, enif_make_uint(env, res->ids[k]), row);
-    rows = enif_make_list_cell(env, row, rows);
+      ids = enif_make_list_cell(env, enif_make_uint(env, res->ids[k]), ids);
+    for (uint64_t k = dl->row_ptr[i + 1]; k-- > dl->row_ptr[i];)
+      dv = enif_make_list_cell(
+          env, enif_make_tuple2(env, enif_make_uint(env, dl->fid[k]), enif_make_uint(env, dl->sub[k])), dv);
+    out = enif_make_list_cell(env, enif_make_tuple2(env, ids, dv), out);
   }
   egm_result_free(res);
-  if (rc) return error_tuple(env, r->ctx, rc);
-  return enif_make_tuple2(env, ATOM_OK, rows);
+  egm_result_free(dl);
+  return enif_make_tuple2(env, ATOM_OK, out);
 }
 
 static ErlNifFunc nif_funcs[] = {
@@ -202,6 +332,10 @@ static ErlNifFunc nif_funcs[] = {
     {"build", 2, nif_build, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"apply_delta", 3, nif_apply_delta, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"match_batch", 3, nif_match_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"submit", 3, nif_submit, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"wait", 2, nif_wait, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"subs_build", 2, nif_subs_build, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"publish_batch", 2, nif_publish_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
 };
 
 ERL_NIF_INIT(emqx_gpu_match, nif_funcs, load, NULL, NULL, NULL)

@@ -12,6 +12,17 @@ Delivery entries:
   ("group", filter, group, member)           $share group, one member picked
   ("node", filter, node)                     route to another node (forward)
 
+``publish_result`` / ``publish_result_batch`` return what ``publish/1``
+returns (``emqx_types:publish_result()``): one entry per aggregated route
+(``aggre/1``, :249-260) — ``(node, filter, {ok, N} | {error, no_subscribers})``
+for this node (``dispatch/2``, :283-295: N alive subscribers), ``(node,
+filter, "forward")`` for another node (async ``forward/4``, :265-271), and
+``("share", filter, {ok, 1} | {error, no_subscribers})`` per $share group
+(emqx_shared_sub.erl:120-127) — and keep the reference's metrics: a message
+with no route, or a local route none of whose subscribers is alive, counts
+``messages.dropped`` and ``messages.dropped.no_subscribers`` (not for a
+system message, ``inc_dropped_cnt/1`` :311-316, emqx_message.erl:173-177).
+
 Subscriber sharding ({shard, Topic, I} bags beyond 1024 subscribers,
 emqx_broker.erl:149-157, emqx_broker_helper.erl:82-86) changes only the layout
 of the reference's ETS bags, never the delivery set; the fan-out CSR is the
@@ -52,6 +63,14 @@ class Broker:
         self._sticky: Dict[Tuple[bytes, bytes], int] = {}
         self._shards = shards
         self._csr_dirty = True
+        self.dead: set = set()   # subscribers whose process is gone (is_process_alive/1 false)
+        self.metrics = {"messages.publish": 0, "messages.dropped": 0, "messages.dropped.no_subscribers": 0,
+                        "messages.forward": 0}
+
+    def kill(self, sub_id: int):
+        """The subscriber's process exits without unsubscribing: dispatch/3
+        skips it (emqx_broker.erl:297-302) until it unsubscribes."""
+        self.dead.add(sub_id)
 
     # -- subscribe side (emqx_broker.erl:116-162, emqx_shared_sub.erl:108-109) --
     def subscribe(self, topic: bytes, sub_id: int, opts: Optional[dict] = None, clientid: Optional[bytes] = None):
@@ -149,14 +168,71 @@ class Broker:
             out.append(dl)
         return out
 
-    def _pick(self, group: bytes, flt: bytes, source_topic: bytes, clientid: bytes) -> Optional[int]:
+    @staticmethod
+    def _is_sys(topic: bytes, sys_flag: bool) -> bool:
+        return sys_flag or topic.startswith(b"$SYS/")
+
+    def _dropped(self, topic: bytes, sys_flag: bool):
+        if not self._is_sys(topic, sys_flag):
+            self.metrics["messages.dropped"] += 1
+            self.metrics["messages.dropped.no_subscribers"] += 1
+
+    def publish_result(self, topic: bytes, clientid: bytes = b"", sys: bool = False) -> List[tuple]:
+        return self.publish_result_batch([topic], [clientid], [sys])[0]
+
+    def publish_result_batch(self, topics: Sequence[bytes], clientids: Optional[Sequence[bytes]] = None,
+                             sys_flags: Optional[Sequence[bool]] = None) -> List[List[tuple]]:
+        """``publish/1`` results for a batch (see the module docstring)."""
+        self._upload_csr()
+        r = self.router
+        res = r.match_filters_batch(topics)
+        drow, dfid, dsub = r.m.fanout(res)
+        out = []
+        for k, t in enumerate(topics):
+            sysf = bool(sys_flags[k]) if sys_flags else False
+            if not self._is_sys(t, sysf):
+                self.metrics["messages.publish"] += 1
+            alive: Dict[int, int] = {}
+            for j in range(int(drow[k]), int(drow[k + 1])):
+                s = int(dsub[j])
+                if not s & GROUP_BIT and s not in self.dead:
+                    f = int(dfid[j])
+                    alive[f] = alive.get(f, 0) + 1
+            entries: List[tuple] = []
+            groups = set()
+            for fid in res.row(k).tolist():
+                f = r.filter_of(fid)
+                for d in r.routes[f]:
+                    if isinstance(d, tuple) and d[0] == "group":
+                        groups.add((f, d[1]))
+                    elif d == self.node:
+                        n = alive.get(fid, 0)
+                        if n:
+                            entries.append((d, f, ("ok", n)))
+                        else:
+                            self._dropped(t, sysf)
+                            entries.append((d, f, ("error", "no_subscribers")))
+                    else:
+                        self.metrics["messages.forward"] += 1
+                        entries.append((d, f, "forward"))
+            for f, g in sorted(groups):   # aggre/1 usorts the {Topic, Group} entries
+                live = [m for m in self.shared.get((g, f), []) if m not in self.dead]
+                m = self._pick(g, f, t, clientids[k] if clientids else b"", live)
+                entries.append(("share", f, ("ok", 1) if m is not None else ("error", "no_subscribers")))
+            if not entries:   # route([], Delivery)
+                self._dropped(t, sysf)
+            out.append(entries)
+        return out
+
+    def _pick(self, group: bytes, flt: bytes, source_topic: bytes, clientid: bytes,
+              members: Optional[List[int]] = None) -> Optional[int]:
         """``pick/6`` + ``do_pick_subscriber/6`` (emqx_shared_sub.erl:239-290).
 
         phash2 (ERTS) is replaced by crc32: the member a hash strategy picks is
         therefore not the reference's (parity is at (filter, group) level,
         SURVEY §8c); each strategy keeps its reference behaviour otherwise.
         """
-        mem = self.shared.get((group, flt))
+        mem = self.shared.get((group, flt)) if members is None else members
         if not mem:
             return None
         n = len(mem)

@@ -87,17 +87,19 @@ struct PinBuf {
 // caller reads until egm_result_free.
 struct PipeSlot {
   bool busy = false;     // submitted, not yet waited for
+  bool waiting = false;  // a thread is in egm_match_wait for it
   bool held = false;     // its result is with the caller
   uint32_t n = 0;
   int mode = 0;
   uint64_t bytes = 0, maxlen = 0, cap = 0;
   PinBuf h_in, h_out, h_stats;
-  DevBuf d_blob, d_off, d_row, d_ids, d_flags;
-  hipEvent_t ev_in = nullptr, ev_done = nullptr;
+  DevBuf d_blob, d_off, d_row, d_ids, d_flags, d_cnt;
+  hipEvent_t ev_in = nullptr, ev_done = nullptr, ev_out = nullptr;
   uint64_t epoch = 0;
   ~PipeSlot() {
     if (ev_in) hipEventDestroy(ev_in);
     if (ev_done) hipEventDestroy(ev_done);
+    if (ev_out) hipEventDestroy(ev_out);
   }
 };
 constexpr size_t PIPE_MAX_SLOTS = 8;
@@ -188,7 +190,8 @@ struct egm_ctx {
   }
   // host pipeline (egm_match_submit / egm_match_wait)
   std::vector<std::unique_ptr<PipeSlot>> pipe;
-  hipStream_t copy_stream = nullptr;
+  hipStream_t copy_stream = nullptr;   // pipeline host->device copies
+  hipStream_t d2h_stream = nullptr;    // pipeline device->host copies (PCIe is full duplex)
   // last fan-out (egm_last_fanout)
   const uint64_t* fan_drow = nullptr;
   uint32_t fan_topics = 0;
@@ -649,9 +652,11 @@ void egm_close(egm_ctx* c) {
     if (c->work_ev) hipEventDestroy(c->work_ev);
     c->work_ev = nullptr;
     if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
+    if (c->d2h_stream) hipStreamSynchronize(c->d2h_stream);
     c->pipe.clear();
     if (c->copy_stream) hipStreamDestroy(c->copy_stream);
-    c->copy_stream = nullptr;
+    if (c->d2h_stream) hipStreamDestroy(c->d2h_stream);
+    c->copy_stream = c->d2h_stream = nullptr;
   }
   hipStreamDestroy(c->stream);
   delete c;
@@ -854,6 +859,7 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   if ((e = S.d_row.ensure((n + 1) * 8)) != hipSuccess) return c->hip_fail(e, "pipe row");
   if ((e = S.d_ids.ensure((S.cap + 1) * 4)) != hipSuccess) return c->hip_fail(e, "pipe ids");
   if ((e = S.d_flags.ensure(n + 8)) != hipSuccess) return c->hip_fail(e, "pipe flags");
+  if ((e = S.d_cnt.ensure(n * 4 + 16)) != hipSuccess) return c->hip_fail(e, "pipe counts");
   if ((e = S.h_stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "pipe stats");
   if ((e = hipStreamWaitEvent(s, S.ev_in, 0)) != hipSuccess) return c->hip_fail(e, "pipe wait input");
   r = run_match(c, *ep, S.d_blob.as<uint8_t>(), S.d_off.as<uint32_t>(), S.n, S.mode, s, S.d_row.as<uint64_t>(),
@@ -861,6 +867,7 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   if (r) return r;
   c->last_pending = false;   // this batch's counters travel with the slot
   if ((n && (e = hipMemcpyAsync(S.d_flags.p, c->tfl.p, n, hipMemcpyDeviceToDevice, s)) != hipSuccess) ||
+      (n && (e = hipMemcpyAsync(S.d_cnt.p, c->cnt.p, n * 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) ||
       (e = hipMemcpyAsync(S.h_stats.p, c->stats.p, sizeof(MatchStats), hipMemcpyDeviceToHost, s)) != hipSuccess ||
       (e = hipEventRecord(S.ev_done, s)) != hipSuccess)
     return c->hip_fail(e, "pipe epilogue");
@@ -875,6 +882,8 @@ int egm_match_submit(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint3
   hipError_t e;
   if (!c->copy_stream && (e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking)) != hipSuccess)
     return c->hip_fail(e, "copy stream");
+  if (!c->d2h_stream && (e = hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking)) != hipSuccess)
+    return c->hip_fail(e, "d2h stream");
   size_t k = 0;
   while (k < c->pipe.size() && (c->pipe[k]->busy || c->pipe[k]->held)) ++k;
   if (k == c->pipe.size()) {
@@ -882,7 +891,8 @@ int egm_match_submit(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint3
     c->pipe.emplace_back(new PipeSlot());
     PipeSlot& N = *c->pipe.back();
     if (hipEventCreateWithFlags(&N.ev_in, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&N.ev_done, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&N.ev_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&N.ev_out, hipEventDisableTiming) != hipSuccess)
       return c->fail(EGM_E_DEVICE, "pipe events");
   }
   PipeSlot& S = *c->pipe[k];
@@ -918,30 +928,36 @@ int egm_match_submit(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint3
   return EGM_OK;
 }
 
+// The device syncs happen without the context lock, so another thread can
+// submit (stage + enqueue) the next batch while this one waits.
 int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   if (!c || !out || ticket == 0) return EGM_E_INVAL;
   *out = nullptr;
-  std::lock_guard<std::recursive_mutex> g(c->mu);
-  if (ticket > c->pipe.size() || !c->pipe[ticket - 1]->busy) return c->fail(EGM_E_STATE, "unknown ticket");
+  std::unique_lock<std::recursive_mutex> g(c->mu);
+  if (ticket > c->pipe.size() || !c->pipe[ticket - 1]->busy || c->pipe[ticket - 1]->waiting)
+    return c->fail(EGM_E_STATE, "unknown ticket");
   if (set_device(c)) return EGM_E_DEVICE;
   PipeSlot& S = *c->pipe[ticket - 1];
+  S.waiting = true;
+  auto done = [&](int rc) {   // the slot is free again (its result, if any, held by the caller)
+    if (!g.owns_lock()) g.lock();
+    S.busy = S.waiting = false;
+    return rc;
+  };
   hipError_t e;
   MatchStats st{};
   for (int attempt = 0;; ++attempt) {
-    if ((e = hipEventSynchronize(S.ev_done)) != hipSuccess) return c->hip_fail(e, "pipe wait");
+    g.unlock();
+    e = hipEventSynchronize(S.ev_done);
+    g.lock();
+    if (e != hipSuccess) return done(c->hip_fail(e, "pipe wait"));
     st = *(const MatchStats*)S.h_stats.p;
     if (!st.overflow) break;
-    if (attempt == 2 || (st.overflow & ~3u)) {
-      S.busy = false;
-      return c->fail(EGM_E_NOMEM, "ids capacity");
-    }
+    if (attempt == 2 || (st.overflow & ~3u)) return done(c->fail(EGM_E_NOMEM, "ids capacity"));
     // the exact total is known even on overflow: rerun the staged batch once with room for it
     S.cap = st.total_ids + st.total_ids / 8 + 1024;
-    int r = pipe_launch(c, S);
-    if (r) {
-      S.busy = false;
-      return r;
-    }
+    const int r = pipe_launch(c, S);
+    if (r) return done(r);
   }
   c->last = st;   // egm_last_stats reports the waited batch
   const uint64_t n = S.n, nids = st.total_ids;
@@ -949,10 +965,7 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   const size_t o_res = sizeof(ResultHdr), o_cnt = (o_res + sizeof(egm_result) + 15) & ~(size_t)15,
                o_row = (o_cnt + n * 4 + 15) & ~(size_t)15, o_ids = o_row + (n + 1) * 8,
                o_fl = (o_ids + nids * 4 + 15) & ~(size_t)15, total = o_fl + n + 16;
-  if ((e = S.h_out.ensure(total)) != hipSuccess) {
-    S.busy = false;
-    return c->hip_fail(e, "pipe pinned result");
-  }
+  if ((e = S.h_out.ensure(total)) != hipSuccess) return done(c->hip_fail(e, "pipe pinned result"));
   uint8_t* h = (uint8_t*)S.h_out.p;
   ResultHdr* hdr = (ResultHdr*)h;
   egm_result* res = (egm_result*)(h + o_res);
@@ -966,27 +979,29 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   res->epoch = S.epoch;
   res->visited = st.visited;
   res->n_error = st.errors;
-  if ((e = hipMemcpyAsync(res->row_ptr, S.d_row.p, (n + 1) * 8, hipMemcpyDeviceToHost, c->copy_stream)) !=
-          hipSuccess ||
-      (nids && (e = hipMemcpyAsync(res->ids, S.d_ids.p, nids * 4, hipMemcpyDeviceToHost, c->copy_stream)) !=
-                   hipSuccess) ||
-      (n && (e = hipMemcpyAsync(res->flags, S.d_flags.p, n, hipMemcpyDeviceToHost, c->copy_stream)) != hipSuccess) ||
-      (e = hipStreamSynchronize(c->copy_stream)) != hipSuccess) {
-    S.busy = false;
-    return c->hip_fail(e, "pipe D2H");
-  }
-  S.busy = false;
-  if (res->row_ptr[n] != nids) return c->fail(EGM_E_DEVICE, "row_ptr total mismatch");
+  hipStream_t d = c->d2h_stream;
+  if ((e = hipMemcpyAsync(res->row_ptr, S.d_row.p, (n + 1) * 8, hipMemcpyDeviceToHost, d)) != hipSuccess ||
+      (nids && (e = hipMemcpyAsync(res->ids, S.d_ids.p, nids * 4, hipMemcpyDeviceToHost, d)) != hipSuccess) ||
+      (n && (e = hipMemcpyAsync(res->counts, S.d_cnt.p, n * 4, hipMemcpyDeviceToHost, d)) != hipSuccess) ||
+      (n && (e = hipMemcpyAsync(res->flags, S.d_flags.p, n, hipMemcpyDeviceToHost, d)) != hipSuccess) ||
+      (e = hipEventRecord(S.ev_out, d)) != hipSuccess)
+    return done(c->hip_fail(e, "pipe D2H"));
+  g.unlock();
+  e = hipEventSynchronize(S.ev_out);
   uint32_t heavy = 0;
-  for (uint64_t i = 0; i < n; ++i) {
-    res->counts[i] = (uint32_t)(res->row_ptr[i + 1] - res->row_ptr[i]);
-    heavy += (res->flags[i] & TF_HEAVY) ? 1 : 0;
+  if (e == hipSuccess) {
+    const uint8_t* fl = res->flags;
+    for (uint64_t i = 0; i < n; ++i) heavy += (fl[i] & TF_HEAVY) ? 1u : 0u;
   }
+  g.lock();
+  if (e != hipSuccess) return done(c->hip_fail(e, "pipe D2H"));
+  if (res->row_ptr[n] != nids) return done(c->fail(EGM_E_DEVICE, "row_ptr total mismatch"));
   res->n_heavy = heavy;
   hdr->magic = RES_PIPE;
   hdr->owner = c;
   hdr->slot = ticket - 1;
   S.held = true;
+  done(EGM_OK);
   *out = res;
   if (res->n_error) {
     c->err = "some topics could not be walked (flag EGM_TF_ERROR)";
@@ -1002,7 +1017,6 @@ int egm_match_batch(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32
                     egm_result** out) {
   if (!c || !out) return EGM_E_INVAL;
   *out = nullptr;
-  std::lock_guard<std::recursive_mutex> g(c->mu);
   uint64_t t = 0;
   int r = egm_match_submit(c, blob, off, n, mode, &t);
   if (r) return r;

@@ -412,15 +412,28 @@ constexpr uint32_t WPS = EGM_WALK_WPS;
 #endif
 constexpr uint32_t WALK_STACK = EGM_WALK_STACK;
 constexpr uint32_t WALK_STAGE = EGM_WALK_STAGE;
-constexpr uint32_t SLOTS = 64;                       // topics in flight per wave (slot = lane)
+constexpr uint32_t SLOTS = 64;                       // topic slots per wave (slot = lane)
+#ifndef EGM_WALK_ADMIT
+#define EGM_WALK_ADMIT 64    // new topics enter while the stack holds fewer items than this
+#endif
+#ifndef EGM_WALK_LIVE
+#define EGM_WALK_LIVE 32     // ... and fewer topics than this are in flight
+#endif
+#ifndef EGM_WALK_WPE
+#define EGM_WALK_WPE 4       // waves per SIMD the walk is compiled for (<= 128 VGPRs)
+#endif
+constexpr uint32_t WALK_ADMIT = EGM_WALK_ADMIT;
+constexpr uint32_t WALK_LIVE = EGM_WALK_LIVE;
 constexpr uint32_t SLOT_BITS = 6;
-// The pop bound below keeps room >= dmax after every iteration and a refill
-// fills the stack to at most 64 items, so the stack cannot overflow while
-// 64 + dmax <= WALK_STACK.  Chunks with a deeper topic go to k_heavy.
+// The pop bound below keeps room >= dmax once the batch in flight has
+// landed, and admission adds roots only within the same bound, so the stack
+// cannot overflow.  Chunks with a topic deeper than LIGHT_DMAX go to k_heavy
+// (an empty wave can always admit: 64 + dmax <= WALK_STACK).
 constexpr uint32_t LIGHT_DMAX = WALK_STACK - 64;
 static_assert(SLOTS == 64 && (1u << SLOT_BITS) == SLOTS && WALK_CHUNK == 64, "one slot, one prefetched topic per lane");
 static_assert(WALK_STAGE >= 256 && WALK_STAGE <= 256, "stage: 4 emits x 64 lanes per step; u8 ranks and starts");
 static_assert(LIGHT_DMAX >= 16, "stack too small");
+static_assert(WALK_ADMIT <= 64 && WALK_LIVE >= 1 && WALK_LIVE <= SLOTS, "a refill adds at most 64 items");
 
 struct alignas(16) WaveLds {
   uint4 stack[WALK_STACK];
@@ -436,7 +449,9 @@ struct alignas(16) WaveLds {
   uint32_t live[SLOTS];            // the topic's items in the stack (or being expanded)
   uint32_t tid[SLOTS];             // the topic's index in the batch
   uint32_t finmask[2];             // slots whose topic finished this iteration
+  uint32_t stmask[2];              // slots that staged an emit this iteration
 };
+
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
 // readfirstlane returns int: widen each half as unsigned (a sign-extended low
@@ -565,7 +580,8 @@ struct Pend {
   uint4 it;                 // the item
   uint32_t D, nw;           // its topic's depth, the word at level + 1
   bool act, lit, plus, d1;  // d1: a one-word '$' topic (do_match/1's lookup_topic probe)
-  uint4 prec, l0, h0, l1, h1;
+  uint4 prec, l0, l1;
+  uint3 h0, h1;             // the slots' child record copies (12 of 16 bytes)
 };
 
 // Branch-free on purpose: every lane issues its loads unconditionally (an
@@ -582,9 +598,9 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* __res
   p.prec = ld16(tab.nodes + (p.plus ? p.it.z : 0u));
   const uint8_t* bp = (const uint8_t*)(tab.edges + (size_t)(p.lit ? bkt : 0u) * EDGE_BUCKET);
   p.l0 = ld16(bp);
-  p.h0 = ld16(bp + 16);
+  p.h0 = *(const uint3*)(bp + 16);
   p.l1 = ld16(bp + 32);
-  p.h1 = ld16(bp + 48);
+  p.h1 = *(const uint3*)(bp + 48);
   // the next level's word (clamped; used only if level + 1 < D)
   const uint32_t level = meta & LEVEL_MAX;
   // from the LDS stage for the first WPS levels, else from HBM (deep topics;
@@ -700,6 +716,7 @@ __device__ __forceinline__ uint32_t root_flags(uint4 root, bool dollar, uint32_t
 // such a loop made the structurizer give the lanes different exits).
 struct Prefetch {
   uint32_t t0, nt, next;    // wave-uniform: first topic, topics, next to admit
+  uint32_t dmax;            // wave-uniform: the chunk's deepest topic
   uint32_t D, f, base;      // lane j: topic t0 + j
   uint32_t wv[WPS];
 };
@@ -708,7 +725,7 @@ __device__ __forceinline__ void prefetch_chunk(Prefetch& P, const uint32_t* __re
                                                const uint32_t* __restrict__ wid, uint32_t n, uint32_t nchunks,
                                                uint32_t lane) {
   ConstWork& w = *fresh();
-  P.t0 = P.nt = P.next = 0;
+  P.t0 = P.nt = P.next = P.dmax = 0;
   uint32_t guard = 0;
   while (++guard < (1u << EGM_GUARD_BITS)) {
     uint32_t c = 0;
@@ -735,6 +752,7 @@ __device__ __forceinline__ void prefetch_chunk(Prefetch& P, const uint32_t* __re
     } else {
       P.t0 = t0;
       P.nt = nt;
+      P.dmax = dmax;
       P.D = D;
       P.f = f;
       P.base = base;
@@ -759,7 +777,7 @@ __device__ __forceinline__ uint32_t slots_dmax(const WaveLds& L, uint64_t held, 
 // item left (and none of whose emits is still staged) is retired — counts
 // and piece head written — and refilled at once: the stack never drains
 // between topics or chunks.
-__global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const uint32_t* __restrict__ wid,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(EGM_WALK_WPE, 8))) void k_walk(MatchWork wk, DevTable tab, const uint32_t* __restrict__ wid,
                                              const uint32_t* __restrict__ off, uint32_t n, int mode) {
   __shared__ WaveLds L;
   const uint32_t lane = threadIdx.x;
@@ -774,11 +792,18 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
   Slab sid{0, 0}, spc{0, 0};
   L.fcnt[lane] = 0;   // slot = lane
   L.live[lane] = 0;
-  if (lane < 2) L.finmask[lane] = 0;
+  if (lane < 2) {
+    L.finmask[lane] = 0;
+    L.stmask[lane] = 0;
+  }
   Prefetch P;
   prefetch_chunk(P, off, wid, n, nchunks, lane);
-  uint64_t freem = ~0ull, donem = 0;   // slots: free; done (no item left) but not yet retired
+  // slots: free; done (no item left) but not yet retired; with emits in the stage
+  uint64_t freem = ~0ull, donem = 0, stagedm = 0;
   uint32_t sp = 0, nstage = 0, dmax = 0;
+  Pend pa;           // batch A: popped, reads in flight
+  pa.act = false;
+  uint32_t ka = 0;   // its items (wave-uniform)
   uint32_t guard = 0;   // every loop of the kernel is bounded: a bug reports, it never hangs the GPU
   for (;;) {
     if (++guard > (1u << EGM_GUARD_BITS)) {
@@ -788,14 +813,17 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
     const bool more = P.next < P.nt;
     // ---- the one flush point of the loop top: room for 64 root emits, done
     // slots to recycle, or the end ----
-    if (nstage && (nstage + 64u > WALK_STAGE || (donem && (!freem || (sp == 0 && !more))) ||
-                   (donem && sp < 64u && popc(freem) < 8u))) {
+    const uint64_t held = donem & stagedm;   // done, but its last emits are still staged
+    const uint32_t busy = SLOTS - popc(freem);   // slots in flight or awaiting retirement
+    if (nstage && (nstage + 64u > WALK_STAGE || (held && (busy >= WALK_LIVE || (sp == 0 && ka == 0 && !more))) ||
+                   (held && sp < WALK_ADMIT && busy + 8u > WALK_LIVE))) {
       flush_stage(L, nstage, lane, sid, spc);
       nstage = 0;
+      stagedm = 0;
     }
     // ---- retire done slots with nothing staged ----
     {
-      const uint64_t rm = __ballot(((donem >> lane) & 1) && L.fcnt[lane] == 0);
+      const uint64_t rm = donem & ~stagedm;
       if (rm) {
         if ((rm >> lane) & 1) {
           ConstWork& w = *fresh();
@@ -809,8 +837,12 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
       }
     }
     // ---- admission: new topics into free slots while the stack is short ----
-    if (sp < 64u && freem && more) {
-      const uint32_t k = min(min(64u - sp, popc(freem)), P.nt - P.next);
+    const uint32_t inflight = SLOTS - popc(freem);
+    // (the new roots must leave room for batch A's children and the deepest
+    // topic's DFS: sp + 2 ka + dmax <= WALK_STACK after admission)
+    const int alim = (int)WALK_STACK - (int)max(dmax, P.dmax) - (int)sp - 2 * (int)ka;
+    if (sp < WALK_ADMIT && inflight < WALK_LIVE && more && alim > 0) {
+      const uint32_t k = min(min(min(WALK_ADMIT - sp, WALK_LIVE - inflight), P.nt - P.next), (uint32_t)alim);
       const bool fr = (freem >> lane) & 1;
       const uint32_t r = mbcnt(freem);               // rank of this free slot
       const bool tk = fr && r < k;                   // slot `lane` takes prefetched topic P.next + r
@@ -848,6 +880,7 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
       if (has) L.stack[sp + mbcnt(b)] = it;
       sp += popc(b);
       const uint64_t be = __ballot(em);
+      stagedm |= be;   // slot = lane
       if (em) {
         const uint32_t q = nstage + mbcnt(be);
         L.stage_fid[q] = fid;
@@ -867,89 +900,103 @@ __global__ __launch_bounds__(64) void k_walk(MatchWork wk, DevTable tab, const u
       wave_sync();
       if (P.next >= P.nt) prefetch_chunk(P, off, wid, n, nchunks, lane);
     }
-    if (sp == 0) {
+    if (sp == 0 && ka == 0) {
       if (!(P.next < P.nt) && !donem) break;   // no topic left, every slot retired
       continue;
     }
 
-    // ---- pop up to 64 items and issue all their reads ----
-    // An item pushes at most two children (net +1), so popping k <= room - dmax
-    // items keeps room >= dmax afterwards; with room <= dmax the wave pops one
-    // item at a time, a plain DFS, whose stack grows by at most one pending
-    // sibling per level below the top item.  So the stack never overflows: a
+    // ---- pop batch B and issue all its reads; then consume batch A, whose
+    // reads were issued one iteration earlier (two batches in flight) ----
+    // An item pushes at most two children.  With batch A (ka items) still to
+    // push, popping kb <= STACK - dmax - sp - 2 ka items leaves room >= dmax
+    // once both have landed; with no batch pending and room <= dmax the wave
+    // pops the top item alone, a plain DFS whose stack grows by at most one
+    // pending sibling per level below it.  So the stack never overflows: a
     // deep, wide frontier (C3: depth 16, '+' p=.35) narrows the wave instead.
-    const uint32_t room = WALK_STACK - sp;
-    const uint32_t lim = room > dmax ? room - dmax : 1u;
-    const uint32_t want = min(64u, sp), take = min(want, lim), bi = sp - take;
-    bounded += take < want ? 1u : 0u;
+    const int lim = (int)WALK_STACK - (int)dmax - (int)sp - 2 * (int)ka;
+    const uint32_t want = min(64u, sp);
+    const uint32_t kb = lim > 0 ? min(want, (uint32_t)lim) : (ka == 0 && sp ? 1u : 0u);
+    bounded += kb < want ? 1u : 0u;
     iters += 1;
-    popped += take;
-    Pend p;
-    p.act = lane < take;
-    p.it = L.stack[min(bi + lane, WALK_STACK - 1)];   // unconditional: see issue()
-    sp = bi;
-    const uint32_t slot = (p.it.y >> MT_SHIFT) & (SLOTS - 1);
-    const uint32_t ti = L.tinfo[slot];
-    p.D = ti & 0xFFFFFFu;
-    p.d1 = p.D == 1 && ((ti >> 24) & TF_DOLLAR);
-    issue(tab, wid, L.tbase[slot], L.words + slot * WPS, p);
+    popped += kb;
+    Pend pb;
+    pb.act = lane < kb;
+    pb.it = L.stack[sp - 1 - min(lane, kb ? kb - 1 : 0u)];   // unconditional: see issue()
+    sp -= kb;
+    {
+      const uint32_t slot = (pb.it.y >> MT_SHIFT) & (SLOTS - 1);
+      const uint32_t ti = L.tinfo[slot];
+      pb.D = ti & 0xFFFFFFu;
+      pb.d1 = pb.D == 1 && ((ti >> 24) & TF_DOLLAR);
+      issue(tab, wid, L.tbase[slot], L.words + slot * WPS, pb);
+    }
     wave_sync();
 
-    // ---- consume: children -> stack, emits -> stage ----
-    Out o;
-    finish(tab, mode, p, o);
-    created += o.created;
-    const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
-    const uint32_t m0 = popc(c0b);
-    if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
-    if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;
-    sp += m0 + popc(c1b);
-    // live items per topic: children first, then the popped item, so the lane
-    // that takes a topic's count to zero is the last one
-    const uint32_t pushes = (o.p0 ? 1u : 0u) + (o.p1 ? 1u : 0u);
-    if (pushes) atomicAdd(&L.live[slot], pushes);
-    wave_sync();
-    if (p.act && atomicSub(&L.live[slot], 1u) == 1u) atomicOr(&L.finmask[slot >> 5], 1u << (slot & 31));
-    // emits (at most 4 per lane): the stage is flushed first if they do not fit
-    {
-      const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
-      const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
-      if (nstage + ne > WALK_STAGE) {
+    if (ka) {   // ---- consume A: children -> stack, emits -> stage ----
+      const uint32_t slot = (pa.it.y >> MT_SHIFT) & (SLOTS - 1);
+      Out o;
+      finish(tab, mode, pa, o);
+      created += o.created;
+      const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
+      const uint32_t m0 = popc(c0b);
+      if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
+      if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;
+      sp += m0 + popc(c1b);
+      // live items per topic: children first, then the popped item, so the
+      // lane that takes a topic's count to zero is the last one
+      const uint32_t pushes = (o.p0 ? 1u : 0u) + (o.p1 ? 1u : 0u);
+      if (pushes) atomicAdd(&L.live[slot], pushes);
+      wave_sync();
+      if (pa.act && atomicSub(&L.live[slot], 1u) == 1u) atomicOr(&L.finmask[slot >> 5], 1u << (slot & 31));
+      // emits (at most 4 per lane): the stage is flushed first if they do not fit
+      {
+        const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
+        const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
+        if (nstage + ne > WALK_STAGE) {
+          wave_sync();
+          flush_stage(L, nstage, lane, sid, spc);
+          nstage = 0;
+          stagedm = 0;
+        }
+        if (o.e0 || o.e1 || o.e2 || o.e3) atomicOr(&L.stmask[slot >> 5], 1u << (slot & 31));
+        const uint8_t st = (uint8_t)slot;
+        if (o.e0) {
+          const uint32_t q = nstage + mbcnt(b0);
+          L.stage_fid[q] = o.f0;
+          L.stage_t[q] = st;
+        }
+        if (o.e1) {
+          const uint32_t q = nstage + n0 + mbcnt(b1);
+          L.stage_fid[q] = o.f1;
+          L.stage_t[q] = st;
+        }
+        if (o.e2) {
+          const uint32_t q = nstage + n1 + mbcnt(b2);
+          L.stage_fid[q] = o.f2;
+          L.stage_t[q] = st;
+        }
+        if (o.e3) {
+          const uint32_t q = nstage + n2 + mbcnt(b3);
+          L.stage_fid[q] = o.f3;
+          L.stage_t[q] = st;
+        }
+        nstage += ne;
+      }
+      wave_sync();
+      {   // topics that finished this iteration
+        const uint64_t fin = ((uint64_t)uni(L.finmask[1]) << 32) | uni(L.finmask[0]);
+        donem |= fin;
+        stagedm |= ((uint64_t)uni(L.stmask[1]) << 32) | uni(L.stmask[0]);
         wave_sync();
-        flush_stage(L, nstage, lane, sid, spc);
-        nstage = 0;
+        if (lane < 2) {
+          L.finmask[lane] = 0;
+          L.stmask[lane] = 0;
+        }
+        wave_sync();
       }
-      const uint8_t st = (uint8_t)slot;
-      if (o.e0) {
-        const uint32_t q = nstage + mbcnt(b0);
-        L.stage_fid[q] = o.f0;
-        L.stage_t[q] = st;
-      }
-      if (o.e1) {
-        const uint32_t q = nstage + n0 + mbcnt(b1);
-        L.stage_fid[q] = o.f1;
-        L.stage_t[q] = st;
-      }
-      if (o.e2) {
-        const uint32_t q = nstage + n1 + mbcnt(b2);
-        L.stage_fid[q] = o.f2;
-        L.stage_t[q] = st;
-      }
-      if (o.e3) {
-        const uint32_t q = nstage + n2 + mbcnt(b3);
-        L.stage_fid[q] = o.f3;
-        L.stage_t[q] = st;
-      }
-      nstage += ne;
     }
-    wave_sync();
-    {   // topics that finished this iteration
-      const uint64_t fin = ((uint64_t)uni(L.finmask[1]) << 32) | uni(L.finmask[0]);
-      donem |= fin;
-      wave_sync();
-      if (lane < 2) L.finmask[lane] = 0;
-      wave_sync();
-    }
+    pa = pb;
+    ka = kb;
   }
   unsigned long long v = created;
 #pragma unroll

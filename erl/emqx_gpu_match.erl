@@ -10,13 +10,13 @@
 %% below fall back to the reference implementation, so semantics never change.
 %%
 %% Not compiled in this repository's CI (no ERTS in the build image); see
-%% INTEGRATION.md for the build line and for the batching process that turns
-%% per-message publish calls into GPU batches.
+%% INTEGRATION.md for the build line; emqx_gpu_batch is the batching process
+%% that turns per-message publish calls into pipelined GPU batches.
 %%--------------------------------------------------------------------
 -module(emqx_gpu_match).
 
--export([open/1, build/2, apply_delta/3, match_batch/3]).
--export([init/0, insert/1, delete/1, match/1, match_routes/1]).
+-export([open/1, build/2, apply_delta/3, match_batch/3, submit/3, wait/2, subs_build/2, publish_batch/2]).
+-export([init/0, ctx/0, filter_of/1, insert/1, delete/1, match/1, match_routes/1]).
 
 -on_load(load_nif/0).
 
@@ -36,6 +36,10 @@ open(_Device) -> erlang:nif_error(nif_not_loaded).
 build(_Ctx, _Filters) -> erlang:nif_error(nif_not_loaded).
 apply_delta(_Ctx, _Inserts, _Deletes) -> erlang:nif_error(nif_not_loaded).
 match_batch(_Ctx, _Topics, _Mode) -> erlang:nif_error(nif_not_loaded).
+submit(_Ctx, _Topics, _Mode) -> erlang:nif_error(nif_not_loaded).
+wait(_Ctx, _Ticket) -> erlang:nif_error(nif_not_loaded).
+subs_build(_Ctx, _SubsByFilterId) -> erlang:nif_error(nif_not_loaded).
+publish_batch(_Ctx, _Topics) -> erlang:nif_error(nif_not_loaded).
 
 %% ---------------------------------------------------------------------
 %% emqx_trie-shaped API
@@ -49,6 +53,9 @@ init() ->
     ok.
 
 ctx() -> persistent_term:get(?MODULE).
+
+%% Filter binary of a filter id (ids are assigned by insert/1).
+filter_of(Id) -> ets:lookup_element(?TAB, Id, 2).
 
 %% emqx_trie:insert/1 — idempotent (emqx_trie.erl:82-87)
 insert(Filter) when is_binary(Filter) ->

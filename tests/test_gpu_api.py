@@ -104,3 +104,87 @@ def test_broker_random_deliveries_vs_oracle():
     for t, g in zip(topics, got):
         want = R.deliveries(o, subs, t)
         assert set(d[:3] for d in g) == want, t
+
+
+def test_publish_result_nosub_and_sub_pub():
+    """emqx_broker_SUITE t_nosub_pub / t_sub_pub (test/emqx_broker_SUITE.erl:121-138)
+    as publish/1 results and the dropped counters (emqx_broker.erl:232-235, 283-295)."""
+    br = Broker()
+    assert br.metrics["messages.dropped"] == 0
+    assert br.publish_result(b"topic") == []
+    assert br.metrics["messages.dropped"] == 1 and br.metrics["messages.dropped.no_subscribers"] == 1
+    br.subscribe(b"topic", 1)
+    assert br.publish_result(b"topic") == [("local", b"topic", ("ok", 1))]
+    assert br.metrics["messages.dropped"] == 1
+    br.subscribe(b"+", 2)
+    br.subscribe(b"#", 3)
+    br.subscribe(b"#", 4)
+    got = br.publish_result(b"topic")
+    assert sorted(got) == [("local", b"#", ("ok", 2)), ("local", b"+", ("ok", 1)), ("local", b"topic", ("ok", 1))]
+    # a subscriber whose process is gone is not counted; no one left -> dropped
+    br.kill(1)
+    got = br.publish_result(b"topic")
+    assert ("local", b"topic", ("error", "no_subscribers")) in got
+    assert br.metrics["messages.dropped"] == 2
+    # system messages are never counted as dropped (emqx_broker.erl:311-316)
+    assert br.publish_result(b"$SYS/brokers") == []
+    assert br.publish_result(b"a/b", sys=True) == [("local", b"#", ("ok", 2))]
+    assert br.publish_result(b"$SYS/x/y", sys=False) == []
+    assert br.metrics["messages.dropped"] == 2
+
+
+def test_publish_result_share_and_forward():
+    br = Broker(shared_strategy="round_robin")
+    br.subscribe(b"$share/g/s/+", 10)
+    br.subscribe(b"$share/g/s/+", 11)
+    br.subscribe(b"$share/h/s/+", 12)
+    br.router.do_add_route(b"s/#", "n2")
+    got = br.publish_result(b"s/1")
+    assert sorted(got, key=repr) == sorted([("share", b"s/+", ("ok", 1)), ("share", b"s/+", ("ok", 1)),
+                                            ("n2", b"s/#", "forward")], key=repr)
+    assert br.metrics["messages.forward"] == 1
+    br.kill(12)
+    got = br.publish_result(b"s/1")
+    assert ("share", b"s/+", ("error", "no_subscribers")) in got and ("share", b"s/+", ("ok", 1)) in got
+    assert br.metrics["messages.dropped"] == 0   # a shared group's miss is not a drop
+
+
+def test_publish_result_random_vs_oracle():
+    rng = random.Random(17)
+    br = Broker(shared_strategy="random")
+    o = R.Router()
+    subs, groups = {}, {}
+    fl = list(dict.fromkeys(rand_filter(rng) for _ in range(120)))
+    sid = 0
+    for f in fl:
+        if rng.random() < 0.8:
+            for _ in range(rng.randint(1, 3)):
+                br.subscribe(f, sid)
+                subs.setdefault(f, []).append(sid)
+                sid += 1
+            o.do_add_route(f, "local")
+        if rng.random() < 0.2:
+            g = b"g%d" % rng.randint(0, 2)
+            br.subscribe(b"$share/" + g + b"/" + f, sid)
+            groups.setdefault(f, set()).add(g)
+            sid += 1
+            o.do_add_route(f, ("group", g))
+    dead = set(rng.sample(range(sid), sid // 4))
+    for x in dead:
+        br.kill(x)
+    topics = [rand_topic(rng) for _ in range(300)]
+    got = br.publish_result_batch(topics)
+    dropped = 0
+    for t, g in zip(topics, got):
+        want = []
+        for x, d in o.match_routes(t):
+            if d == "local":
+                n = sum(1 for s in subs.get(x, []) if s not in dead)
+                want.append(("local", x, ("ok", n) if n else ("error", "no_subscribers")))
+                dropped += 0 if n or t.startswith(b"$SYS/") else 1
+            else:
+                live = [m for m in br.shared[(d[1], x)] if m not in dead]
+                want.append(("share", x, ("ok", 1) if live else ("error", "no_subscribers")))
+        dropped += 0 if want or t.startswith(b"$SYS/") else 1
+        assert sorted(g, key=repr) == sorted(want, key=repr), t
+    assert br.metrics["messages.dropped"] == dropped
