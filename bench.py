@@ -39,7 +39,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 WORKLOADS = {
     "c1": "C1: 1M filters (depth 4-8, 20% wildcard) x 10M-topic batch per GPU",
     "c2": "C2: 10M wildcard filters (depth 4-8, '+' p=.15, '#' p=.5) x 10M-topic batch per GPU",
-    "c3": "C3: 10M wildcard filters, depth-16 topics, '+' p=.35, '#' p=.7",
+    "c3": "C3: 10M wildcard filters, depth-16 topics, '+' p=.35, '#' p=.7, match + subscriber fan-out "
+          "(1+Poisson(1) subscribers, 0.1% of filters with 2000, 10% $share/g0..g63 groups of 2-16 members)",
     "c4": "C4: 100M filters (depth 4-8, 20% wildcard) x 10M-topic batch per GPU, match + subscriber fan-out "
           "(1+Poisson(1) subscribers, 0.1% of filters with 2000, 10% $share groups)",
 }
@@ -167,11 +168,11 @@ def main():
     ap.add_argument("--mode", default="replicate", choices=sorted(LAYOUTS))
     ap.add_argument("--match", default="routes", choices=["routes", "trie"])
     ap.add_argument("--fanout", default="auto", choices=["auto", "on", "off"],
-                    help="add emqx_broker:dispatch/2 subscriber fan-out to each step (auto: on for c4)")
+                    help="add emqx_broker:dispatch/2 subscriber fan-out to each step (auto: on for c3, c4)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
-    fanout = args.fanout == "on" or (args.fanout == "auto" and args.config == "c4")
+    fanout = args.fanout == "on" or (args.fanout == "auto" and args.config in ("c3", "c4"))
     if fanout and args.mode == "shard":
         ap.error("--fanout runs with --mode replicate (a shard's fan-out would precede the id gather)")
     _heartbeat()
@@ -226,7 +227,7 @@ def main():
     if fanout:
         # filter id -> subscriber CSR (emqx_subscriber bag, shards flattened)
         t0 = time.time()
-        srow, ssubs = synth.subscribers(f.n, lam=1.0, p_big=0.001, n_big=2000, p_share=0.1, seed=seed)
+        srow, ssubs = synth.subscribers(f.n, lam=1.0, p_big=0.001, n_big=2000, p_share=0.1, groups=64, seed=seed)
         gm.subs_build(srow, ssubs)
         sub_entries = len(ssubs)
         del srow, ssubs

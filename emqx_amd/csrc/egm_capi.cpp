@@ -150,7 +150,7 @@ struct egm_ctx {
   std::string err;
 
   // per-batch workspace
-  DevBuf wid, lv, tfl, cnt, head, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats;
+  DevBuf wid, lv, tfl, cnt, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats;
   uint64_t pieces_cap = 0, ids_tmp_cap = 0;
   DevBuf in_blob, in_off, out_row, out_ids;
   uint32_t heavy_waves = 64;     // waves of the heavy kernel (rare path; each owns an HBM stack)
@@ -499,7 +499,6 @@ static int ensure_work(egm_ctx* c, uint32_t n, uint64_t blob_bytes, uint64_t ids
   if ((e = c->lv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "lv");
   if ((e = c->tfl.ensure(nn)) != hipSuccess) return c->hip_fail(e, "tfl");
   if ((e = c->cnt.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "cnt");
-  if ((e = c->head.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "head");
   // ids in flush order and their pieces, plus the slack of per-wave slabs
   const uint64_t tcap = ids_tmp_capacity(ids_cap, n);
   if (tcap >= 0xFFFFFFF0ull) return c->fail(EGM_E_INVAL, "batch too large: > 4G matched ids (split it)");
@@ -523,7 +522,6 @@ static MatchWork work_view(egm_ctx* c) {
   w.lv = c->lv.as<uint32_t>();
   w.tfl = c->tfl.as<uint8_t>();
   w.cnt = c->cnt.as<uint32_t>();
-  w.head = c->head.as<uint32_t>();
   w.ids_tmp = c->ids_tmp.as<uint32_t>();
   w.ids_cap = c->ids_tmp_cap;   // ids_tmp entries (the output capacity is MatchOut's)
   w.pieces = c->pieces.as<uint4>();

@@ -37,9 +37,8 @@ struct MatchStats {               // device-side counters, zeroed per batch
 };
 
 // A piece is one flush's run of a topic's ids in ids_tmp:
-// {count, ids_tmp offset, offset inside the topic's row, the topic's previous
-// piece or NONE}.  head[t] is the topic's last piece, so CSR rows are
-// assembled by following the chains, without atomics.
+// {topic, count, ids_tmp offset, offset inside the topic's CSR row}, so the
+// compaction places every run without atomics (count 0: an unused slot).
 // Each wave reserves its output space in slabs (one device-scope atomic per
 // slab): a single shared counter bumped per flush serialises across the 8
 // XCDs at the memory side.
@@ -51,7 +50,6 @@ struct MatchWork {                // per-batch device workspace
   uint32_t* lv;                   // [n] levels
   uint8_t* tfl;                   // [n] TF_* flags
   uint32_t* cnt;                  // [n] number of ids of topic t
-  uint32_t* head;                 // [n] last piece of topic t (NONE: no ids)
   uint32_t* ids_tmp;              // [ids_cap] ids in flush order
   uint64_t ids_cap;
   uint4* pieces;                  // [pieces_cap]

@@ -401,57 +401,37 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #endif
 
 #ifndef EGM_WALK_STACK
-#define EGM_WALK_STACK 176   // items (16 B) per wave
+#define EGM_WALK_STACK 320   // items (16 B) per wave
 #endif
-#ifndef EGM_WALK_WPS
-#define EGM_WALK_WPS 8       // words per topic staged in LDS (deeper levels are read from HBM)
-#endif
-constexpr uint32_t WPS = EGM_WALK_WPS;
 #ifndef EGM_WALK_STAGE
-#define EGM_WALK_STAGE 256   // staged emits per flush (6 B each; >= 4 emits x 64 lanes)
+#define EGM_WALK_STAGE 320   // staged emits per flush (7 B each; >= 4 emits x 64 lanes)
+#endif
+#ifndef EGM_WALK_WORDS
+#define EGM_WALK_WORDS 448   // staged topic word ids per wave (a chunk's topics, [topic][level])
 #endif
 constexpr uint32_t WALK_STACK = EGM_WALK_STACK;
 constexpr uint32_t WALK_STAGE = EGM_WALK_STAGE;
-constexpr uint32_t SLOTS = 64;                       // topic slots per wave (slot = lane)
-#ifndef EGM_WALK_ADMIT
-#define EGM_WALK_ADMIT 64    // new topics enter while the stack holds fewer items than this
-#endif
-#ifndef EGM_WALK_LIVE
-#define EGM_WALK_LIVE 32     // ... and fewer topics than this are in flight
-#endif
-#ifndef EGM_WALK_WPE
-#define EGM_WALK_WPE 4       // waves per SIMD the walk is compiled for (<= 128 VGPRs)
-#endif
-constexpr uint32_t WALK_ADMIT = EGM_WALK_ADMIT;
-constexpr uint32_t WALK_LIVE = EGM_WALK_LIVE;
-constexpr uint32_t SLOT_BITS = 6;
-// The pop bound below keeps room >= dmax once the batch in flight has
-// landed, and admission adds roots only within the same bound, so the stack
-// cannot overflow.  Chunks with a topic deeper than LIGHT_DMAX go to k_heavy
-// (an empty wave can always admit: 64 + dmax <= WALK_STACK).
-constexpr uint32_t LIGHT_DMAX = WALK_STACK - 64;
-static_assert(SLOTS == 64 && (1u << SLOT_BITS) == SLOTS && WALK_CHUNK == 64, "one slot, one prefetched topic per lane");
-static_assert(WALK_STAGE >= 256 && WALK_STAGE <= 256, "stage: 4 emits x 64 lanes per step; u8 ranks and starts");
+constexpr uint32_t WALK_WORDS = EGM_WALK_WORDS;
+// The pop bound (below) keeps room >= dmax after every iteration and a refill
+// fills the stack to at most 64 items, so the stack cannot overflow while
+// 64 + dmax <= WALK_STACK; the words of one topic must fit the word stage.
+// A chunk with a deeper topic goes to k_heavy before any of it is walked.
+constexpr uint32_t LIGHT_DMAX = (WALK_STACK - 64) < WALK_WORDS ? (WALK_STACK - 64) : WALK_WORDS;
+static_assert(WALK_CHUNK == 64, "one topic per lane in the chunk prologue");
+static_assert(WALK_STAGE >= 256, "a step stages up to 4 emits x 64 lanes");
 static_assert(LIGHT_DMAX >= 16, "stack too small");
-static_assert(WALK_ADMIT <= 64 && WALK_LIVE >= 1 && WALK_LIVE <= SLOTS, "a refill adds at most 64 items");
 
 struct alignas(16) WaveLds {
   uint4 stack[WALK_STACK];
   uint32_t stage_fid[WALK_STAGE];
-  uint8_t stage_t[WALK_STAGE];     // slot of the emit
-  uint8_t stage_rank[WALK_STAGE];  // rank within its slot in this flush
-  uint32_t tinfo[SLOTS];           // D | tflags << 24
-  uint32_t tbase[SLOTS];           // wid index of the topic's word 0
-  uint32_t cnt[SLOTS];             // ids flushed so far
-  uint32_t last[SLOTS];            // the topic's last piece (NONE: none)
-  uint16_t fcnt[SLOTS];            // ids in the current stage / start inside the flush
-  uint32_t words[SLOTS * WPS];     // the topic's first WPS word ids
-  uint32_t live[SLOTS];            // the topic's items in the stack (or being expanded)
-  uint32_t tid[SLOTS];             // the topic's index in the batch
-  uint32_t finmask[2];             // slots whose topic finished this iteration
-  uint32_t stmask[2];              // slots that staged an emit this iteration
+  uint16_t stage_rank[WALK_STAGE];
+  uint8_t stage_t[WALK_STAGE];       // topic in chunk of the emit
+  uint32_t words[WALK_WORDS];        // the sub-chunk's word ids, [topic][level]
+  uint32_t tinfo[WALK_CHUNK];        // D | tflags << 24
+  uint32_t tbase[WALK_CHUNK];        // LDS index of the topic's word 0
+  uint32_t cnt[WALK_CHUNK];          // ids per topic, whole chunk
+  uint32_t fcnt[WALK_CHUNK];         // ids per topic in the current stage / start inside the flush
 };
-
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
 // readfirstlane returns int: widen each half as unsigned (a sign-extended low
@@ -460,20 +440,8 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | (uint64_t)uni((uint32_t)v);
 }
 
-// The workspace descriptor is k_walk's first kernel argument, so it sits at
-// offset 0 of the kernarg segment.  It is re-read at each rare use (chunk
-// take, retire, flush) through a pointer the compiler cannot see through:
-// hoisted out of the loop its fields would pin ~30 SGPRs and push the walk's
-// wave-uniform state into VGPRs.
-typedef const __attribute__((address_space(4))) MatchWork ConstWork;   // scalar (s_load) view
-__device__ __forceinline__ ConstWork* fresh() {
-  uint64_t v = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(v));
-  // an asm result counts as divergent: without readfirstlane every value read
-  // through it, and the whole loop's control flow, would be treated as
-  // per-lane (exec-masked branches, uniform state in VGPRs)
-  return (ConstWork*)uni64(v);
-}
+// An unused pieces-slab slot: count 0, skipped by k_compact.
+__device__ __forceinline__ uint4 empty_piece() { return make_uint4(0, 0, 0, 0); }
 
 // Per-wave output slab (uniform across the wave).
 struct Slab {
@@ -482,14 +450,17 @@ struct Slab {
 
 // Take `need` entries from the wave's slab, reserving a new slab of at least
 // `grain` entries (one device-scope atomic) when the current one is short.
+// The unused tail of an abandoned pieces slab is marked empty (count 0).
 __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, uint32_t grain,
-                                                        unsigned long long* counter, uint32_t lane) {
+                                                        unsigned long long* counter, uint32_t lane,
+                                                        uint4* tail_fill, unsigned long long tail_cap) {
   if (s.cur + need > s.end) {
+    if (tail_fill)
+      for (unsigned long long i = s.cur + lane; i < s.end && i < tail_cap; i += 64) tail_fill[i] = empty_piece();
     const unsigned long long sz = need > grain ? need : grain;
     unsigned long long b = 0;
     if (lane == 0) b = atomicAdd(counter, sz);
-    b = __shfl(b, 0, 64);
-    b = uni64(b);   // wave-uniform: keep it in SGPRs
+    b = uni64(__shfl(b, 0, 64));   // wave-uniform: keep it in SGPRs
     s.cur = b;
     s.end = b + sz;
   }
@@ -498,15 +469,14 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
   return r;
 }
 
-// Write the stage out.  Entries are ranked within their slot by a
-// conflict-free multi-split (lanes holding the same slot find each other with
-// 7 ballots; the leader of each group updates the slot's count), then
-// scattered into the wave's ids slab grouped by slot.  One piece per slot
-// present: {count, ids_tmp offset, offset inside the topic's CSR row, the
-// topic's previous piece} — a topic's pieces form a chain from head[t], so
-// the compaction gathers each topic's ids without scanning all pieces.
-__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t lane, Slab& sid, Slab& spc) {
-  ConstWork& w = *fresh();
+// Write the stage out.  Entries are ranked within their topic by a
+// conflict-free multi-split (lanes holding the same topic find each other
+// with 6 ballots; one LDS add per topic per 64 entries), then scattered into
+// the wave's ids slab grouped by topic: one piece {topic, count, ids_tmp
+// offset, offset inside the topic's CSR row} per topic present, so the
+// compaction needs no atomics.
+__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane,
+                                            const MatchWork& w, Slab& sid, Slab& spc) {
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {
     const uint32_t i = i0 + lane;
@@ -514,41 +484,34 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
     const uint32_t tt = act ? L.stage_t[i] : 0u;
     uint64_t m = __ballot(act);
 #pragma unroll
-    for (uint32_t b = 0; b < SLOT_BITS; ++b) {
+    for (uint32_t b = 0; b < 6; ++b) {
       const bool bit = (tt >> b) & 1u;
       const uint64_t bb = __ballot(bit);
       m &= bit ? bb : ~bb;
     }
     const uint32_t leader = act ? (uint32_t)__builtin_ctzll(m) : lane;
     uint32_t old = 0;
-    if (act && lane == leader) {   // one leader per slot: a plain read-modify-write
-      old = L.fcnt[tt];
-      L.fcnt[tt] = (uint16_t)(old + popc(m));
-    }
+    if (act && lane == leader) old = atomicAdd(&L.fcnt[tt], popc(m));
     old = __shfl(old, (int)leader, 64);
-    if (act) L.stage_rank[i] = (uint8_t)(old + mbcnt(m));
+    if (act) L.stage_rank[i] = (uint16_t)(old + mbcnt(m));
   }
   wave_sync();
-  const uint32_t fl = L.fcnt[lane];   // slot = lane
+  const uint32_t fl = L.fcnt[lane];   // topic t0 + lane
   uint32_t tot, ptot;
   const uint32_t ex = wave_excl_scan(fl, lane, &tot);
   const uint32_t pex = wave_excl_scan(fl ? 1u : 0u, lane, &ptot);
-  const unsigned long long base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane);
-  const unsigned long long pbase = slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane);
+  const unsigned long long base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
+  const unsigned long long pbase = slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
   const bool ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
   if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
-  if (fl && ok) {
-    const uint32_t p = (uint32_t)(pbase + pex);
-    w.pieces[p] = make_uint4(fl, (uint32_t)(base + ex), L.cnt[lane], L.last[lane]);
-    L.last[lane] = p;
-  }
-  L.fcnt[lane] = (uint16_t)ex;   // the slot's start inside this flush
+  if (fl && ok) w.pieces[pbase + pex] = make_uint4(t0 + lane, fl, (uint32_t)(base + ex), L.cnt[lane]);
+  L.fcnt[lane] = ex;   // the topic's start inside this flush
   L.cnt[lane] += fl;
   wave_sync();
   if (ok) {
-    uint32_t* dst = w.ids_tmp + base;
 #pragma unroll 1
-    for (uint32_t i = lane; i < nstage; i += 64) dst[L.fcnt[L.stage_t[i]] + L.stage_rank[i]] = L.stage_fid[i];
+    for (uint32_t i = lane; i < nstage; i += 64)
+      w.ids_tmp[base + L.fcnt[L.stage_t[i]] + L.stage_rank[i]] = L.stage_fid[i];
   }
   wave_sync();
   L.fcnt[lane] = 0;
@@ -580,16 +543,17 @@ struct Pend {
   uint4 it;                 // the item
   uint32_t D, nw;           // its topic's depth, the word at level + 1
   bool act, lit, plus, d1;  // d1: a one-word '$' topic (do_match/1's lookup_topic probe)
-  uint4 prec, l0, l1;
-  uint3 h0, h1;             // the slots' child record copies (12 of 16 bytes)
+  uint4 prec, l0, h0, l1, h1;
 };
 
 // Branch-free on purpose: every lane issues its loads unconditionally (an
-// idle lane reads node 0 / bucket 0 / word 0, lines every wave keeps hot).  A
-// load inside an `if` makes LLVM merge its result at the end of the block,
-// and the copy it inserts there waits for the load.
-__device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* __restrict__ wid, uint32_t tbase,
-                                      const uint32_t* wlds, Pend& p) {
+// idle lane reads node 0 / bucket 0, lines every wave keeps hot).  A load
+// inside an `if` makes LLVM merge its result at the end of the block, and
+// the copy it inserts there waits for the load.  The next level's word comes
+// from the LDS word stage (k_walk: `words` = the topic's staged words) or
+// from HBM (k_heavy: `words` = null, `wid` + `gbase`).
+__device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* words, const uint32_t* __restrict__ wid,
+                                      uint32_t gbase, Pend& p) {
   const uint32_t meta = p.it.y;
   const uint32_t fl = (meta >> MF_SHIFT) & 0xFu;
   p.plus = p.act && (fl & F_PLUS);
@@ -598,18 +562,12 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* __res
   p.prec = ld16(tab.nodes + (p.plus ? p.it.z : 0u));
   const uint8_t* bp = (const uint8_t*)(tab.edges + (size_t)(p.lit ? bkt : 0u) * EDGE_BUCKET);
   p.l0 = ld16(bp);
-  p.h0 = *(const uint3*)(bp + 16);
+  p.h0 = ld16(bp + 16);
   p.l1 = ld16(bp + 32);
-  p.h1 = *(const uint3*)(bp + 48);
+  p.h1 = ld16(bp + 48);
   // the next level's word (clamped; used only if level + 1 < D)
-  const uint32_t level = meta & LEVEL_MAX;
-  // from the LDS stage for the first WPS levels, else from HBM (deep topics;
-  // the other lanes read word 0, one hot line)
-  const uint32_t nl = min(level + 1, p.D - 1);
-  const bool far = p.act && (nl >= WPS || !wlds);   // k_heavy stages no words
-  const uint32_t wg = wid[far ? tbase + nl : 0u];
-  const uint32_t wl = wlds ? wlds[min(nl, WPS - 1)] : 0u;
-  p.nw = far ? wg : wl;
+  const uint32_t nl = min((meta & LEVEL_MAX) + 1, p.D - 1);
+  p.nw = words ? words[nl] : wid[p.act ? gbase + nl : 0u];
 }
 
 // Children and emits of one popped item.
@@ -708,77 +666,13 @@ __device__ __forceinline__ uint32_t root_flags(uint4 root, bool dollar, uint32_t
   return (dollar ? 0u : (root.w & F_PLUS)) | ((root.w & s0) ? (root.w & F_LIT) : 0u);
 }
 
-// The next topics of a wave, prefetched into registers: lane j (< nt) holds
-// topic t0 + j's depth, flags, wid base and first WPS words.  Chunks come from
-// a global counter; a chunk with a topic deeper than LIGHT_DMAX (or every
-// chunk under DEBUG_FORCE_HEAVY) is deferred to k_heavy.  Straight-line loop
-// with wave-uniform flags only (a return from lane-conditional code inside
-// such a loop made the structurizer give the lanes different exits).
-struct Prefetch {
-  uint32_t t0, nt, next;    // wave-uniform: first topic, topics, next to admit
-  uint32_t dmax;            // wave-uniform: the chunk's deepest topic
-  uint32_t D, f, base;      // lane j: topic t0 + j
-  uint32_t wv[WPS];
-};
-
-__device__ __forceinline__ void prefetch_chunk(Prefetch& P, const uint32_t* __restrict__ off,
-                                               const uint32_t* __restrict__ wid, uint32_t n, uint32_t nchunks,
-                                               uint32_t lane) {
-  ConstWork& w = *fresh();
-  P.t0 = P.nt = P.next = P.dmax = 0;
-  uint32_t guard = 0;
-  while (++guard < (1u << EGM_GUARD_BITS)) {
-    uint32_t c = 0;
-    if (lane == 0) c = atomicAdd(&w.stats->next_chunk, 1u);
-    c = uni(__shfl(c, 0, 64));
-    if (c >= nchunks) break;
-    const uint32_t t0 = c * WALK_CHUNK;
-    const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
-    uint32_t D = 0, f = 0, base = 0;
-    if (lane < nt) {
-      D = w.lv[t0 + lane];
-      f = w.tfl[t0 + lane];
-      base = off[t0 + lane] + t0 + lane;
-    }
-    uint32_t dmax = D;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, d, 64));
-    dmax = uni(dmax);
-    if (dmax > LIGHT_DMAX || (uni(w.debug) & DEBUG_FORCE_HEAVY)) {   // deferred to k_heavy
-      uint32_t d = 0;
-      if (lane == 0) d = atomicAdd(&w.stats->n_deferred, 1u);
-      d = uni(__shfl(d, 0, 64));
-      if (lane == 0) w.deferred[d] = c;
-    } else {
-      P.t0 = t0;
-      P.nt = nt;
-      P.dmax = dmax;
-      P.D = D;
-      P.f = f;
-      P.base = base;
-#pragma unroll
-      for (uint32_t r = 0; r < WPS; ++r) P.wv[r] = wid[(lane < nt && r < D) ? base + r : 0u];
-      break;
-    }
-  }
-}
-
-// Deepest topic held in the wave's slots (the pop bound needs it).
-__device__ __forceinline__ uint32_t slots_dmax(const WaveLds& L, uint64_t held, uint32_t lane) {
-  uint32_t d = ((held >> lane) & 1) ? (L.tinfo[lane] & 0xFFFFFFu) : 0u;
-#pragma unroll
-  for (int k = 32; k >= 1; k >>= 1) d = max(d, (uint32_t)__shfl_xor(d, k, 64));
-  return uni(d);
-}
-
-// One wave walks up to 64 topics at once, one per slot (slot = lane for the
-// per-slot bookkeeping).  A topic enters a free slot when the stack runs
-// short, its live item count is kept in LDS, and a slot whose topic has no
-// item left (and none of whose emits is still staged) is retired — counts
-// and piece head written — and refilled at once: the stack never drains
-// between topics or chunks.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(EGM_WALK_WPE, 8))) void k_walk(MatchWork wk, DevTable tab, const uint32_t* __restrict__ wid,
-                                             const uint32_t* __restrict__ off, uint32_t n, int mode) {
+// One wave walks one chunk of 64 topics at a time (a grid stride over the
+// chunks).  The chunk's words are staged in LDS ([topic][level]; deep topics
+// in sub-chunks of S topics with S * dmax <= WALK_WORDS), topics are admitted
+// 64 roots at a time while the stack is short, and the wave pops up to 64
+// items per iteration.
+__global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __restrict__ off, uint32_t n, int mode,
+                                             MatchWork w) {
   __shared__ WaveLds L;
   const uint32_t lane = threadIdx.x;
   const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
@@ -790,176 +684,147 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(EGM_WALK_WPE
   uint32_t created = 0;
   unsigned long long iters = 0, popped = 0, bounded = 0;
   Slab sid{0, 0}, spc{0, 0};
-  L.fcnt[lane] = 0;   // slot = lane
-  L.live[lane] = 0;
-  if (lane < 2) {
-    L.finmask[lane] = 0;
-    L.stmask[lane] = 0;
-  }
-  Prefetch P;
-  prefetch_chunk(P, off, wid, n, nchunks, lane);
-  // slots: free; done (no item left) but not yet retired; with emits in the stage
-  uint64_t freem = ~0ull, donem = 0, stagedm = 0;
-  uint32_t sp = 0, nstage = 0, dmax = 0;
-  Pend pa;           // batch A: popped, reads in flight
-  pa.act = false;
-  uint32_t ka = 0;   // its items (wave-uniform)
-  uint32_t guard = 0;   // every loop of the kernel is bounded: a bug reports, it never hangs the GPU
-  for (;;) {
-    if (++guard > (1u << EGM_GUARD_BITS)) {
-      if (lane == 0) atomicOr(&fresh()->stats->overflow, 8u);
-      break;
+  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uint32_t t0 = c * WALK_CHUNK;
+    const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
+    // ---- topic info (lane j: topic t0 + j) ----
+    uint32_t D = 0, f = 0;
+    if (lane < nt) {
+      D = w.lv[t0 + lane];
+      f = w.tfl[t0 + lane];
     }
-    const bool more = P.next < P.nt;
-    // ---- the one flush point of the loop top: room for 64 root emits, done
-    // slots to recycle, or the end ----
-    const uint64_t held = donem & stagedm;   // done, but its last emits are still staged
-    const uint32_t busy = SLOTS - popc(freem);   // slots in flight or awaiting retirement
-    if (nstage && (nstage + 64u > WALK_STAGE || (held && (busy >= WALK_LIVE || (sp == 0 && ka == 0 && !more))) ||
-                   (held && sp < WALK_ADMIT && busy + 8u > WALK_LIVE))) {
-      flush_stage(L, nstage, lane, sid, spc);
-      nstage = 0;
-      stagedm = 0;
-    }
-    // ---- retire done slots with nothing staged ----
-    {
-      const uint64_t rm = donem & ~stagedm;
-      if (rm) {
-        if ((rm >> lane) & 1) {
-          ConstWork& w = *fresh();
-          const uint32_t t = L.tid[lane];
-          w.cnt[t] = L.cnt[lane];
-          w.head[t] = L.last[lane];
-        }
-        donem &= ~rm;
-        freem |= rm;
-        dmax = slots_dmax(L, ~freem, lane);
-      }
-    }
-    // ---- admission: new topics into free slots while the stack is short ----
-    const uint32_t inflight = SLOTS - popc(freem);
-    // (the new roots must leave room for batch A's children and the deepest
-    // topic's DFS: sp + 2 ka + dmax <= WALK_STACK after admission)
-    const int alim = (int)WALK_STACK - (int)max(dmax, P.dmax) - (int)sp - 2 * (int)ka;
-    if (sp < WALK_ADMIT && inflight < WALK_LIVE && more && alim > 0) {
-      const uint32_t k = min(min(min(WALK_ADMIT - sp, WALK_LIVE - inflight), P.nt - P.next), (uint32_t)alim);
-      const bool fr = (freem >> lane) & 1;
-      const uint32_t r = mbcnt(freem);               // rank of this free slot
-      const bool tk = fr && r < k;                   // slot `lane` takes prefetched topic P.next + r
-      const uint32_t src = P.next + (tk ? r : 0u);
-      const uint32_t D = (uint32_t)__shfl(P.D, (int)src, 64), f = (uint32_t)__shfl(P.f, (int)src, 64);
-      const uint32_t base = (uint32_t)__shfl(P.base, (int)src, 64);
-      uint32_t wv[WPS];
+    L.tinfo[lane] = D | (f << 24);
+    L.cnt[lane] = 0;
+    L.fcnt[lane] = 0;
+    uint32_t dmax = D;
 #pragma unroll
-      for (uint32_t q = 0; q < WPS; ++q) wv[q] = (uint32_t)__shfl(P.wv[q], (int)src, 64);
-      bool has = false, em = false;
-      uint32_t fid = NONE;
-      uint4 it = make_uint4(0, 0, 0, 0);
-      if (tk) {
-        L.tinfo[lane] = D | (f << 24);
-        L.tbase[lane] = base;
-        L.tid[lane] = P.t0 + src;
-        L.cnt[lane] = 0;
-        L.last[lane] = NONE;
-#pragma unroll
-        for (uint32_t q = 0; q < WPS; ++q) L.words[lane * WPS + q] = wv[q];
-        if (f & TF_WILDCARD) {
-          if (mode == MODE_ROUTES) em = exact_walk(tab, wid, base, D, &fid);
-        } else {
-          const bool dollar = (f & TF_DOLLAR) != 0;
-          em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
-          fid = root.y;
-          created += 1;
-          const uint32_t fl = root_flags(root, dollar, wv[0]);
-          has = fl != 0;
-          it = make_uint4(0, (lane << MT_SHIFT) | (fl << MF_SHIFT), root.x, wv[0]);
-        }
-        L.live[lane] = has ? 1u : 0u;
+    for (int d = 32; d >= 1; d >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, d, 64));
+    dmax = uni(dmax);
+    if (dmax > LIGHT_DMAX || (w.debug & DEBUG_FORCE_HEAVY)) {   // the whole chunk goes to k_heavy
+      if (lane == 0) {
+        const uint32_t d = atomicAdd(&w.stats->n_deferred, 1u);
+        w.deferred[d] = c;
       }
-      const uint64_t b = __ballot(has);
-      if (has) L.stack[sp + mbcnt(b)] = it;
-      sp += popc(b);
-      const uint64_t be = __ballot(em);
-      stagedm |= be;   // slot = lane
-      if (em) {
-        const uint32_t q = nstage + mbcnt(be);
-        L.stage_fid[q] = fid;
-        L.stage_t[q] = (uint8_t)lane;
-      }
-      nstage += popc(be);
-      const uint64_t tkm = __ballot(tk);
-      freem &= ~tkm;
-      donem |= tkm & ~b;   // a topic with no item is done at once
-      {
-        uint32_t dm = tk ? D : 0u;
-#pragma unroll
-        for (int d2 = 32; d2 >= 1; d2 >>= 1) dm = max(dm, (uint32_t)__shfl_xor(dm, d2, 64));
-        dmax = max(dmax, uni(dm));
-      }
-      P.next += k;
-      wave_sync();
-      if (P.next >= P.nt) prefetch_chunk(P, off, wid, n, nchunks, lane);
-    }
-    if (sp == 0 && ka == 0) {
-      if (!(P.next < P.nt) && !donem) break;   // no topic left, every slot retired
       continue;
     }
-
-    // ---- pop batch B and issue all its reads; then consume batch A, whose
-    // reads were issued one iteration earlier (two batches in flight) ----
-    // An item pushes at most two children.  With batch A (ka items) still to
-    // push, popping kb <= STACK - dmax - sp - 2 ka items leaves room >= dmax
-    // once both have landed; with no batch pending and room <= dmax the wave
-    // pops the top item alone, a plain DFS whose stack grows by at most one
-    // pending sibling per level below it.  So the stack never overflows: a
-    // deep, wide frontier (C3: depth 16, '+' p=.35) narrows the wave instead.
-    const int lim = (int)WALK_STACK - (int)dmax - (int)sp - 2 * (int)ka;
-    const uint32_t want = min(64u, sp);
-    const uint32_t kb = lim > 0 ? min(want, (uint32_t)lim) : (ka == 0 && sp ? 1u : 0u);
-    bounded += kb < want ? 1u : 0u;
-    iters += 1;
-    popped += kb;
-    Pend pb;
-    pb.act = lane < kb;
-    pb.it = L.stack[sp - 1 - min(lane, kb ? kb - 1 : 0u)];   // unconditional: see issue()
-    sp -= kb;
-    {
-      const uint32_t slot = (pb.it.y >> MT_SHIFT) & (SLOTS - 1);
-      const uint32_t ti = L.tinfo[slot];
-      pb.D = ti & 0xFFFFFFu;
-      pb.d1 = pb.D == 1 && ((ti >> 24) & TF_DOLLAR);
-      issue(tab, wid, L.tbase[slot], L.words + slot * WPS, pb);
-    }
+    uint32_t S = WALK_CHUNK;
+    while (S > 1 && S * dmax > WALK_WORDS) S >>= 1;
+    uint32_t nstage = 0;
     wave_sync();
-
-    if (ka) {   // ---- consume A: children -> stack, emits -> stage ----
-      const uint32_t slot = (pa.it.y >> MT_SHIFT) & (SLOTS - 1);
-      Out o;
-      finish(tab, mode, pa, o);
-      created += o.created;
-      const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
-      const uint32_t m0 = popc(c0b);
-      if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
-      if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;
-      sp += m0 + popc(c1b);
-      // live items per topic: children first, then the popped item, so the
-      // lane that takes a topic's count to zero is the last one
-      const uint32_t pushes = (o.p0 ? 1u : 0u) + (o.p1 ? 1u : 0u);
-      if (pushes) atomicAdd(&L.live[slot], pushes);
+    for (uint32_t sub = 0; sub < nt; sub += S) {
+      const uint32_t end = min(sub + S, nt);
+      if (lane < end - sub) {   // stage the sub-chunk's words
+        const uint32_t j = sub + lane, Dj = L.tinfo[j] & 0xFFFFFFu;
+        const uint32_t* src = w.wid + off[t0 + j] + t0 + j;
+        uint32_t* dst = L.words + lane * dmax;
+        L.tbase[j] = lane * dmax;
+        uint32_t i = 0;
+        for (; i + 4 <= Dj; i += 4) {
+          const uint32_t a0 = src[i], a1 = src[i + 1], a2 = src[i + 2], a3 = src[i + 3];
+          dst[i] = a0;
+          dst[i + 1] = a1;
+          dst[i + 2] = a2;
+          dst[i + 3] = a3;
+        }
+        for (; i < Dj; ++i) dst[i] = src[i];
+      }
       wave_sync();
-      if (pa.act && atomicSub(&L.live[slot], 1u) == 1u) atomicOr(&L.finmask[slot >> 5], 1u << (slot & 31));
-      // emits (at most 4 per lane): the stage is flushed first if they do not fit
-      {
+      uint32_t next = sub, sp = 0;
+      uint32_t guard = 0;   // every loop of the kernel is bounded: a bug reports, it never hangs the GPU
+      for (;;) {
+        if (++guard > (1u << EGM_GUARD_BITS)) {
+          if (lane == 0) atomicOr(&w.stats->overflow, 8u);
+          break;
+        }
+        // ---- admit new topics while the stack is short: their root '#'
+        // emit, their root item (a wildcard topic in ROUTES mode: one exact
+        // lookup, no item) ----
+        if (sp < 64u && next < end) {
+          const uint32_t k = min(64u - sp, end - next);
+          if (nstage + 64u > WALK_STAGE) {
+            flush_stage(L, nstage, t0, lane, w, sid, spc);
+            nstage = 0;
+          }
+          bool has = false, em = false;
+          uint32_t fid = NONE;
+          uint4 it = make_uint4(0, 0, 0, 0);
+          const uint32_t j = next + lane;
+          if (lane < k) {
+            const uint32_t ti = L.tinfo[j], Dj = ti & 0xFFFFFFu, tf = ti >> 24;
+            if (tf & TF_WILDCARD) {
+              if (mode == MODE_ROUTES) em = exact_walk(tab, w.wid, off[t0 + j] + t0 + j, Dj, &fid);
+            } else {
+              const bool dollar = (tf & TF_DOLLAR) != 0;
+              em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
+              fid = root.y;
+              created += 1;
+              const uint32_t w0 = L.words[L.tbase[j]];
+              const uint32_t rf = root_flags(root, dollar, w0);
+              has = rf != 0;
+              it = make_uint4(0, (j << MT_SHIFT) | (rf << MF_SHIFT), root.x, w0);
+            }
+          }
+          const uint64_t b = __ballot(has);
+          if (has) L.stack[sp + mbcnt(b)] = it;
+          sp += popc(b);
+          const uint64_t be = __ballot(em);
+          if (em) {
+            const uint32_t q = nstage + mbcnt(be);
+            L.stage_fid[q] = fid;
+            L.stage_t[q] = (uint8_t)j;
+          }
+          nstage += popc(be);
+          next += k;
+          wave_sync();
+        }
+        if (sp == 0) {
+          if (next >= end) break;
+          continue;
+        }
+        // ---- pop up to 64 items and issue all their reads ----
+        // An item pushes at most two children (net +1), so popping k <= room -
+        // dmax items keeps room >= dmax afterwards; with room <= dmax the wave
+        // pops one item at a time, a plain DFS, whose stack grows by at most
+        // one pending sibling per level below the top item.  So the stack
+        // never overflows: a deep, wide frontier (C3: depth 16, '+' p=.35)
+        // narrows the wave instead.
+        const uint32_t room = WALK_STACK - sp;
+        const uint32_t lim = room > dmax ? room - dmax : 1u;
+        const uint32_t want = min(64u, sp), take = min(want, lim), bi = sp - take;
+        bounded += take < want ? 1u : 0u;
+        iters += 1;
+        popped += take;
+        Pend p;
+        p.act = lane < take;
+        p.it = L.stack[min(bi + lane, WALK_STACK - 1)];   // unconditional: see issue()
+        sp = bi;
+        const uint32_t tt = (p.it.y >> MT_SHIFT) & 0x7Fu;
+        const uint32_t ti = L.tinfo[tt];
+        p.D = ti & 0xFFFFFFu;
+        p.d1 = p.D == 1 && ((ti >> 24) & TF_DOLLAR);
+        issue(tab, L.words + L.tbase[tt], nullptr, 0, p);
+        wave_sync();
+        // ---- consume: children -> stack, emits -> stage ----
+        Out o;
+        finish(tab, mode, p, o);
+        created += o.created;
+        const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
+        const uint32_t m0 = popc(c0b), nc = m0 + popc(c1b);
+        if (sp + nc > WALK_STACK) {   // guard only: the pop bound keeps sp + pushes <= WALK_STACK
+          if (lane == 0) atomicOr(&w.stats->overflow, 4u);
+          break;
+        }
+        if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
+        if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;
+        sp += nc;
         const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
         const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
         if (nstage + ne > WALK_STAGE) {
           wave_sync();
-          flush_stage(L, nstage, lane, sid, spc);
+          flush_stage(L, nstage, t0, lane, w, sid, spc);
           nstage = 0;
-          stagedm = 0;
         }
-        if (o.e0 || o.e1 || o.e2 || o.e3) atomicOr(&L.stmask[slot >> 5], 1u << (slot & 31));
-        const uint8_t st = (uint8_t)slot;
+        const uint8_t st = (uint8_t)tt;
         if (o.e0) {
           const uint32_t q = nstage + mbcnt(b0);
           L.stage_fid[q] = o.f0;
@@ -981,28 +846,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(EGM_WALK_WPE
           L.stage_t[q] = st;
         }
         nstage += ne;
-      }
-      wave_sync();
-      {   // topics that finished this iteration
-        const uint64_t fin = ((uint64_t)uni(L.finmask[1]) << 32) | uni(L.finmask[0]);
-        donem |= fin;
-        stagedm |= ((uint64_t)uni(L.stmask[1]) << 32) | uni(L.stmask[0]);
-        wave_sync();
-        if (lane < 2) {
-          L.finmask[lane] = 0;
-          L.stmask[lane] = 0;
-        }
         wave_sync();
       }
     }
-    pa = pb;
-    ka = kb;
+    if (nstage) flush_stage(L, nstage, t0, lane, w, sid, spc);
+    if (lane < nt) w.cnt[t0 + lane] = L.cnt[lane];
+    wave_sync();
   }
+  for (unsigned long long i = spc.cur + lane; i < spc.end && i < w.pieces_cap; i += 64)
+    w.pieces[i] = empty_piece();   // unused tail of the last pieces slab
   unsigned long long v = created;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
   if (lane == 0) {
-    ConstWork& w = *fresh();
     if (v) atomicAdd(&w.stats->visited, v);
     atomicAdd(&w.stats->iters, iters);
     atomicAdd(&w.stats->popped, popped);
@@ -1055,20 +911,17 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
       uint32_t fid = NONE;
       const bool em = mode == MODE_ROUTES && exact_walk(tab, w.wid, tb, D, &fid);
       if (lane == 0) {
-        uint32_t pc = NONE;
         if (em) {
           const unsigned long long base = atomicAdd(&w.stats->cursor, 1ull);
           const unsigned long long p = atomicAdd(&w.stats->pieces, 1ull);
           if (base < w.ids_cap && p < w.pieces_cap) {
             w.ids_tmp[base] = fid;
-            w.pieces[p] = make_uint4(1, (uint32_t)base, 0, NONE);
-            pc = (uint32_t)p;
+            w.pieces[p] = make_uint4(t, 1, (uint32_t)base, 0);
           } else {
             atomicOr(&w.stats->overflow, 1u);
           }
         }
         w.cnt[t] = em ? 1u : 0u;
-        w.head[t] = pc;
         w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
       }
       continue;
@@ -1077,7 +930,6 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
       if (lane == 0) {
         atomicAdd(&w.stats->errors, 1u);
         w.cnt[t] = 0;
-        w.head[t] = NONE;
         w.tfl[t] = (uint8_t)(tf | TF_HEAVY | TF_ERROR);
       }
       continue;
@@ -1115,7 +967,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
         p.it = ld16_l2(stk + (p.act ? bi + lane : 0u));
         p.D = D;
         p.d1 = D == 1 && (tf & TF_DOLLAR);
-        issue(tab, w.wid, tb, nullptr, p);
+        issue(tab, nullptr, w.wid, tb, p);
         sp = bi;
         Out o;
         finish(tab, mode, p, o);
@@ -1156,8 +1008,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
         if (lane == 0) {
           if (!fits) atomicOr(&w.stats->overflow, 1u);
           w.cnt[t] = count;
-          w.head[t] = (count && fits) ? (uint32_t)pb : NONE;
-          if (count && fits) w.pieces[pb] = make_uint4(count, (uint32_t)base, 0, NONE);
+          if (count && fits) w.pieces[pb] = make_uint4(t, count, (uint32_t)base, 0);
           w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
         }
         if (!count || !fits) break;
@@ -1245,25 +1096,27 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
   if (blockIdx.x == 0 && threadIdx.x == 0) row_ptr[n] = tile_sums[ntiles];
 }
 
-// Pieces -> CSR rows, no atomics.  One wave per window of 64 topics: lane k
-// follows topic k's piece chain (head[t] -> prev ...; usually one or two
-// pieces), and in each round the wave lays the window's current pieces out as
-// one run [0, tot) by a scan and copies it with consecutive lanes on
-// consecutive ids (a binary search over the 64 scan values finds each id's
-// piece).  Every output line of the window's rows [row_ptr[t0],
-// row_ptr[t0 + 64]) is written by this one wave within a few rounds, so the
-// L2 merges the partial writes into whole lines.
+// Pieces -> CSR rows, no atomics.  One wave per window of 64 pieces: a wave
+// scan lays the window's ids out as one run [0, tot), and the lanes copy that
+// run with consecutive lanes on consecutive ids (a binary search over the
+// window's 64 scan values finds each id's piece).  The pieces of one flush
+// have contiguous sources and topics of one chunk, so the reads and the
+// row_ptr loads coalesce; a contiguous range of windows per wave (not a grid
+// stride) keeps a chunk's flushes — and so the cache lines of its rows — with
+// one wave.  Unused slab slots (count 0) are skipped.
 #ifndef EGM_COMPACT_WAVES
 #define EGM_COMPACT_WAVES 4
 #endif
+#ifndef EGM_COMPACT_BLOCKS
+#define EGM_COMPACT_BLOCKS 65536   // grid cap; A/B at C2: 8192 -> 2.07 ms, 32768 -> 1.80, 65536 -> 1.74
+#endif
 constexpr int COMPACT_WAVES = EGM_COMPACT_WAVES;
 constexpr int COMPACT_IPL = 8;   // ids per lane per copy round in flight
-__global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint32_t* __restrict__ head,
-                                                                const uint4* __restrict__ pieces,
+__global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __restrict__ pieces,
                                                                 const uint32_t* __restrict__ ids_tmp, uint32_t n,
                                                                 const uint64_t* __restrict__ row_ptr,
                                                                 uint32_t* __restrict__ ids, uint64_t ids_cap,
-                                                                MatchStats* stats) {
+                                                                uint64_t pieces_cap, MatchStats* stats) {
   __shared__ uint32_t s_scan[COMPACT_WAVES][64];
   __shared__ uint32_t s_src[COMPACT_WAVES][64];
   __shared__ uint64_t s_dst[COMPACT_WAVES][64];
@@ -1275,69 +1128,52 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint32_t* 
     return;
   }
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t nwin = (n + 63) / 64;
-  for (uint32_t win = blockIdx.x * COMPACT_WAVES + wave; win < nwin; win += gridDim.x * COMPACT_WAVES) {
-    const uint32_t t = win * 64 + lane;
-    uint32_t p = t < n ? head[t] : NONE;
-    const uint64_t rs = row_ptr[min(t, n)];
-    uint32_t guard = 0;
-    while (__ballot(p != NONE)) {
-      if (++guard > (1u << EGM_GUARD_BITS)) {
-        if (lane == 0) atomicOr(&stats->overflow, 8u);
-        break;
+  const uint64_t np = min((uint64_t)stats->pieces, pieces_cap);
+  if (np == 0) return;
+  const uint64_t nwin = (np + 63) / 64, nw = (uint64_t)gridDim.x * COMPACT_WAVES;
+  const uint64_t per = (nwin + nw - 1) / nw, me = (uint64_t)blockIdx.x * COMPACT_WAVES + wave;
+  const uint64_t wend = min(nwin, (me + 1) * per) * 64;
+  uint64_t w0 = me * per * 64;
+  uint4 pc = pieces[min(w0 + lane, np - 1)];   // unconditional (a load under a branch is waited for at once)
+  for (; w0 < wend; w0 += 64) {
+    const uint64_t i = w0 + lane;
+    const uint32_t c = i < np ? pc.y : 0u;
+    const uint64_t rp = row_ptr[c ? pc.x : 0u];
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan(c, lane, &tot);
+    s_scan[wave][lane] = ex;
+    s_src[wave][lane] = pc.z;
+    s_dst[wave][lane] = rp + pc.w;
+    wave_sync();
+    pc = pieces[min(i + 64, np - 1)];   // the next window's piece, in flight during the copy
+    for (uint32_t q0 = lane; q0 < tot; q0 += 64 * COMPACT_IPL) {
+      uint32_t v[COMPACT_IPL];
+      uint64_t d[COMPACT_IPL];
+#pragma unroll
+      for (int r = 0; r < COMPACT_IPL; ++r) {
+        const uint32_t q = min(q0 + 64u * r, tot - 1);
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t step = 32; step >= 1; step >>= 1)
+          if (s_scan[wave][k + step] <= q) k += step;
+        const uint32_t o = q - s_scan[wave][k];
+        d[r] = s_dst[wave][k] + o;
+        v[r] = ids_tmp[s_src[wave][k] + o];
       }
-      const uint4 pc = pieces[p != NONE ? p : 0u];   // unconditional (a load under a branch is waited for at once)
-      const uint32_t c = p != NONE ? pc.x : 0u;
-      uint32_t tot;
-      const uint32_t ex = wave_excl_scan(c, lane, &tot);
-      s_scan[wave][lane] = ex;
-      s_src[wave][lane] = pc.y;
-      s_dst[wave][lane] = rs + pc.z;
-      wave_sync();
-      for (uint32_t q0 = lane; q0 < tot; q0 += 64 * COMPACT_IPL) {
-        uint32_t v[COMPACT_IPL];
-        uint64_t d[COMPACT_IPL];
 #pragma unroll
-        for (int r = 0; r < COMPACT_IPL; ++r) {
-          const uint32_t q = min(q0 + 64u * r, tot - 1);
-          uint32_t k = 0;
-#pragma unroll
-          for (uint32_t step = 32; step >= 1; step >>= 1)
-            if (s_scan[wave][k + step] <= q) k += step;
-          const uint32_t o = q - s_scan[wave][k];
-          d[r] = s_dst[wave][k] + o;
-          v[r] = ids_tmp[s_src[wave][k] + o];
-        }
-#pragma unroll
-        for (int r = 0; r < COMPACT_IPL; ++r)
-          if (q0 + 64u * r < tot) ids[d[r]] = v[r];
-      }
-      wave_sync();
-      p = p != NONE ? pc.w : NONE;
+      for (int r = 0; r < COMPACT_IPL; ++r)
+        if (q0 + 64u * r < tot) ids[d[r]] = v[r];   // plain stores: nontemporal ones measured 2x slower here
     }
+    wave_sync();
   }
 }
 
 // ------------------------------------------------------------- launchers ----
-// The walk runs persistent waves (one per block) that take chunks from a
-// global counter: as many as the GPU holds at once, fewer for a small batch.
-static uint32_t walk_resident_waves() {
-  static uint32_t cached = 0;
-  if (!cached) {
-    int dev = 0, cus = 256, per = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_walk, 64, 0) != hipSuccess || per <= 0) per = 16;
-    cached = (uint32_t)(cus * per);
-  }
-  return cached;
-}
-
+// One wave per block; a grid stride over the chunks beyond 32 waves per CU.
 int walk_grid_blocks(uint32_t n) {
   const uint32_t chunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
-  uint32_t blocks = chunks;   // waves keep taking chunks until none is left
-  const uint32_t cap = walk_resident_waves();
-  if (blocks > cap) blocks = cap;
+  uint32_t blocks = chunks < 256u * 32u ? chunks : 256u * 32u;
+  blocks = (blocks + 7) & ~7u;   // a multiple of the 8 XCDs
   return blocks ? (int)blocks : 1;
 }
 
@@ -1383,19 +1219,19 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
                      off, n, w.wid, w.lv, w.tfl);
   trace(s, "k_tokenise");
   if (ev_walk) hipEventRecord(ev_walk[0], s);
-  hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64), 0, s, w, tab, (const uint32_t*)w.wid, off, n,
-                     mode);
+  hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64), 0, s, tab, off, n, mode, w);
   if (ev_walk) hipEventRecord(ev_walk[1], s);
   trace(s, "k_walk");
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
   trace(s, "k_heavy");
   scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);
   trace(s, "scan");
-  const uint32_t nwin = (n + 63) / 64;
-  const uint32_t cblocks = std::min<uint32_t>(65536, (nwin + COMPACT_WAVES - 1) / COMPACT_WAVES);
-  hipLaunchKernelGGL(k_compact, dim3(cblocks ? cblocks : 1), dim3(64 * COMPACT_WAVES), 0, s, w.head, w.pieces,
-                     w.ids_tmp, n, out.row_ptr, out.ids, out.ids_cap, w.stats);
-  trace(s, "k_compact");
+  // shorter window ranges per wave keep more copies in flight; small batches
+  // get a small grid (the piece count is only known on the device)
+  const uint32_t cblocks =
+      (uint32_t)std::min<uint64_t>(EGM_COMPACT_BLOCKS, std::max<uint64_t>(256, ((uint64_t)n + 63) / 64));
+  hipLaunchKernelGGL(k_compact, dim3(cblocks), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.ids_tmp, n, out.row_ptr,
+                     out.ids, out.ids_cap, w.pieces_cap, w.stats);
   return hipGetLastError();
 }
 

@@ -192,5 +192,23 @@ def test_c3_dense_dfs_regime(mode):
         grow, gids = sampled_rows(res.row_ptr, res.ids, idx)
         assert np.array_equal(grow, row)
         assert np.array_equal(canonical(grow, gids), canonical(row, ids))
+        if mode == L.EGM_MODE_ROUTES:
+            # bench --config c3's fan-out: 1+Poisson(1) subscribers, 10% of the
+            # filters through $share groups g0..g63 (2-16 members)
+            srow, subs = synth.subscribers(f.n, lam=1.0, p_big=0.001, n_big=2000, p_share=0.1, groups=64,
+                                           seed=synth.SEED_BASE + synth.CONFIG_INDEX["c3"])
+            gm.subs_build(srow, subs)
+            drow, dfid, dsub = gm.fanout(res)
+            mids = res.ids.astype(np.int64)
+            cnt = (srow[mids + 1] - srow[mids]).astype(np.uint64)
+            dpos = np.zeros(len(mids) + 1, np.uint64)
+            np.cumsum(cnt, out=dpos[1:])
+            assert np.array_equal(drow, dpos[res.row_ptr.astype(np.int64)])
+            for i in np.random.default_rng(6).choice(t.n, 3_000, replace=False):
+                a, b = int(res.row_ptr[i]), int(res.row_ptr[i + 1])
+                wf, ws = _expected_deliveries(res.ids[a:b], srow, subs)
+                lo, hi = int(drow[i]), int(drow[i + 1])
+                assert np.array_equal(dfid[lo:hi], wf) and np.array_equal(dsub[lo:hi], ws), i
+            assert np.count_nonzero(dsub & np.uint32(L.GROUP_BIT)) > 0
     finally:
         gm.close()
