@@ -169,6 +169,9 @@ def main():
     ap.add_argument("--match", default="routes", choices=["routes", "trie"])
     ap.add_argument("--fanout", default="auto", choices=["auto", "on", "off"],
                     help="add emqx_broker:dispatch/2 subscriber fan-out to each step (auto: on for c3, c4)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="replicate mode: consecutive batches alternate over this many HIP streams (each with its "
+                         "own match workspace), so one batch's compaction overlaps the next one's walk")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
@@ -235,16 +238,20 @@ def main():
 
     # one explicit stream for every kernel and copy of the step (the library
     # and torch share one HIP runtime: emqx_amd._lib loads torch first)
-    stream = torch.cuda.Stream(dev)
+    nstreams = 1 if shard else max(1, args.streams)
+    streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+    stream = streams[0]
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     n = t.n
     nbytes = int(t.off[-1])
     d_blob = torch.from_numpy(t.blob).to(dev)
     d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
-    bufs = {"cap": max(4 * n, 1 << 20)}
-    bufs["row"] = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    bufs["ids"] = torch.zeros(bufs["cap"], dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    bufs = {"cap": max(4 * n, 1 << 20), "k": 0}
+    bufs["rows"] = [torch.zeros(n + 1, dtype=torch.int64, device=dev) for _ in range(nstreams)]
+    bufs["idss"] = [torch.zeros(bufs["cap"], dtype=torch.int32, device=dev) for _ in range(nstreams)]
+    bufs["row"], bufs["ids"] = bufs["rows"][0], bufs["idss"][0]
 
     fcap = max(8 * n, 1 << 20) if fanout else 0
     d_drow = torch.zeros(n + 1, dtype=torch.int64, device=dev) if fanout else None
@@ -253,10 +260,15 @@ def main():
     fan_on = False   # enabled once the id buffer holds a whole match batch
 
     def run_local():
-        gm.match_device(d_blob.data_ptr(), nbytes, d_off.data_ptr(), n, mode, sp, bufs["row"].data_ptr(),
-                        bufs["ids"].data_ptr(), bufs["cap"])
+        # batch k on stream k mod nstreams, with that stream's output buffers
+        i = bufs["k"] % nstreams
+        bufs["k"] += 1
+        s_i = streams[i].cuda_stream
+        row, ids = bufs["rows"][i], bufs["idss"][i]
+        gm.match_device(d_blob.data_ptr(), nbytes, d_off.data_ptr(), n, mode, s_i, row.data_ptr(), ids.data_ptr(),
+                        bufs["cap"])
         if fan_on:
-            gm.fanout_device(bufs["row"].data_ptr(), bufs["ids"].data_ptr(), bufs["cap"], n, sp, d_drow.data_ptr(),
+            gm.fanout_device(row.data_ptr(), ids.data_ptr(), bufs["cap"], n, s_i, d_drow.data_ptr(),
                              d_fid.data_ptr(), d_sub.data_ptr(), fcap)
 
     exchange = None
@@ -309,10 +321,13 @@ def main():
         if not st["overflow"]:
             break
         bufs["cap"] = int(st["n_ids"] * 1.25) + 1024
-        bufs["ids"] = torch.zeros(bufs["cap"], dtype=torch.int32, device=dev)
-        log(f"[rank {rank}] grew id buffer to {bufs['cap']}")
+        bufs["idss"] = [torch.zeros(bufs["cap"], dtype=torch.int32, device=dev) for _ in range(nstreams)]
+        bufs["ids"] = bufs["idss"][0]
+        bufs["k"] = 0
+        log(f"[rank {rank}] grew id buffers to {bufs['cap']}")
     if fanout:
         fan_on = True
+        bufs["k"] = 0
         step()
         torch.cuda.synchronize(dev)
         need = int(d_drow[n].item())
@@ -351,6 +366,18 @@ def main():
         assert deliveries <= fcap, (deliveries, fcap)
     wc = gm.walk_counters()
     gm.set_timing(False)
+    iso_ms = None
+    if nstreams > 1:
+        # the walk alone (one stream, nothing overlapping it), untimed: the
+        # kernel's own speed next to its time inside the overlapped steps
+        gm.set_timing(True)
+        for _ in range(3):
+            bufs["k"] = 0
+            run_local()
+        torch.cuda.synchronize(dev)
+        ti = gm.get_timing()
+        iso_ms = ti["walk_ms"] / max(1, ti["walk_launches"])
+        gm.set_timing(False)
     merged_ids = sum(exchange.last_totals) if exchange is not None else None
 
     units_per_step = n if shard else n * world
@@ -384,13 +411,15 @@ def main():
                        "topics_per_step": units_per_step, "topics_per_gpu": n,
                        "filters_on_rank0": tstats["filters"],
                        "match": "emqx_router:match_routes" if args.match == "routes" else "emqx_trie:match",
-                       "parallelism": f"{args.mode}{world}", "table": tstats},
+                       "parallelism": f"{args.mode}{world}", "streams": nstreams, "table": tstats},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic[0]["traffic_bytes_per_launch"] if traffic else None,
                          "traffic_source": traffic[1] if traffic else None,
                          "kernel": "k_walk", "kernel_ms": walk_ms, "bytes_per_launch": walk_bytes,
                          "kernel_src_sha": kernel_src_sha(),
+                         "kernel_ms_isolated": iso_ms,
+                         "frac_isolated": (walk_bytes / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if iso_ms else None,
                          "path_frac": path_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "stats": {"ids_per_step": n_ids, "visited_per_step": visited, "levels_per_step": sum_d,
                       "merged_ids_per_step": merged_ids,

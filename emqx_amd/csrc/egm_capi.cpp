@@ -104,6 +104,20 @@ struct PipeSlot {
 };
 constexpr size_t PIPE_MAX_SLOTS = 8;
 
+// One match workspace: the per-batch scratch of launch_match.
+struct MatchWs {
+  DevBuf wid, lv, tfl, cnt, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats;
+  uint64_t pieces_cap = 0, ids_tmp_cap = 0;
+  uint32_t heavy_cap = 0;        // stack items per heavy wave
+  hipEvent_t ev = nullptr;       // recorded after its last batch
+  hipStream_t stream = nullptr;  // stream of its last batch
+  uint64_t used = 0;             // LRU clock
+  ~MatchWs() {
+    if (ev) hipEventDestroy(ev);
+  }
+};
+constexpr uint32_t MATCH_WORKSPACES = 2;
+
 // One device copy of the table image.  Two slots alternate: a commit writes
 // the slot that is NOT current, so batches still reading the current epoch are
 // never disturbed, and it brings that slot up to date with the records the
@@ -149,12 +163,15 @@ struct egm_ctx {
   CommitStats last_commit;
   std::string err;
 
-  // per-batch workspace
-  DevBuf wid, lv, tfl, cnt, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats;
-  uint64_t pieces_cap = 0, ids_tmp_cap = 0;
+  // per-batch match workspaces: batches on different streams get different
+  // ones, so consecutive batches overlap (one's compaction with the next one's
+  // walk); a workspace reused from another stream waits for its last batch
+  MatchWs ws[MATCH_WORKSPACES];
+  uint32_t cur_ws = 0;           // workspace of the last batch (egm_last_stats)
+  hipEvent_t walk_order = nullptr;   // end of the last walk (launch_match)
+  uint64_t ws_clock = 0;
   DevBuf in_blob, in_off, out_row, out_ids;
   uint32_t heavy_waves = 64;     // waves of the heavy kernel (rare path; each owns an HBM stack)
-  uint32_t heavy_cap = 0;        // stack items per heavy wave
   uint32_t debug = 0;
   MatchStats last{};
   bool last_pending = false;
@@ -492,62 +509,86 @@ static int commit_locked(egm_ctx* c, uint64_t* epoch) {
 
 // max_levels: an upper bound on the levels of any topic of the batch (the
 // heavy kernel's stack must hold the deepest one's DFS, egm_kernels.hip).
-static int ensure_work(egm_ctx* c, uint32_t n, uint64_t blob_bytes, uint64_t ids_cap, uint64_t max_levels) {
+// The workspace for a batch on stream s: the one that last ran on s (stream
+// order protects it), else the least recently used one, ordered after its
+// last batch on the other stream.
+static MatchWs& pick_ws(egm_ctx* c, hipStream_t s) {
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < MATCH_WORKSPACES; ++i) {
+    if (c->ws[i].stream == s && c->ws[i].used) {
+      k = i;
+      break;
+    }
+    if (c->ws[i].used < c->ws[k].used) k = i;
+  }
+  MatchWs& W = c->ws[k];
+  if (W.stream && W.stream != s && W.ev) hipStreamWaitEvent(s, W.ev, 0);
+  c->cur_ws = k;
+  W.used = ++c->ws_clock;
+  return W;
+}
+
+// max_levels: an upper bound on the levels of any topic of the batch (the
+// heavy kernel's stack must hold the deepest one's DFS, egm_kernels.hip).
+static int ensure_work(egm_ctx* c, MatchWs& W, uint32_t n, uint64_t blob_bytes, uint64_t ids_cap,
+                       uint64_t max_levels) {
   hipError_t e;
   const uint64_t nn = (uint64_t)n + 1;
-  if ((e = c->wid.ensure((blob_bytes + nn) * 4)) != hipSuccess) return c->hip_fail(e, "wid");
-  if ((e = c->lv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "lv");
-  if ((e = c->tfl.ensure(nn)) != hipSuccess) return c->hip_fail(e, "tfl");
-  if ((e = c->cnt.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "cnt");
+  if ((e = W.wid.ensure((blob_bytes + nn) * 4)) != hipSuccess) return c->hip_fail(e, "wid");
+  if ((e = W.lv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "lv");
+  if ((e = W.tfl.ensure(nn)) != hipSuccess) return c->hip_fail(e, "tfl");
+  if ((e = W.cnt.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "cnt");
   // ids in flush order and their pieces, plus the slack of per-wave slabs
   const uint64_t tcap = ids_tmp_capacity(ids_cap, n);
   if (tcap >= 0xFFFFFFF0ull) return c->fail(EGM_E_INVAL, "batch too large: > 4G matched ids (split it)");
-  if ((e = c->ids_tmp.ensure(tcap * 4)) != hipSuccess) return c->hip_fail(e, "ids_tmp");
-  c->ids_tmp_cap = c->ids_tmp.cap / 4;
-  if ((e = c->pieces.ensure(pieces_capacity(ids_cap, n) * 16)) != hipSuccess) return c->hip_fail(e, "pieces");
-  c->pieces_cap = std::min<uint64_t>(c->pieces.cap / 16, 0xFFFFFFF0ull);
-  if ((e = c->deferred.ensure((n / WALK_CHUNK + 2) * 4)) != hipSuccess) return c->hip_fail(e, "deferred");
+  if ((e = W.ids_tmp.ensure(tcap * 4)) != hipSuccess) return c->hip_fail(e, "ids_tmp");
+  W.ids_tmp_cap = W.ids_tmp.cap / 4;
+  if ((e = W.pieces.ensure(pieces_capacity(ids_cap, n) * 16)) != hipSuccess) return c->hip_fail(e, "pieces");
+  W.pieces_cap = std::min<uint64_t>(W.pieces.cap / 16, 0xFFFFFFF0ull);
+  if ((e = W.deferred.ensure((n / WALK_CHUNK + 2) * 4)) != hipSuccess) return c->hip_fail(e, "deferred");
   const uint32_t hcap = heavy_stack_items(max_levels);
-  if ((e = c->heavy_stack.ensure((uint64_t)c->heavy_waves * hcap * 16)) != hipSuccess)
+  if ((e = W.heavy_stack.ensure((uint64_t)c->heavy_waves * hcap * 16)) != hipSuccess)
     return c->hip_fail(e, "heavy stack");
-  c->heavy_cap = (uint32_t)std::min<uint64_t>(c->heavy_stack.cap / 16 / c->heavy_waves, 0xFFFFFFFFull);
-  if ((e = c->tile_sums.ensure((scan_tiles(n) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "tile_sums");
-  if ((e = c->stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "stats");
+  W.heavy_cap = (uint32_t)std::min<uint64_t>(W.heavy_stack.cap / 16 / c->heavy_waves, 0xFFFFFFFFull);
+  if ((e = W.tile_sums.ensure((scan_tiles(n) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "tile_sums");
+  if ((e = W.stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "stats");
+  if (!W.ev && (e = hipEventCreateWithFlags(&W.ev, hipEventDisableTiming)) != hipSuccess)
+    return c->hip_fail(e, "workspace event");
   return EGM_OK;
 }
 
-static MatchWork work_view(egm_ctx* c) {
+static MatchWork work_view(egm_ctx* c, MatchWs& W) {
   MatchWork w{};
-  w.wid = c->wid.as<uint32_t>();
-  w.lv = c->lv.as<uint32_t>();
-  w.tfl = c->tfl.as<uint8_t>();
-  w.cnt = c->cnt.as<uint32_t>();
-  w.ids_tmp = c->ids_tmp.as<uint32_t>();
-  w.ids_cap = c->ids_tmp_cap;   // ids_tmp entries (the output capacity is MatchOut's)
-  w.pieces = c->pieces.as<uint4>();
-  w.pieces_cap = c->pieces_cap;
-  w.deferred = c->deferred.as<uint32_t>();
-  w.heavy_stack = c->heavy_stack.as<uint4>();
+  w.wid = W.wid.as<uint32_t>();
+  w.lv = W.lv.as<uint32_t>();
+  w.tfl = W.tfl.as<uint8_t>();
+  w.cnt = W.cnt.as<uint32_t>();
+  w.ids_tmp = W.ids_tmp.as<uint32_t>();
+  w.ids_cap = W.ids_tmp_cap;   // ids_tmp entries (the output capacity is MatchOut's)
+  w.pieces = W.pieces.as<uint4>();
+  w.pieces_cap = W.pieces_cap;
+  w.deferred = W.deferred.as<uint32_t>();
+  w.heavy_stack = W.heavy_stack.as<uint4>();
   w.heavy_waves = c->heavy_waves;
-  w.heavy_cap = c->heavy_cap;
-  w.tile_sums = c->tile_sums.as<uint64_t>();
-  w.stats = c->stats.as<MatchStats>();
+  w.heavy_cap = W.heavy_cap;
+  w.tile_sums = W.tile_sums.as<uint64_t>();
+  w.stats = W.stats.as<MatchStats>();
   w.debug = c->debug;
   return w;
 }
 
-static int run_match(egm_ctx* c, const Epoch& ep, const uint8_t* d_blob, const uint32_t* d_off, uint32_t n,
-                     int mode, hipStream_t s, uint64_t* d_row, uint32_t* d_ids, uint64_t ids_cap) {
-  MatchWork w = work_view(c);
+static int run_match(egm_ctx* c, MatchWs& W, const Epoch& ep, const uint8_t* d_blob, const uint32_t* d_off,
+                     uint32_t n, int mode, hipStream_t s, uint64_t* d_row, uint32_t* d_ids, uint64_t ids_cap) {
+  MatchWork w = work_view(c, W);
   MatchOut o{d_row, d_ids, ids_cap};
   hipEvent_t evp[2] = {nullptr, nullptr};
   if (c->timing) {
     evp[0] = c->take_event();
     evp[1] = c->take_event();
   }
-  c->work_begin(s);
-  hipError_t e = launch_match(ep.view, d_blob, d_off, n, mode, w, o, s, c->timing ? evp : nullptr);
-  c->work_end(s);
+  if (!c->walk_order && hipEventCreateWithFlags(&c->walk_order, hipEventDisableTiming) != hipSuccess)
+    c->walk_order = nullptr;
+  hipError_t e = launch_match(ep.view, d_blob, d_off, n, mode, w, o, s, c->timing ? evp : nullptr, c->walk_order);
   note_use(c, ep.slot, s);   // a later commit must not overwrite this slot before the walk is done
   if (c->timing) {
     c->ev_walk.push_back(evp[0]);
@@ -559,11 +600,17 @@ static int run_match(egm_ctx* c, const Epoch& ep, const uint8_t* d_blob, const u
   return EGM_OK;
 }
 
+// After the batch's last use of W on s (a flags/counts copy included).
+static void ws_done(MatchWs& W, hipStream_t s) {
+  hipEventRecord(W.ev, s);
+  W.stream = s;
+}
+
 static int sync_last(egm_ctx* c) {
   if (!c->last_pending) return EGM_OK;
   hipError_t e = hipStreamSynchronize(c->last_stream);
   if (e != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize");
-  e = hipMemcpy(&c->last, c->stats.p, sizeof(MatchStats), hipMemcpyDeviceToHost);
+  e = hipMemcpy(&c->last, c->ws[c->cur_ws].stats.p, sizeof(MatchStats), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return c->hip_fail(e, "stats readback");
   c->last_pending = false;
   return EGM_OK;
@@ -629,7 +676,7 @@ int egm_open(const egm_config* cfg, egm_ctx** out) {
     return EGM_E_DEVICE;
   }
   if (cfg && cfg->max_batch)
-    ensure_work(c, cfg->max_batch, (uint64_t)cfg->max_batch * 64, (uint64_t)cfg->max_batch * 4, 1024);
+    ensure_work(c, c->ws[0], cfg->max_batch, (uint64_t)cfg->max_batch * 64, (uint64_t)cfg->max_batch * 4, 1024);
   *out = c;
   return EGM_OK;
 }
@@ -649,6 +696,8 @@ void egm_close(egm_ctx* c) {
     c->patch_host = nullptr;
     if (c->work_ev) hipEventDestroy(c->work_ev);
     c->work_ev = nullptr;
+    if (c->walk_order) hipEventDestroy(c->walk_order);
+    c->walk_order = nullptr;
     if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
     if (c->d2h_stream) hipStreamSynchronize(c->d2h_stream);
     c->pipe.clear();
@@ -749,16 +798,17 @@ int egm_match_device(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, con
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
   // a topic has at most (its bytes + 1) levels, and a legal one at most 65 536
   // (emqx_topic.erl:45, 99-100): bound the device batch's depth by its blob
-  int r = ensure_work(c, n, blob_bytes, ids_cap, std::min<uint64_t>(blob_bytes, 65535) + 1);
+  MatchWs& W = pick_ws(c, s);
+  int r = ensure_work(c, W, n, blob_bytes, ids_cap, std::min<uint64_t>(blob_bytes, 65535) + 1);
   if (r) return r;
   std::shared_ptr<Epoch> ep = c->cur;
-  r = run_match(c, *ep, d_blob, d_off, n, mode, s, d_row, d_ids, ids_cap);
-  if (r) return r;
-  if (d_flags && n) {
-    hipError_t e = hipMemcpyAsync(d_flags, c->tfl.p, n, hipMemcpyDeviceToDevice, s);
-    if (e != hipSuccess) return c->hip_fail(e, "flags copy");
+  r = run_match(c, W, *ep, d_blob, d_off, n, mode, s, d_row, d_ids, ids_cap);
+  if (r == EGM_OK && d_flags && n) {
+    hipError_t e = hipMemcpyAsync(d_flags, W.tfl.p, n, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) r = c->hip_fail(e, "flags copy");
   }
-  return EGM_OK;
+  ws_done(W, s);
+  return r;
 }
 
 int egm_last_commit_stats(egm_ctx* c, uint64_t* h2d_bytes, uint64_t* d2d_bytes, uint64_t* patched,
@@ -852,7 +902,8 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   const uint64_t n = S.n;
   std::shared_ptr<Epoch> ep = c->cur;
   S.epoch = ep->id;
-  int r = ensure_work(c, S.n, S.bytes, S.cap, S.maxlen + 1);
+  MatchWs& W = pick_ws(c, s);
+  int r = ensure_work(c, W, S.n, S.bytes, S.cap, S.maxlen + 1);
   if (r) return r;
   if ((e = S.d_row.ensure((n + 1) * 8)) != hipSuccess) return c->hip_fail(e, "pipe row");
   if ((e = S.d_ids.ensure((S.cap + 1) * 4)) != hipSuccess) return c->hip_fail(e, "pipe ids");
@@ -860,15 +911,21 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   if ((e = S.d_cnt.ensure(n * 4 + 16)) != hipSuccess) return c->hip_fail(e, "pipe counts");
   if ((e = S.h_stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "pipe stats");
   if ((e = hipStreamWaitEvent(s, S.ev_in, 0)) != hipSuccess) return c->hip_fail(e, "pipe wait input");
-  r = run_match(c, *ep, S.d_blob.as<uint8_t>(), S.d_off.as<uint32_t>(), S.n, S.mode, s, S.d_row.as<uint64_t>(),
+  r = run_match(c, W, *ep, S.d_blob.as<uint8_t>(), S.d_off.as<uint32_t>(), S.n, S.mode, s, S.d_row.as<uint64_t>(),
                 S.d_ids.as<uint32_t>(), S.cap);
-  if (r) return r;
+  if (r) {
+    ws_done(W, s);
+    return r;
+  }
   c->last_pending = false;   // this batch's counters travel with the slot
-  if ((n && (e = hipMemcpyAsync(S.d_flags.p, c->tfl.p, n, hipMemcpyDeviceToDevice, s)) != hipSuccess) ||
-      (n && (e = hipMemcpyAsync(S.d_cnt.p, c->cnt.p, n * 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) ||
-      (e = hipMemcpyAsync(S.h_stats.p, c->stats.p, sizeof(MatchStats), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipEventRecord(S.ev_done, s)) != hipSuccess)
+  if ((n && (e = hipMemcpyAsync(S.d_flags.p, W.tfl.p, n, hipMemcpyDeviceToDevice, s)) != hipSuccess) ||
+      (n && (e = hipMemcpyAsync(S.d_cnt.p, W.cnt.p, n * 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) ||
+      (e = hipMemcpyAsync(S.h_stats.p, W.stats.p, sizeof(MatchStats), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipEventRecord(S.ev_done, s)) != hipSuccess) {
+    ws_done(W, s);
     return c->hip_fail(e, "pipe epilogue");
+  }
+  ws_done(W, s);
   return EGM_OK;
 }
 

@@ -7,6 +7,7 @@
 #   tests      pytest -m gpu, fast tests only (not the full-size ones)
 #   scale      pytest -m "gpu and slow": the full-size C1/C2/C3/C4 parity tests
 #   bench      bench.py C2 (driver command shape) + rocprofv3 --stats -> gpurun_out/TAG_prof
+#   bench_sK   the C2 bench with K streams (bench_s1: no overlap of consecutive batches)
 #   bench_c1|bench_c3|bench_c4   the other configs under rocprofv3 --stats
 #   shard1     bench.py --mode shard at world 1 via torch.distributed.run
 #   pmc        FETCH_SIZE and WRITE_SIZE passes over the C2 bench (one counter per pass)
@@ -42,6 +43,9 @@ for step in "$@"; do
     tests) run tests 900 python -u -m pytest tests -m "gpu and not slow" -x -v --timeout 300 --timeout-method thread ;;
     scale) run scale 1100 python -u -m pytest tests -m "gpu and slow" -x -v --timeout 600 --timeout-method thread ;;
     bench) run bench 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o run --output-format csv -- $B --steps 20 --warmup 5 ;;
+    bench_s[0-9])
+      k=${step#bench_s}
+      run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_s$k" -o run --output-format csv -- $B --steps 20 --warmup 5 --streams "$k" --cpu-baseline off ;;
     bench_c1|bench_c3|bench_c4)
       cfg=${step#bench_}
       run "$step" 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$cfg" -o run --output-format csv -- $B --config "$cfg" --steps 10 --warmup 2 ;;

@@ -1,19 +1,20 @@
-"""Per-kernel PMC counter averages from rocprofv3 counter_collection CSVs.
-
-    python tools/pmc_summary.py gpurun_out/pmc_tcc gpurun_out/pmc_sq ...
-"""
+"""Per-kernel means of rocprofv3 --pmc passes: python tools/pmc_summary.py TAG > profiles/X.txt
+(reads gpurun_out/TAG_pmc_*/run_counter_collection.csv)."""
 import collections
 import csv
+import glob
 import os
 import sys
 
-for d in sys.argv[1:]:
-    agg = collections.defaultdict(float)
-    n = collections.Counter()
-    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
-        k = r["Kernel_Name"].split("(")[0].replace("egm::", "")
-        agg[(k, r["Counter_Name"])] += float(r["Counter_Value"])
-        n[(k, r["Counter_Name"])] += 1
-    for (k, c), v in sorted(agg.items()):
-        if k.startswith("k_") or "rand" in k:
-            print(f"{os.path.basename(d):10s} {k:14s} {c:22s} {v / n[(k, c)]:16.4g}  (x{n[(k, c)]})")
+tag = sys.argv[1]
+root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+for d in sorted(glob.glob(os.path.join(root, f"{tag}_pmc_*"))):
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        acc = collections.defaultdict(lambda: [0.0, 0])
+        for r in csv.DictReader(open(f)):
+            k = (r["Kernel_Name"].split("(")[0].replace("egm::", ""), r["Counter_Name"])
+            acc[k][0] += float(r["Counter_Value"])
+            acc[k][1] += 1
+        for (kn, cn), (v, c) in sorted(acc.items()):
+            if kn.startswith("k_"):
+                print(f"{os.path.basename(d)[len(tag) + 1:]:10s} {kn:14s} {cn:22s} {v / max(1, c):12.4g}  (mean of {c})")
