@@ -118,6 +118,35 @@ def cpu_baseline(f, t, match_mode: int, seconds: float) -> dict:
             "host": hostinfo.describe()}
 
 
+def host_e2e(gm, t, mode, batch: int = 1_000_000, batches: int = 8) -> dict:
+    """The PCIe-inclusive rate the NIF sees: topics/s from
+    a host topic blob to a host CSR through egm_match_submit / egm_match_wait
+    (pinned staging, H2D on a copy stream, match, D2H), two batches in
+    flight.  Never `value` (which is measured with the batch in HBM)."""
+    batch = min(batch, t.n)
+    parts = [t.subset(np.arange(i * batch, (i + 1) * batch)) for i in range(max(1, min(2, t.n // batch)))]
+    for p in parts:   # size the pipeline's buffers
+        gm.wait(gm.submit(p.blob, p.off, mode), copy=False)
+    ids = 0
+    t0 = time.perf_counter()
+    inflight = []
+    for k in range(batches):
+        p = parts[k % len(parts)]
+        inflight.append(gm.submit(p.blob, p.off, mode))
+        if len(inflight) == 2:
+            gm.wait(inflight.pop(0), copy=False)
+            ids += gm.last_stats()["n_ids"]
+    while inflight:
+        gm.wait(inflight.pop(0), copy=False)
+        ids += gm.last_stats()["n_ids"]
+    dt = time.perf_counter() - t0
+    return {"value": batch * batches / dt, "unit": "topics/s", "batch_topics": batch, "batches": batches,
+            "in_flight": 2, "ms_per_batch": dt / batches * 1e3,
+            "host_bytes_per_batch": {"in": int(parts[0].off[-1]) + 4 * (batch + 1),
+                                     "out": int(ids / batches) * 4 + 13 * batch + 8},
+            "path": "host blob -> pinned staging -> H2D -> match -> D2H into pinned CSR (egm_match_submit/wait)"}
+
+
 def _heartbeat(period: float = 30.0):
     """Progress on stderr while long host steps (100M-filter generation and
     table build) run inside ctypes calls, so a watchdog sees a live process."""
@@ -169,9 +198,15 @@ def main():
     ap.add_argument("--match", default="routes", choices=["routes", "trie"])
     ap.add_argument("--fanout", default="auto", choices=["auto", "on", "off"],
                     help="add emqx_broker:dispatch/2 subscriber fan-out to each step (auto: on for c3, c4)")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=1,
                     help="replicate mode: consecutive batches alternate over this many HIP streams (each with its "
                          "own match workspace), so one batch's compaction overlaps the next one's walk")
+    ap.add_argument("--x-presort", type=int, default=-1,
+                    help="experiment: sort the batch's topics on the host (untimed) by their first K levels "
+                         "(0: whole topic) to measure how much trie-path locality between neighbouring topics "
+                         "would save the walk")
+    ap.add_argument("--host-e2e", default="on", choices=["on", "off"],
+                    help="also time the host-visible path (pinned staging, H2D, match, D2H) at N=1")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
@@ -210,6 +245,15 @@ def main():
     tseed = seed + (0 if shard else 7919 * rank)   # shard: rank 0's batch is the one broadcast
     t = synth.topics(nt, f, c["dmin"], c["dmax"], seed=tseed)
     log(f"[rank {rank}] generated {f.n} filters, {t.n} topics in {time.time() - t0:.1f}s")
+    if args.x_presort >= 0:
+        tl = t.to_list()
+        K = args.x_presort
+        keys = tl if K == 0 else [b"/".join(x.split(b"/", K)[:K]) for x in tl]
+        order = sorted(range(len(tl)), key=keys.__getitem__)
+        del keys
+        t = t.subset(np.asarray(order, dtype=np.int64))
+        del tl, order
+        log(f"[rank {rank}] topics presorted (experiment)")
 
     gm = GpuMatcher(local, max_batch=nt)
     t0 = time.time()
@@ -394,6 +438,10 @@ def main():
     path_bytes = (nbytes + 4 * n) + 16 * sum_d + 32 * visited + 4 * (n_ids + n)
 
     traffic = walk_traffic(args.config, f.n, n) if (not shard and world == 1) else None
+    host = None
+    if _host_leg(args, world, shard):
+        log("[rank 0] timing the host-visible path ...")
+        host = host_e2e(gm, t, mode)
     if rank == 0:
         cpu = None
         if args.cpu_baseline == "auto" and world == 1 and f.n > 20_000_000:
@@ -431,12 +479,17 @@ def main():
                         "deliveries_per_s": deliveries * world * args.steps / elapsed,
                         "bytes_per_launch": 12 * deliveries + 20 * n_ids + 8 * (n + 1)}
                        if fanout else None),
+            "host_e2e": host,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     gm.close()
     if have_pg:
         dist.destroy_process_group()
+
+
+def _host_leg(args, world, shard):
+    return args.host_e2e == "on" and world == 1 and not shard
 
 
 if __name__ == "__main__":

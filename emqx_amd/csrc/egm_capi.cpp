@@ -168,7 +168,6 @@ struct egm_ctx {
   // walk); a workspace reused from another stream waits for its last batch
   MatchWs ws[MATCH_WORKSPACES];
   uint32_t cur_ws = 0;           // workspace of the last batch (egm_last_stats)
-  hipEvent_t walk_order = nullptr;   // end of the last walk (launch_match)
   uint64_t ws_clock = 0;
   DevBuf in_blob, in_off, out_row, out_ids;
   uint32_t heavy_waves = 64;     // waves of the heavy kernel (rare path; each owns an HBM stack)
@@ -586,9 +585,7 @@ static int run_match(egm_ctx* c, MatchWs& W, const Epoch& ep, const uint8_t* d_b
     evp[0] = c->take_event();
     evp[1] = c->take_event();
   }
-  if (!c->walk_order && hipEventCreateWithFlags(&c->walk_order, hipEventDisableTiming) != hipSuccess)
-    c->walk_order = nullptr;
-  hipError_t e = launch_match(ep.view, d_blob, d_off, n, mode, w, o, s, c->timing ? evp : nullptr, c->walk_order);
+  hipError_t e = launch_match(ep.view, d_blob, d_off, n, mode, w, o, s, c->timing ? evp : nullptr);
   note_use(c, ep.slot, s);   // a later commit must not overwrite this slot before the walk is done
   if (c->timing) {
     c->ev_walk.push_back(evp[0]);
@@ -696,8 +693,6 @@ void egm_close(egm_ctx* c) {
     c->patch_host = nullptr;
     if (c->work_ev) hipEventDestroy(c->work_ev);
     c->work_ev = nullptr;
-    if (c->walk_order) hipEventDestroy(c->walk_order);
-    c->walk_order = nullptr;
     if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
     if (c->d2h_stream) hipStreamSynchronize(c->d2h_stream);
     c->pipe.clear();

@@ -91,11 +91,9 @@ inline uint64_t pieces_capacity(uint64_t ids, uint32_t n) {
 }
 
 // Timing hooks: when ev != nullptr, ev[0]/ev[1] bracket the walk kernel.
-// walk_order (optional): the walk waits for it and records it when done, so
-// the walks of batches on different streams do not overlap each other.
 hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n,
                         int mode, const MatchWork& w, const MatchOut& out, hipStream_t s,
-                        hipEvent_t* ev_walk, hipEvent_t walk_order);
+                        hipEvent_t* ev_walk);
 
 // Fan-out (emqx_broker:dispatch/2, emqx_broker.erl:283-324): expand each
 // topic's filter ids through the filter -> subscriber CSR.

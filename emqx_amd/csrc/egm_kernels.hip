@@ -1209,7 +1209,7 @@ static void trace(hipStream_t s, const char* what) {
 
 hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n,
                         int mode, const MatchWork& w, const MatchOut& out, hipStream_t s,
-                        hipEvent_t* ev_walk, hipEvent_t walk_order) {
+                        hipEvent_t* ev_walk) {
   hipError_t e = hipMemsetAsync(w.stats, 0, sizeof(MatchStats), s);
   if (e != hipSuccess) return e;
   if (n == 0) {
@@ -1218,13 +1218,9 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   hipLaunchKernelGGL(k_tokenise, dim3((n + TOK_BLOCK - 1) / TOK_BLOCK), dim3(TOK_BLOCK), 0, s, tab, blob,
                      off, n, w.wid, w.lv, w.tfl);
   trace(s, "k_tokenise");
-  // walks of batches on different streams run one after the other (each
-  // fills the GPU); their tokenise / scan / compaction overlap the other's walk
-  if (walk_order) hipStreamWaitEvent(s, walk_order, 0);
   if (ev_walk) hipEventRecord(ev_walk[0], s);
   hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64), 0, s, tab, off, n, mode, w);
   if (ev_walk) hipEventRecord(ev_walk[1], s);
-  if (walk_order) hipEventRecord(walk_order, s);
   trace(s, "k_walk");
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
   trace(s, "k_heavy");

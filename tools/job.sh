@@ -43,6 +43,9 @@ for step in "$@"; do
     tests) run tests 900 python -u -m pytest tests -m "gpu and not slow" -x -v --timeout 300 --timeout-method thread ;;
     scale) run scale 1100 python -u -m pytest tests -m "gpu and slow" -x -v --timeout 600 --timeout-method thread ;;
     bench) run bench 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o run --output-format csv -- $B --steps 20 --warmup 5 ;;
+    bench_presort[0-9])
+      k=${step#bench_presort}
+      run "$step" 900 python $R/bench.py --steps 10 --warmup 2 --streams 1 --x-presort "$k" --cpu-baseline off ;;
     bench_s[0-9])
       k=${step#bench_s}
       run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_s$k" -o run --output-format csv -- $B --steps 20 --warmup 5 --streams "$k" --cpu-baseline off ;;
