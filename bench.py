@@ -128,13 +128,19 @@ def host_e2e(gm, t, mode, batch: int = 1_000_000, batches: int = 8) -> dict:
     for p in parts:   # size the pipeline's buffers
         gm.wait(gm.submit(p.blob, p.off, mode), copy=False)
     ids = 0
+    t_sub = t_wait = 0.0
     t0 = time.perf_counter()
     inflight = []
-    for k in range(batches):
-        p = parts[k % len(parts)]
-        inflight.append(gm.submit(p.blob, p.off, mode))
-        if len(inflight) == 2:
+    for k in range(batches + 1):
+        if k < batches:
+            p = parts[k % len(parts)]
+            a = time.perf_counter()
+            inflight.append(gm.submit(p.blob, p.off, mode))
+            t_sub += time.perf_counter() - a
+        if len(inflight) == 2 or (k == batches and inflight):
+            a = time.perf_counter()
             gm.wait(inflight.pop(0), copy=False)
+            t_wait += time.perf_counter() - a
             ids += gm.last_stats()["n_ids"]
     while inflight:
         gm.wait(inflight.pop(0), copy=False)
@@ -142,6 +148,7 @@ def host_e2e(gm, t, mode, batch: int = 1_000_000, batches: int = 8) -> dict:
     dt = time.perf_counter() - t0
     return {"value": batch * batches / dt, "unit": "topics/s", "batch_topics": batch, "batches": batches,
             "in_flight": 2, "ms_per_batch": dt / batches * 1e3,
+            "submit_ms_per_batch": t_sub / batches * 1e3, "wait_ms_per_batch": t_wait / batches * 1e3,
             "host_bytes_per_batch": {"in": int(parts[0].off[-1]) + 4 * (batch + 1),
                                      "out": int(ids / batches) * 4 + 13 * batch + 8},
             "path": "host blob -> pinned staging -> H2D -> match -> D2H into pinned CSR (egm_match_submit/wait)"}

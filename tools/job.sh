@@ -6,7 +6,9 @@
 # Steps (each under its own time limit, logs in gpurun_out/TAG_<step>.log):
 #   tests      pytest -m gpu, fast tests only (not the full-size ones)
 #   scale      pytest -m "gpu and slow": the full-size C1/C2/C3/C4 parity tests
-#   bench      bench.py C2 (driver command shape) + rocprofv3 --stats -> gpurun_out/TAG_prof
+#   bench      bench.py C2 under rocprofv3 --stats -> gpurun_out/TAG_prof (host leg off: the
+#              rocprof averages are then over the 10M-topic launches only)
+#   drv        the driver's command as is (python bench.py --gpus 1 --steps 20 --warmup 5)
 #   bench_sK   the C2 bench with K streams (bench_s1: no overlap of consecutive batches)
 #   bench_c1|bench_c3|bench_c4   the other configs under rocprofv3 --stats
 #   shard1     bench.py --mode shard at world 1 via torch.distributed.run
@@ -42,28 +44,29 @@ for step in "$@"; do
   case $step in
     tests) run tests 900 python -u -m pytest tests -m "gpu and not slow" -x -v --timeout 300 --timeout-method thread ;;
     scale) run scale 1100 python -u -m pytest tests -m "gpu and slow" -x -v --timeout 600 --timeout-method thread ;;
-    bench) run bench 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o run --output-format csv -- $B --steps 20 --warmup 5 ;;
+    bench) run bench 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o run --output-format csv -- $B --steps 20 --warmup 5 --host-e2e off ;;
+    drv) run drv 600 python $R/bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench_presort[0-9])
       k=${step#bench_presort}
       run "$step" 900 python $R/bench.py --steps 10 --warmup 2 --streams 1 --x-presort "$k" --cpu-baseline off ;;
     bench_s[0-9])
       k=${step#bench_s}
-      run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_s$k" -o run --output-format csv -- $B --steps 20 --warmup 5 --streams "$k" --cpu-baseline off ;;
+      run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_s$k" -o run --output-format csv -- $B --steps 20 --warmup 5 --streams "$k" --cpu-baseline off --host-e2e off ;;
     bench_c1|bench_c3|bench_c4)
       cfg=${step#bench_}
-      run "$step" 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$cfg" -o run --output-format csv -- $B --config "$cfg" --steps 10 --warmup 2 ;;
+      run "$step" 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$cfg" -o run --output-format csv -- $B --config "$cfg" --steps 10 --warmup 2 --host-e2e off ;;
     shard1) run shard1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --mode shard --steps 10 --warmup 2 --cpu-baseline off ;;
     pmc)
-      run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off
-      run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc_write" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off ;;
+      run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off
+      run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc_write" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off ;;
     sq)
-      run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU -d "$R/gpurun_out/${TAG}_pmc_sq" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off
-      run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off ;;
+      run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU -d "$R/gpurun_out/${TAG}_pmc_sq" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off
+      run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off ;;
     host) run host 600 python tools/bench_host.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     ab_*)   # A/B variant built by tools/build_variant.py: C2 bench under rocprof stats
       v=${step#ab_}
-      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$v" -o run --output-format csv -- $B --steps 10 --warmup 2 --cpu-baseline off ;;
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$v" -o run --output-format csv -- $B --steps 10 --warmup 2 --cpu-baseline off --host-e2e off ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
