@@ -480,7 +480,8 @@ def main():
                       "merged_ids_per_step": merged_ids,
                       "deferred_chunks": st["deferred_chunks"], "walk_iters": wc["iters"],
                       "walk_popped": wc["popped"], "walk_bounded_pops": wc["bounded"],
-                      "walk_lane_occupancy": wc["lane_occupancy"]},
+                      "walk_lane_occupancy": wc["lane_occupancy"], "walk_bucket_reads": wc["lit_probes"],
+                      "walk_plus_record_reads": wc["plus_reads"]},
             "fanout": ({"deliveries_per_step": deliveries, "subscriber_entries": sub_entries,
                         "fanout_ms": tim["fanout_ms"] / max(1, tim["fanout_launches"]),
                         "deliveries_per_s": deliveries * world * args.steps / elapsed,

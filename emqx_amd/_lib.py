@@ -91,7 +91,7 @@ SIGNATURES = {
     "egm_match_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(C.POINTER(egm_result))]),
     "egm_match_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, _P, _P, C.c_uint64, _P]),
     "egm_last_stats": (C.c_int, [_P, _u64p, _u64p, _u32p, _u32p, _u32p]),
-    "egm_last_walk_counters": (C.c_int, [_P, _u64p, _u64p, _u64p]),
+    "egm_last_walk_counters": (C.c_int, [_P, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "egm_set_timing": (C.c_int, [_P, C.c_int]),
     "egm_set_debug": (C.c_int, [_P, C.c_uint32]),
     "egm_get_timing": (C.c_int, [_P, C.POINTER(C.c_double), _u64p, C.POINTER(C.c_double), _u64p]),

@@ -817,7 +817,8 @@ int egm_last_commit_stats(egm_ctx* c, uint64_t* h2d_bytes, uint64_t* d2d_bytes, 
   return EGM_OK;
 }
 
-int egm_last_walk_counters(egm_ctx* c, uint64_t* iters, uint64_t* popped, uint64_t* bounded) {
+int egm_last_walk_counters(egm_ctx* c, uint64_t* iters, uint64_t* popped, uint64_t* bounded, uint64_t* lit_probes,
+                           uint64_t* plus_reads) {
   if (!c) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   int r = sync_last(c);
@@ -825,6 +826,8 @@ int egm_last_walk_counters(egm_ctx* c, uint64_t* iters, uint64_t* popped, uint64
   if (iters) *iters = c->last.iters;
   if (popped) *popped = c->last.popped;
   if (bounded) *bounded = c->last.bounded;
+  if (lit_probes) *lit_probes = c->last.lit_probes;
+  if (plus_reads) *plus_reads = c->last.plus_reads;
   return EGM_OK;
 }
 

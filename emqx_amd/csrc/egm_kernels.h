@@ -32,8 +32,8 @@ struct MatchStats {               // device-side counters, zeroed per batch
   unsigned long long iters;       // walk iterations (instrumentation)
   unsigned long long popped;      // items popped by the walk (lane occupancy = popped / (iters * 64))
   unsigned long long bounded;     // walk iterations whose pop was cut by the stack-room bound (DFS regime)
-  unsigned int next_chunk;        // chunk counter of the persistent walk waves
-  unsigned int pad;
+  unsigned long long lit_probes;  // walk pops that read an edge bucket (instrumentation)
+  unsigned long long plus_reads;  // walk pops that read a '+' child's record (instrumentation)
 };
 
 // A piece is one flush's run of a topic's ids in ids_tmp:

@@ -682,7 +682,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
   root.z = uni(root.z);
   root.w = uni(root.w);
   uint32_t created = 0;
-  unsigned long long iters = 0, popped = 0, bounded = 0;
+  unsigned long long iters = 0, popped = 0, bounded = 0, lit_probes = 0, plus_reads = 0;
   Slab sid{0, 0}, spc{0, 0};
   for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const uint32_t t0 = c * WALK_CHUNK;
@@ -803,6 +803,8 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         p.D = ti & 0xFFFFFFu;
         p.d1 = p.D == 1 && ((ti >> 24) & TF_DOLLAR);
         issue(tab, L.words + L.tbase[tt], nullptr, 0, p);
+        lit_probes += popc(__ballot(p.lit));
+        plus_reads += popc(__ballot(p.plus));
         wave_sync();
         // ---- consume: children -> stack, emits -> stage ----
         Out o;
@@ -863,6 +865,8 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
     atomicAdd(&w.stats->iters, iters);
     atomicAdd(&w.stats->popped, popped);
     if (bounded) atomicAdd(&w.stats->bounded, bounded);
+    atomicAdd(&w.stats->lit_probes, lit_probes);
+    atomicAdd(&w.stats->plus_reads, plus_reads);
   }
 }
 

@@ -221,11 +221,12 @@ class GpuMatcher:
                 "errors": e.value}
 
     def walk_counters(self) -> dict:
-        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
-        self._check(self.lib.egm_last_walk_counters(self.ctx, C.byref(a), C.byref(b), C.byref(c)),
-                    "egm_last_walk_counters")
+        a, b, c, d, e = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._check(self.lib.egm_last_walk_counters(self.ctx, C.byref(a), C.byref(b), C.byref(c), C.byref(d),
+                                                    C.byref(e)), "egm_last_walk_counters")
         occ = b.value / max(1, a.value * 64)
-        return {"iters": a.value, "popped": b.value, "bounded": c.value, "lane_occupancy": occ}
+        return {"iters": a.value, "popped": b.value, "bounded": c.value, "lane_occupancy": occ,
+                "lit_probes": d.value, "plus_reads": e.value}
 
     def set_debug(self, flags: int):
         self._check(self.lib.egm_set_debug(self.ctx, flags), "egm_set_debug")

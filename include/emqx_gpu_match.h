@@ -164,9 +164,12 @@ int egm_match_device(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes, c
 int egm_last_stats(egm_ctx* ctx, uint64_t* n_ids, uint64_t* visited, uint32_t* n_deferred_chunks,
                    uint32_t* overflow, uint32_t* n_error);
 /* Instrumentation: walk iterations and items popped of the last batch (lane
-   occupancy = popped / (iters*64)), and the iterations whose pop the
-   stack-room bound cut short (the depth-first regime of deep, wide frontiers). */
-int egm_last_walk_counters(egm_ctx* ctx, uint64_t* iters, uint64_t* popped, uint64_t* bounded);
+   occupancy = popped / (iters*64)), the iterations whose pop the stack-room
+   bound cut short (the depth-first regime of deep, wide frontiers), and the
+   pops that read an edge bucket / a '+' child's record (the walk's random
+   line reads).  Any pointer may be NULL. */
+int egm_last_walk_counters(egm_ctx* ctx, uint64_t* iters, uint64_t* popped, uint64_t* bounded, uint64_t* lit_probes,
+                           uint64_t* plus_reads);
 /* Enable per-kernel timing with HIP events on the launch stream (0/1) and read
    the accumulated walk-kernel time (ms) and launch count. */
 int egm_set_timing(egm_ctx* ctx, int enable);
