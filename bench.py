@@ -212,6 +212,11 @@ def main():
                     help="experiment: sort the batch's topics on the host (untimed) by their first K levels "
                          "(0: whole topic) to measure how much trie-path locality between neighbouring topics "
                          "would save the walk")
+    ap.add_argument("--x-orders", default="",
+                    help="experiment: after the timed steps, time the same steps under each walk order "
+                         "'shape/slabs,...' (EGM_WALK_KEY: key bits per level as hex nibbles, level 0 lowest, 0 = "
+                         "input order; EGM_CHUNK_SLABS 0/1) and check "
+                         "that every order gives the same rows (stderr)")
     ap.add_argument("--host-e2e", default="on", choices=["on", "off"],
                     help="also time the host-visible path (pinned staging, H2D, match, D2H) at N=1")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
@@ -430,6 +435,8 @@ def main():
         iso_ms = ti["walk_ms"] / max(1, ti["walk_launches"])
         gm.set_timing(False)
     merged_ids = sum(exchange.last_totals) if exchange is not None else None
+    if args.x_orders and exchange is None:
+        order_experiment(args, gm, run_local, bufs, dev, n)
 
     units_per_step = n if shard else n * world
     value = units_per_step * args.steps / elapsed
@@ -494,6 +501,55 @@ def main():
     gm.close()
     if have_pg:
         dist.destroy_process_group()
+
+
+def order_experiment(args, gm, run_local, bufs, dev, n):
+    """Walk-order A/B inside one process (the table is built once): steps
+    timed per order, rows checked against the default order's (row_ptr equal,
+    per-row id sums equal)."""
+    import torch
+
+    def rows_sig():
+        row, ids = bufs["rows"][0], bufs["idss"][0]
+        tot = int(row[n].item())
+        cs = torch.cumsum(ids[:tot].to(torch.int64), 0)
+        cs = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), cs])
+        return row.clone(), cs[row]
+
+    saved = {k: os.environ.get(k) for k in ("EGM_WALK_KEY", "EGM_CHUNK_SLABS")}
+    bufs["k"] = 0
+    run_local()
+    torch.cuda.synchronize(dev)
+    ref_row, ref_sig = rows_sig()
+    for spec in args.x_orders.split(","):
+        shape, _, slabs = spec.partition("/")
+        os.environ["EGM_WALK_KEY"], os.environ["EGM_CHUNK_SLABS"] = shape, slabs or "1"
+        for _ in range(2):
+            bufs["k"] = 0
+            run_local()
+        torch.cuda.synchronize(dev)
+        gm.set_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            bufs["k"] = 0
+            run_local()
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / args.steps
+        tim = gm.get_timing()
+        gm.set_timing(False)
+        wc = gm.walk_counters()
+        row, sig = rows_sig()
+        same = bool(torch.equal(row, ref_row) and torch.equal(sig, ref_sig))
+        log(json.dumps({"order": spec, "ms_per_step": dt * 1e3,
+                        "walk_ms": tim["walk_ms"] / max(1, tim["walk_launches"]),
+                        "topics_per_s": n / dt, "lane_occupancy": wc["lane_occupancy"], "rows_equal": same}))
+        if not same:
+            raise RuntimeError(f"walk order {spec} changed the result rows")
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
 
 
 def _host_leg(args, world, shard):

@@ -107,6 +107,7 @@ constexpr size_t PIPE_MAX_SLOTS = 8;
 // One match workspace: the per-batch scratch of launch_match.
 struct MatchWs {
   DevBuf wid, lv, tfl, cnt, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats;
+  DevBuf skey, skey_out, sval, order, wfix, sort_tmp;   // walk-order sort (egm_kernels.hip walk_key)
   uint64_t pieces_cap = 0, ids_tmp_cap = 0;
   uint32_t heavy_cap = 0;        // stack items per heavy wave
   hipEvent_t ev = nullptr;       // recorded after its last batch
@@ -506,8 +507,15 @@ static int commit_locked(egm_ctx* c, uint64_t* epoch) {
   return EGM_OK;
 }
 
-// max_levels: an upper bound on the levels of any topic of the batch (the
-// heavy kernel's stack must hold the deepest one's DFS, egm_kernels.hip).
+// Walk order: the sort key's bits per level as hex nibbles,
+// level 0 in the lowest; 0 walks in input order.  EGM_WALK_KEY is a tuning
+// knob for A/B runs (read at every batch); the default is the measured best.
+static uint32_t walk_key_shape() {
+  const char* v = getenv("EGM_WALK_KEY");
+  const uint32_t shape = (v && *v) ? (uint32_t)strtoul(v, nullptr, 16) & 0xFFFFu : 0x8888u;   // KEY_LEVELS nibbles
+  return walk_key_bits(shape) <= 32 ? shape : 0x8888u;
+}
+
 // The workspace for a batch on stream s: the one that last ran on s (stream
 // order protects it), else the least recently used one, ordered after its
 // last batch on the other stream.
@@ -551,6 +559,15 @@ static int ensure_work(egm_ctx* c, MatchWs& W, uint32_t n, uint64_t blob_bytes, 
   W.heavy_cap = (uint32_t)std::min<uint64_t>(W.heavy_stack.cap / 16 / c->heavy_waves, 0xFFFFFFFFull);
   if ((e = W.tile_sums.ensure((scan_tiles(n) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "tile_sums");
   if ((e = W.stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "stats");
+  const uint32_t shape = walk_key_shape();
+  if (shape) {
+    if ((e = W.skey.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "sort keys");
+    if ((e = W.skey_out.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "sort keys");
+    if ((e = W.sval.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "sort values");
+    if ((e = W.order.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "walk order");
+    if ((e = W.wfix.ensure(nn * 4 * FIX_WORDS)) != hipSuccess) return c->hip_fail(e, "fixed-stride words");
+    if ((e = W.sort_tmp.ensure(walk_sort_temp_bytes(n, shape))) != hipSuccess) return c->hip_fail(e, "sort scratch");
+  }
   if (!W.ev && (e = hipEventCreateWithFlags(&W.ev, hipEventDisableTiming)) != hipSuccess)
     return c->hip_fail(e, "workspace event");
   return EGM_OK;
@@ -573,6 +590,22 @@ static MatchWork work_view(egm_ctx* c, MatchWs& W) {
   w.tile_sums = W.tile_sums.as<uint64_t>();
   w.stats = W.stats.as<MatchStats>();
   w.debug = c->debug;
+  w.key_shape = walk_key_shape();
+  if (w.key_shape && W.order.p) {
+    w.skey = W.skey.as<uint32_t>();
+    w.skey_out = W.skey_out.as<uint32_t>();
+    w.sval = W.sval.as<uint64_t>();
+    w.order = W.order.as<uint64_t>();
+    w.wfix = W.wfix.as<uint32_t>();
+    w.sort_tmp = W.sort_tmp.p;
+    w.sort_tmp_bytes = W.sort_tmp.cap;
+  } else {
+    w.key_shape = 0;
+  }
+  {
+    const char* v = getenv("EGM_CHUNK_SLABS");   // A/B knob
+    w.chunk_slabs = (v && *v) ? (uint32_t)atoi(v) : 1u;
+  }
   return w;
 }
 

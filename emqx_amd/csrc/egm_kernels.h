@@ -43,7 +43,7 @@ struct MatchStats {               // device-side counters, zeroed per batch
 // slab): a single shared counter bumped per flush serialises across the 8
 // XCDs at the memory side.
 constexpr uint32_t SLAB_IDS = 4096;
-constexpr uint32_t SLAB_PIECES = 256;
+constexpr uint32_t SLAB_PIECES = 512;
 
 struct MatchWork {                // per-batch device workspace
   uint32_t* wid;                  // [blob_bytes + n] word ids, topic t at off[t] + t
@@ -61,9 +61,37 @@ struct MatchWork {                // per-batch device workspace
   uint64_t* tile_sums;            // scan scratch
   MatchStats* stats;
   uint32_t debug;                 // DEBUG_* bits
+  // Locality order of the walk: k_tokenise keys each topic
+  // by hashes of its first levels' word ids, a radix sort orders the topics'
+  // records, and the walk takes its chunks from the sorted records, so the
+  // topics a wave walks together share trie paths.
+  uint32_t* skey;                 // [n] sort keys (k_tokenise)
+  uint32_t* skey_out;             // [n]
+  uint64_t* sval;                 // [n] topic records (k_tokenise): t | (D | f << 24 | fixed << 31) << 32
+  uint64_t* order;                // [n] the records in walk order (null: walk in input order)
+  uint32_t* wfix;                 // [n * FIX_WORDS] first word ids of each topic at a fixed stride
+  void* sort_tmp;                 // radix sort scratch
+  size_t sort_tmp_bytes;
+  uint32_t key_shape;             // key bits per level, nibble l = level l (0: walk in input order)
+  uint32_t chunk_slabs;           // each chunk's pieces start a pieces slab (k_compact: a slab per wave)
+};
+
+constexpr uint32_t KEY_LEVELS = 4;           // levels hashed into the walk-order key
+constexpr uint32_t FIX_WORDS = 8;            // word ids per topic at the fixed stride (deeper: wid[] at off[t] + t)
+struct WalkOrderOut {                        // what k_tokenise writes for the sort (all null: nothing)
+  uint32_t* key;
+  uint64_t* val;
+  uint32_t* wfix;
+  uint32_t shape;
 };
 
 constexpr uint32_t DEBUG_FORCE_HEAVY = 1u;   // every chunk goes to k_heavy (test coverage)
+constexpr uint32_t DEBUG_INPUT_ORDER = 4u;   // walk in input order (no locality sort)
+
+// walk-order key: total bits of a key shape; radix sort scratch bytes for a
+// batch of n topics (hipcub)
+uint32_t walk_key_bits(uint32_t shape);
+size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape);
 
 struct MatchOut {                 // CSR result (device)
   uint64_t* row_ptr;              // [n + 1]
@@ -87,7 +115,8 @@ inline uint64_t ids_tmp_capacity(uint64_t ids, uint32_t n) {
 inline uint64_t pieces_capacity(uint64_t ids, uint32_t n) {
   uint64_t p = 2ull * n + 4096;
   if (ids / 2 > p) p = ids / 2;
-  return p + (uint64_t)(walk_grid_blocks(n) + 256) * SLAB_PIECES;
+  // + a slab per wave and per chunk (each chunk's pieces start a slab)
+  return p + (uint64_t)(walk_grid_blocks(n) + 256 + (n + WALK_CHUNK - 1) / WALK_CHUNK) * SLAB_PIECES;
 }
 
 // Timing hooks: when ev != nullptr, ev[0]/ev[1] bracket the walk kernel.

@@ -8,15 +8,17 @@
 //   emqx_broker:dispatch/2        apps/emqx/src/emqx_broker.erl:283-324  -> k_fanout_*
 //
 // The walk is an NFA frontier expansion over the word-level trie (egm_common.h):
-// persistent wavefronts, each walking two chunks of 64 topics at once from an
-// LDS work stack (pop up to 64 items, issue their reads together, compact
-// children and emits back with __ballot / mbcnt), staging emits per topic
-// and flushing them as pieces chained per topic; k_compact assembles the CSR
-// rows from the chains.  Chunks with a topic deeper than the LDS stack allows
-// are walked by k_heavy (one topic per wave, stack in HBM).
+// topics sorted into a locality order (k_sort_key + a radix sort), then one
+// wavefront per chunk of 64 of them, walking from an LDS work stack (pop up to
+// 64 items, issue their reads together, compact children and emits back with
+// __ballot / mbcnt), staging emits per topic and flushing them as pieces;
+// k_compact assembles the CSR rows from the pieces.  Chunks with a topic
+// deeper than the LDS stack allows are walked by k_heavy (one topic per wave,
+// stack in HBM).
 //
 // This is pointer chasing over hashed edges — HBM / latency bound; no MFMA.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -32,7 +34,8 @@ constexpr int MODE_ROUTES = 1;
 
 constexpr int TOK_BLOCK = 256;
 #ifndef EGM_TOK_LDS
-#define EGM_TOK_LDS 16384   // staged topic bytes per tokenise block (A/B at C2: 24 KB -> 1.09 ms, 16 KB -> 0.92, 12 KB -> 1.12)
+#define EGM_TOK_LDS 16256   // staged topic bytes per tokenise block (A/B at C2: 24 KB -> 1.09 ms, 16 KB -> 0.92, 12 KB -> 1.12;
+                            // 16 KB - 128 B keeps 4 blocks per CU beside the walk-order key table)
 #endif
 constexpr int TOK_LDS = EGM_TOK_LDS;
 #ifndef EGM_TOK_WORDS
@@ -194,6 +197,36 @@ __device__ __forceinline__ uint32_t dict_resolve(const DevTable& tab, uint64_t h
   }
 }
 
+// ------------------------------------------------------------ walk order ----
+// The walk's key of a topic: hashes of its 1-, 2-, 3- and 4-level word-id
+// prefixes, b_l bits each (shape: b_l in nibble l, total <= 32 bits), most
+// significant first; a level the topic lacks contributes 0.  Sorting by the
+// key puts topics that share a prefix next to each other — colliding prefixes
+// interleave, a group is never split — so the 64 lanes of a wave issue the
+// same bucket reads (one request serves them all) and the L2 keeps what the
+// neighbouring waves read.  Any order gives the same result sets.  k_tokenise
+// computes the key beside the word ids, and with it the walk's record of the
+// topic (the sort's value) and its first FIX_WORDS word ids at a fixed stride,
+// so that a wave reads its sorted chunk's topics without an offsets lookup.
+__device__ __forceinline__ uint32_t walk_key(const uint32_t* w4, uint32_t D, uint32_t shape) {
+  uint64_t h = FNV_BASIS;
+  uint32_t k = 0, used = 0;
+#pragma unroll
+  for (uint32_t l = 0; l < KEY_LEVELS; ++l) {
+    const uint32_t bl = (shape >> (4 * l)) & 0xFu;
+    h = mix64((h ^ w4[l]) * FNV_PRIME);
+    const uint32_t b = (l < D && bl) ? (uint32_t)(h >> (64 - bl)) : 0u;
+    k = bl ? ((k << bl) | b) : k;
+    used += bl;
+  }
+  return used < 32 ? k << (32 - used) : k;
+}
+
+// the sort's value: topic | (levels | flags << 24 | words at the fixed stride << 31) << 32
+__device__ __forceinline__ uint64_t sort_val(uint32_t t, uint32_t D, uint32_t f, bool fixed) {
+  return (uint64_t)t | ((uint64_t)(min(D, 0xFFFFFFu) | ((f & 0x7Fu) << 24) | (fixed ? 0x80000000u : 0u)) << 32);
+}
+
 // emqx_topic:words/1 (emqx_topic.erl:153-164) + wildcard/1 (:53-62) for a
 // block of TOK_BLOCK topics, in three passes over the block's bytes staged in
 // LDS so that no lane waits on another's divergent work:
@@ -209,11 +242,13 @@ __device__ __forceinline__ uint32_t dict_resolve(const DevTable& tab, uint64_t h
 __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint8_t* __restrict__ blob,
                                                         const uint32_t* __restrict__ off, uint32_t n,
                                                         uint32_t* __restrict__ wid, uint32_t* __restrict__ lv,
-                                                        uint8_t* __restrict__ tfl) {
+                                                        uint8_t* __restrict__ tfl, WalkOrderOut wo) {
   __shared__ __attribute__((aligned(16))) uint32_t sw[TOK_LDS / 4 + 1];   // +1: lds_word reads one word past
   __shared__ uint32_t wpos[TOK_WORDS];   // start | len << 16 (LDS byte index)
   __shared__ uint32_t wdst[TOK_WORDS];   // index into wid[]
   __shared__ uint8_t wtop[TOK_WORDS];    // topic within the segment
+  __shared__ uint32_t tg[TOK_BLOCK];     // wid index of the topic's word 0 (a word's level = wdst - tg)
+  __shared__ uint32_t kw[TOK_BLOCK][KEY_LEVELS];   // the topic's first word ids (walk-order key)
   __shared__ uint32_t tflag[TOK_BLOCK];
   __shared__ uint32_t wsum[TOK_BLOCK / 64];
   const uint32_t blk0 = blockIdx.x * TOK_BLOCK;
@@ -240,6 +275,10 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         tokenise_one(tab, (const uint32_t*)(blob + (ts & ~3u)), ts & 3u, len, ts + t0, wid, &l, &fl);
         lv[t0] = l;
         tfl[t0] = fl;
+        if (wo.key) {
+          wo.key[t0] = 0xFFFFFFFFu;
+          wo.val[t0] = sort_val(t0, l, fl, false);
+        }
       }
       t0 = t1;
       continue;
@@ -286,6 +325,10 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         tokenise_one(tab, sw, ts, len, off[t] + t, wid, &l, &f);
         lv[t] = l;
         tfl[t] = f;
+        if (wo.key) {
+          wo.key[t] = 0xFFFFFFFFu;
+          wo.val[t] = sort_val(t, l, f, false);
+        }
       }
       __syncthreads();
       t0 = t1;
@@ -313,8 +356,11 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
       wpos[ex + l] = ws | ((ts + len - ws) << 16);
       wdst[ex + l] = g + l;
       wtop[ex + l] = (uint8_t)tid;
+      tg[tid] = g;
       lv[t] = D;
     }
+#pragma unroll
+    for (uint32_t k = 0; k < KEY_LEVELS; ++k) kw[tid][k] = 0;
     __syncthreads();
 
     // ---- pass 3: hash + dictionary probe, lane per word ----
@@ -354,10 +400,24 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         if (spec[u]) atomicOr(&tflag[wtop[i]], (uint32_t)TF_WILDCARD);
         else res[u] = dict_resolve(tab, h[u], a[u], b[u], sw, st[u], wl[u]);
         wid[wdst[i]] = res[u];
+        if (wo.key) {
+          const uint32_t tt = wtop[i], l = wdst[i] - tg[tt];
+          if (l < KEY_LEVELS) kw[tt][l] = res[u];
+          if (l < FIX_WORDS) wo.wfix[(uint64_t)(t0 + tt) * FIX_WORDS + l] = res[u];
+        }
       }
     }
     __syncthreads();
-    if (t < t1) tfl[t] = (uint8_t)tflag[tid];
+    if (t < t1) {
+      tfl[t] = (uint8_t)tflag[tid];
+      if (wo.key) {
+        uint32_t w4[KEY_LEVELS];
+#pragma unroll
+        for (uint32_t k = 0; k < KEY_LEVELS; ++k) w4[k] = kw[tid][k];
+        wo.key[t] = walk_key(w4, D, wo.shape);
+        wo.val[t] = sort_val(t, D, tflag[tid], D <= FIX_WORDS);
+      }
+    }
     __syncthreads();   // tflag, wpos and sw are rewritten by the next segment
     t0 = t1;
   }
@@ -427,8 +487,8 @@ struct alignas(16) WaveLds {
   uint16_t stage_rank[WALK_STAGE];
   uint8_t stage_t[WALK_STAGE];       // topic in chunk of the emit
   uint32_t words[WALK_WORDS];        // the sub-chunk's word ids, [topic][level]
-  uint32_t tinfo[WALK_CHUNK];        // D | tflags << 24
-  uint32_t tbase[WALK_CHUNK];        // LDS index of the topic's word 0
+  uint32_t tinfo[WALK_CHUNK];        // D | tflags << 24 | words at the fixed stride << 31
+  uint32_t gbase[WALK_CHUNK];        // the topic's word 0: wid[] index (off[t] + t), or its topic (fixed stride)
   uint32_t cnt[WALK_CHUNK];          // ids per topic, whole chunk
   uint32_t fcnt[WALK_CHUNK];         // ids per topic in the current stage / start inside the flush
 };
@@ -475,7 +535,7 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
 // the wave's ids slab grouped by topic: one piece {topic, count, ids_tmp
 // offset, offset inside the topic's CSR row} per topic present, so the
 // compaction needs no atomics.
-__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t lane,
+__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t my_t, uint32_t lane,
                                             const MatchWork& w, Slab& sid, Slab& spc) {
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {
@@ -504,7 +564,7 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
   const unsigned long long pbase = slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
   const bool ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
   if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
-  if (fl && ok) w.pieces[pbase + pex] = make_uint4(t0 + lane, fl, (uint32_t)(base + ex), L.cnt[lane]);
+  if (fl && ok) w.pieces[pbase + pex] = make_uint4(my_t, fl, (uint32_t)(base + ex), L.cnt[lane]);
   L.fcnt[lane] = ex;   // the topic's start inside this flush
   L.cnt[lane] += fl;
   wave_sync();
@@ -639,11 +699,10 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend
 // 129-134): the topic's words walked as a literal key, '+'/'#' words taking
 // the '+'/'#' edges.  Rare (MQTT publishes never carry wildcards): one lane,
 // one dependent read per level.
-__device__ bool exact_walk(const DevTable& tab, const uint32_t* __restrict__ wid, uint32_t tbase, uint32_t D,
-                           uint32_t* fid) {
+__device__ bool exact_walk(const DevTable& tab, const uint32_t* __restrict__ words, uint32_t D, uint32_t* fid) {
   uint32_t node = 0;
   for (uint32_t l = 0; l < D; ++l) {
-    const uint32_t wd = wid[tbase + l];
+    const uint32_t wd = words[l];
     uint32_t child = NONE;
     if (wd == WID_PLUS) child = tab.nodes[node].plus_child;
     else if (wd == WID_HASH) child = tab.hash_child[node];
@@ -666,6 +725,11 @@ __device__ __forceinline__ uint32_t root_flags(uint4 root, bool dollar, uint32_t
   return (dollar ? 0u : (root.w & F_PLUS)) | ((root.w & s0) ? (root.w & F_LIT) : 0u);
 }
 
+// A topic's word ids: at the fixed stride of the sorted batch, or in wid[].
+__device__ __forceinline__ const uint32_t* topic_words(const MatchWork& w, uint32_t tinfo, uint32_t gbase) {
+  return (tinfo >> 31) ? w.wfix + (uint64_t)gbase * FIX_WORDS : w.wid + gbase;
+}
+
 // One wave walks one chunk of 64 topics at a time (a grid stride over the
 // chunks).  The chunk's words are staged in LDS ([topic][level]; deep topics
 // in sub-chunks of S topics with S * dmax <= WALK_WORDS), topics are admitted
@@ -684,16 +748,32 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
   uint32_t created = 0;
   unsigned long long iters = 0, popped = 0, bounded = 0, lit_probes = 0, plus_reads = 0;
   Slab sid{0, 0}, spc{0, 0};
+  // sorted batch: the record of the chunk's j-th topic in walk order, loaded
+  // one chunk ahead (a grid stride: the wave's next chunk is c + gridDim.x)
+  const uint64_t* ord = w.order;
+  uint64_t rec = ord ? ord[min(blockIdx.x * WALK_CHUNK + lane, n - 1)] : 0ull;
   for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const uint32_t t0 = c * WALK_CHUNK;
     const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
-    // ---- topic info (lane j: topic t0 + j) ----
-    uint32_t D = 0, f = 0;
-    if (lane < nt) {
-      D = w.lv[t0 + lane];
-      f = w.tfl[t0 + lane];
+    // ---- topic info (lane j: the chunk's j-th topic in walk order) ----
+    uint32_t D = 0, f = 0, my_t = 0;
+    bool fixed = false;
+    if (ord) {
+      const uint64_t r = rec;
+      rec = ord[min((c + gridDim.x) * WALK_CHUNK + lane, n - 1)];   // the next chunk's, in flight during this one
+      if (lane < nt) {
+        my_t = (uint32_t)r;
+        D = (uint32_t)(r >> 32) & 0xFFFFFFu;
+        f = (uint32_t)(r >> 56) & 0x7Fu;
+        fixed = (r >> 63) != 0;
+      }
+    } else if (lane < nt) {
+      my_t = t0 + lane;
+      D = w.lv[my_t];
+      f = w.tfl[my_t];
     }
-    L.tinfo[lane] = D | (f << 24);
+    if (lane < nt) L.gbase[lane] = fixed ? my_t : off[my_t] + my_t;   // only words at a variable offset need off[]
+    L.tinfo[lane] = D | (f << 24) | (fixed ? 0x80000000u : 0u);
     L.cnt[lane] = 0;
     L.fcnt[lane] = 0;
     uint32_t dmax = D;
@@ -710,14 +790,17 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
     uint32_t S = WALK_CHUNK;
     while (S > 1 && S * dmax > WALK_WORDS) S >>= 1;
     uint32_t nstage = 0;
+    if (w.chunk_slabs) {   // the chunk's pieces start a slab of their own (the abandoned tail is marked empty)
+      for (unsigned long long i = spc.cur + lane; i < spc.end && i < w.pieces_cap; i += 64) w.pieces[i] = empty_piece();
+      spc.end = spc.cur;
+    }
     wave_sync();
     for (uint32_t sub = 0; sub < nt; sub += S) {
       const uint32_t end = min(sub + S, nt);
-      if (lane < end - sub) {   // stage the sub-chunk's words
+      if (lane < end - sub) {   // stage the sub-chunk's words: topic j's word 0 at LDS (j % S) * dmax
         const uint32_t j = sub + lane, Dj = L.tinfo[j] & 0xFFFFFFu;
-        const uint32_t* src = w.wid + off[t0 + j] + t0 + j;
+        const uint32_t* src = topic_words(w, L.tinfo[j], L.gbase[j]);
         uint32_t* dst = L.words + lane * dmax;
-        L.tbase[j] = lane * dmax;
         uint32_t i = 0;
         for (; i + 4 <= Dj; i += 4) {
           const uint32_t a0 = src[i], a1 = src[i + 1], a2 = src[i + 2], a3 = src[i + 3];
@@ -742,7 +825,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         if (sp < 64u && next < end) {
           const uint32_t k = min(64u - sp, end - next);
           if (nstage + 64u > WALK_STAGE) {
-            flush_stage(L, nstage, t0, lane, w, sid, spc);
+            flush_stage(L, nstage, my_t, lane, w, sid, spc);
             nstage = 0;
           }
           bool has = false, em = false;
@@ -750,15 +833,15 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
           uint4 it = make_uint4(0, 0, 0, 0);
           const uint32_t j = next + lane;
           if (lane < k) {
-            const uint32_t ti = L.tinfo[j], Dj = ti & 0xFFFFFFu, tf = ti >> 24;
+            const uint32_t ti = L.tinfo[j], Dj = ti & 0xFFFFFFu, tf = (ti >> 24) & 0x7Fu;
             if (tf & TF_WILDCARD) {
-              if (mode == MODE_ROUTES) em = exact_walk(tab, w.wid, off[t0 + j] + t0 + j, Dj, &fid);
+              if (mode == MODE_ROUTES) em = exact_walk(tab, topic_words(w, ti, L.gbase[j]), Dj, &fid);
             } else {
               const bool dollar = (tf & TF_DOLLAR) != 0;
               em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
               fid = root.y;
               created += 1;
-              const uint32_t w0 = L.words[L.tbase[j]];
+              const uint32_t w0 = L.words[(j & (S - 1)) * dmax];
               const uint32_t rf = root_flags(root, dollar, w0);
               has = rf != 0;
               it = make_uint4(0, (j << MT_SHIFT) | (rf << MF_SHIFT), root.x, w0);
@@ -801,8 +884,8 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         const uint32_t tt = (p.it.y >> MT_SHIFT) & 0x7Fu;
         const uint32_t ti = L.tinfo[tt];
         p.D = ti & 0xFFFFFFu;
-        p.d1 = p.D == 1 && ((ti >> 24) & TF_DOLLAR);
-        issue(tab, L.words + L.tbase[tt], nullptr, 0, p);
+        p.d1 = p.D == 1 && ((ti >> 24) & TF_DOLLAR);   // TF_DOLLAR < 0x80: the fixed-stride bit is not read
+        issue(tab, L.words + (tt & (S - 1)) * dmax, nullptr, 0, p);
         lit_probes += popc(__ballot(p.lit));
         plus_reads += popc(__ballot(p.plus));
         wave_sync();
@@ -823,7 +906,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
         if (nstage + ne > WALK_STAGE) {
           wave_sync();
-          flush_stage(L, nstage, t0, lane, w, sid, spc);
+          flush_stage(L, nstage, my_t, lane, w, sid, spc);
           nstage = 0;
         }
         const uint8_t st = (uint8_t)tt;
@@ -851,8 +934,8 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         wave_sync();
       }
     }
-    if (nstage) flush_stage(L, nstage, t0, lane, w, sid, spc);
-    if (lane < nt) w.cnt[t0 + lane] = L.cnt[lane];
+    if (nstage) flush_stage(L, nstage, my_t, lane, w, sid, spc);
+    if (lane < nt) w.cnt[my_t] = L.cnt[lane];
     wave_sync();
   }
   for (unsigned long long i = spc.cur + lane; i < spc.end && i < w.pieces_cap; i += 64)
@@ -908,12 +991,13 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
     if (lane == 0) idx = atomicAdd(&w.stats->heavy_next, 1u);
     idx = uni(__shfl(idx, 0, 64));
     if (idx >= total) break;
-    const uint32_t t = w.deferred[idx / WALK_CHUNK] * WALK_CHUNK + idx % WALK_CHUNK;
-    if (t >= n) continue;
+    const uint32_t pos = w.deferred[idx / WALK_CHUNK] * WALK_CHUNK + idx % WALK_CHUNK;   // in walk order
+    if (pos >= n) continue;
+    const uint32_t t = uni(w.order ? (uint32_t)w.order[pos] : pos);
     const uint32_t D = uni(w.lv[t]), tf = uni(w.tfl[t]), tb = uni(off[t] + t);
     if (tf & TF_WILDCARD) {   // no trie walk: TRIE mode matches nothing, ROUTES mode one exact lookup
       uint32_t fid = NONE;
-      const bool em = mode == MODE_ROUTES && exact_walk(tab, w.wid, tb, D, &fid);
+      const bool em = mode == MODE_ROUTES && exact_walk(tab, w.wid + tb, D, &fid);
       if (lane == 0) {
         if (em) {
           const unsigned long long base = atomicAdd(&w.stats->cursor, 1ull);
@@ -1120,7 +1204,8 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
                                                                 const uint32_t* __restrict__ ids_tmp, uint32_t n,
                                                                 const uint64_t* __restrict__ row_ptr,
                                                                 uint32_t* __restrict__ ids, uint64_t ids_cap,
-                                                                uint64_t pieces_cap, MatchStats* stats) {
+                                                                uint64_t pieces_cap, uint32_t slab_windows,
+                                                                MatchStats* stats) {
   __shared__ uint32_t s_scan[COMPACT_WAVES][64];
   __shared__ uint32_t s_src[COMPACT_WAVES][64];
   __shared__ uint64_t s_dst[COMPACT_WAVES][64];
@@ -1135,9 +1220,14 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
   const uint64_t np = min((uint64_t)stats->pieces, pieces_cap);
   if (np == 0) return;
   const uint64_t nwin = (np + 63) / 64, nw = (uint64_t)gridDim.x * COMPACT_WAVES;
-  const uint64_t per = (nwin + nw - 1) / nw, me = (uint64_t)blockIdx.x * COMPACT_WAVES + wave;
-  const uint64_t wend = min(nwin, (me + 1) * per) * 64;
-  uint64_t w0 = me * per * 64;
+  const uint64_t me = (uint64_t)blockIdx.x * COMPACT_WAVES + wave;
+  // a contiguous range of windows per wave; with per-chunk slabs, whole
+  // slabs (one chunk's pieces each) per wave, a grid stride over them
+  const uint64_t per = slab_windows ? slab_windows : (nwin + nw - 1) / nw;
+  const uint64_t stride = nw * per * 64;   // without slabs one range per wave covers every window
+  for (uint64_t r0 = me * per * 64; r0 < np; r0 += stride) {
+  const uint64_t wend = min(nwin * 64, r0 + per * 64);
+  uint64_t w0 = r0;
   uint4 pc = pieces[min(w0 + lane, np - 1)];   // unconditional (a load under a branch is waited for at once)
   for (; w0 < wend; w0 += 64) {
     const uint64_t i = w0 + lane;
@@ -1169,6 +1259,7 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
         if (q0 + 64u * r < tot) ids[d[r]] = v[r];   // plain stores: nontemporal ones measured 2x slower here
     }
     wave_sync();
+  }
   }
 }
 
@@ -1211,17 +1302,51 @@ static void trace(hipStream_t s, const char* what) {
   fprintf(stderr, " %s\n", hipGetErrorString(e));
 }
 
+uint32_t walk_key_bits(uint32_t shape) {
+  uint32_t b = 0;
+  for (uint32_t l = 0; l < KEY_LEVELS; ++l) b += (shape >> (4 * l)) & 0xFu;
+  return b;
+}
+
+size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape) {
+  size_t b = 0;
+  const int bits = (int)min(walk_key_bits(shape), 32u);
+  hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                     (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)n, 32 - bits, 32);
+  return b;
+}
+
+constexpr uint32_t SORT_MIN_TOPICS = 16384;   // below this the sort's fixed cost outweighs the locality
+
 hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n,
-                        int mode, const MatchWork& w, const MatchOut& out, hipStream_t s,
+                        int mode, const MatchWork& w_in, const MatchOut& out, hipStream_t s,
                         hipEvent_t* ev_walk) {
-  hipError_t e = hipMemsetAsync(w.stats, 0, sizeof(MatchStats), s);
+  hipError_t e = hipMemsetAsync(w_in.stats, 0, sizeof(MatchStats), s);
   if (e != hipSuccess) return e;
   if (n == 0) {
     return hipMemsetAsync(out.row_ptr, 0, sizeof(uint64_t), s);
   }
+  MatchWork w = w_in;
+  const uint32_t kbits = min(walk_key_bits(w.key_shape), 32u);
+  const bool sorted = kbits && w.order && n >= SORT_MIN_TOPICS && !(w.debug & DEBUG_INPUT_ORDER);
+  size_t tb = 0;
+  if (sorted) {
+    tb = walk_sort_temp_bytes(n, w.key_shape);
+    if (tb > w.sort_tmp_bytes) return hipErrorInvalidValue;   // a host sizing bug: never sort into too little scratch
+  }
+  WalkOrderOut wo{};
+  if (sorted) wo = WalkOrderOut{w.skey, w.sval, w.wfix, w.key_shape};
   hipLaunchKernelGGL(k_tokenise, dim3((n + TOK_BLOCK - 1) / TOK_BLOCK), dim3(TOK_BLOCK), 0, s, tab, blob,
-                     off, n, w.wid, w.lv, w.tfl);
+                     off, n, w.wid, w.lv, w.tfl, wo);
   trace(s, "k_tokenise");
+  if (sorted) {
+    e = hipcub::DeviceRadixSort::SortPairs(w.sort_tmp, tb, w.skey, w.skey_out, w.sval, w.order, (int)n,
+                                           32 - (int)kbits, 32, s);
+    if (e != hipSuccess) return e;
+    trace(s, "walk order sort");
+  } else {
+    w.order = nullptr;
+  }
   if (ev_walk) hipEventRecord(ev_walk[0], s);
   hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64), 0, s, tab, off, n, mode, w);
   if (ev_walk) hipEventRecord(ev_walk[1], s);
@@ -1235,7 +1360,7 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   const uint32_t cblocks =
       (uint32_t)std::min<uint64_t>(EGM_COMPACT_BLOCKS, std::max<uint64_t>(256, ((uint64_t)n + 63) / 64));
   hipLaunchKernelGGL(k_compact, dim3(cblocks), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.ids_tmp, n, out.row_ptr,
-                     out.ids, out.ids_cap, w.pieces_cap, w.stats);
+                     out.ids, out.ids_cap, w.pieces_cap, w.chunk_slabs ? SLAB_PIECES / 64 : 0u, w.stats);
   return hipGetLastError();
 }
 
@@ -1670,9 +1795,10 @@ __global__ __launch_bounds__(256) void k_rs_expand(RetainView v, RetainWork w, u
 
 hipError_t launch_tokenise(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n, uint32_t* wid,
                            uint32_t* lv, uint8_t* tfl, hipStream_t s) {
+  const WalkOrderOut none{};
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(k_tokenise, dim3((n + TOK_BLOCK - 1) / TOK_BLOCK), dim3(TOK_BLOCK), 0, s, tab, blob, off, n,
-                     wid, lv, tfl);
+                     wid, lv, tfl, none);
   return hipGetLastError();
 }
 

@@ -178,6 +178,7 @@ int egm_set_timing(egm_ctx* ctx, int enable);
    survive into the following commit). */
 #define EGM_DEBUG_FORCE_HEAVY 1u
 #define EGM_DEBUG_FAIL_COMMIT 2u
+#define EGM_DEBUG_INPUT_ORDER 4u   /* walk the batch in input order (no locality sort; A/B and tests) */
 int egm_set_debug(egm_ctx* ctx, uint32_t flags);
 int egm_get_timing(egm_ctx* ctx, double* walk_ms, uint64_t* walk_launches, double* fanout_ms,
                    uint64_t* fanout_launches);

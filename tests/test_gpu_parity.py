@@ -199,6 +199,34 @@ def test_config_c0_heavy_path_vs_cpp_oracle(gm, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+def test_walk_orders_vs_cpp_oracle(gm, mode, monkeypatch):
+    """The walk's locality order (the key k_tokenise computes, the radix sort,
+    the walk reading sorted topic records and fixed-stride words) never
+    changes a result: several key shapes, input order, a partial last chunk
+    and sorted + every chunk through k_heavy, all bit-exact against the C++
+    oracle (egm_kernels.hip launch_match)."""
+    f, t = synth.config("c0", n_topics=70_001)
+    gm.build(f.blob, f.off)
+    o = OracleTrie(True, mode)
+    o.add(f.blob, f.off)
+    row, ids = o.match(t.blob, t.off, threads=8)
+    want = canonical(row, ids)
+    for bits, debug in (("8888", 0), ("444", 0), ("68a6", 0), ("0", 0), ("8888", 4), ("8888", 1), ("8888/0", 0),
+                        ("0/0", 0)):
+        shape, _, slabs = bits.partition("/")
+        monkeypatch.setenv("EGM_WALK_KEY", shape)   # key bits per level (hex nibbles, level 0 lowest)
+        monkeypatch.setenv("EGM_CHUNK_SLABS", slabs or "1")   # each chunk's pieces in a slab of their own
+        gm.set_debug(debug)   # 4: EGM_DEBUG_INPUT_ORDER, 1: EGM_DEBUG_FORCE_HEAVY
+        try:
+            res = gm.match(t.blob, t.off, mode)
+        finally:
+            gm.set_debug(0)
+        assert res.n_error == 0
+        assert np.array_equal(res.row_ptr, row), (bits, debug)
+        assert np.array_equal(canonical(res.row_ptr, res.ids), want), (bits, debug)
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_config_c3_vs_cpp_oracle(gm, mode):
     """C3 shape at reduced size (depth-16 topics and filters,
     '+' p=.35, last-level '#' p=.7): deep chunks are walked as sub-chunks of

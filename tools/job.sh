@@ -15,6 +15,7 @@
 #   pmc        FETCH_SIZE and WRITE_SIZE passes over the C2 bench (one counter per pass)
 #   sq         SQ wait/active counters + TCC hit/miss over the C2 bench
 #   host       host-visible path (egm_match_batch, pinned staging) bench
+#   orders     the C2 bench, then the walk-order A/B (sort key shapes) in the same process
 #   smoke      __graft_entry__.smoke()
 #   ab_V       the C2 bench on variant V (emqx_amd/libemqx_gpu_match_V.so, tools/build_variant.py)
 # An ordinary failure (exit 1..5) moves on; a fault, abort or timeout ends the job.
@@ -63,6 +64,7 @@ for step in "$@"; do
       run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU -d "$R/gpurun_out/${TAG}_pmc_sq" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off
       run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off ;;
     host) run host 600 python tools/bench_host.py ;;
+    orders) run orders 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "8888/1,8888/0,0/1,0/0,a86/1,8664/1,4444/1,8888/1" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     ab_*)   # A/B variant built by tools/build_variant.py: C2 bench under rocprof stats
       v=${step#ab_}
