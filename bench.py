@@ -214,9 +214,12 @@ def main():
                          "would save the walk")
     ap.add_argument("--x-orders", default="",
                     help="experiment: after the timed steps, time the same steps under each walk order "
-                         "'shape/slabs,...' (EGM_WALK_KEY: key bits per level as hex nibbles, level 0 lowest, 0 = "
-                         "input order; EGM_CHUNK_SLABS 0/1) and check "
+                         "'shape[/window],...' (EGM_WALK_KEY: key bits per level as hex nibbles, level 0 lowest, 0 = "
+                         "input order; EGM_WALK_WINDOW: log2 of the sort window, 0 = whole batch) and check "
                          "that every order gives the same rows (stderr)")
+    ap.add_argument("--pipelined", default="on", choices=["on", "off"],
+                    help="after the timed steps, time them again with consecutive batches over two streams "
+                         "(replicate mode, no fan-out; reported as the line's `pipelined`)")
     ap.add_argument("--host-e2e", default="on", choices=["on", "off"],
                     help="also time the host-visible path (pinned staging, H2D, match, D2H) at N=1")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
@@ -295,7 +298,10 @@ def main():
     # one explicit stream for every kernel and copy of the step (the library
     # and torch share one HIP runtime: emqx_amd._lib loads torch first)
     nstreams = 1 if shard else max(1, args.streams)
-    streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+    # the pipelined leg (after the timed steps): consecutive batches over two streams
+    piped = args.pipelined == "on" and not shard and not fanout and nstreams == 1
+    nbuf = 2 if piped else nstreams
+    streams = [torch.cuda.Stream(dev) for _ in range(nbuf)]
     stream = streams[0]
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
@@ -304,9 +310,9 @@ def main():
     d_blob = torch.from_numpy(t.blob).to(dev)
     d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
     torch.cuda.synchronize(dev)
-    bufs = {"cap": max(4 * n, 1 << 20), "k": 0}
-    bufs["rows"] = [torch.zeros(n + 1, dtype=torch.int64, device=dev) for _ in range(nstreams)]
-    bufs["idss"] = [torch.zeros(bufs["cap"], dtype=torch.int32, device=dev) for _ in range(nstreams)]
+    bufs = {"cap": max(4 * n, 1 << 20), "k": 0, "ns": nstreams}
+    bufs["rows"] = [torch.zeros(n + 1, dtype=torch.int64, device=dev) for _ in range(nbuf)]
+    bufs["idss"] = [torch.zeros(bufs["cap"], dtype=torch.int32, device=dev) for _ in range(nbuf)]
     bufs["row"], bufs["ids"] = bufs["rows"][0], bufs["idss"][0]
 
     fcap = max(8 * n, 1 << 20) if fanout else 0
@@ -316,8 +322,8 @@ def main():
     fan_on = False   # enabled once the id buffer holds a whole match batch
 
     def run_local():
-        # batch k on stream k mod nstreams, with that stream's output buffers
-        i = bufs["k"] % nstreams
+        # batch k on stream k mod ns, with that stream's output buffers
+        i = bufs["k"] % bufs["ns"]
         bufs["k"] += 1
         s_i = streams[i].cuda_stream
         row, ids = bufs["rows"][i], bufs["idss"][i]
@@ -377,7 +383,7 @@ def main():
         if not st["overflow"]:
             break
         bufs["cap"] = int(st["n_ids"] * 1.25) + 1024
-        bufs["idss"] = [torch.zeros(bufs["cap"], dtype=torch.int32, device=dev) for _ in range(nstreams)]
+        bufs["idss"] = [torch.zeros(bufs["cap"], dtype=torch.int32, device=dev) for _ in range(nbuf)]
         bufs["ids"] = bufs["idss"][0]
         bufs["k"] = 0
         log(f"[rank {rank}] grew id buffers to {bufs['cap']}")
@@ -434,6 +440,33 @@ def main():
         ti = gm.get_timing()
         iso_ms = ti["walk_ms"] / max(1, ti["walk_launches"])
         gm.set_timing(False)
+    pipelined = None
+    if piped:
+        # the same steps with consecutive batches alternating over two streams,
+        # so one batch's bandwidth-bound kernels (sort, scan, compaction) run
+        # beside the next one's latency-bound walk; reported beside `value`
+        bufs["ns"], bufs["k"] = 2, 0
+        for _ in range(2):
+            run_local()
+        if have_pg:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run_local()
+        torch.cuda.synchronize(dev)
+        pe = time.perf_counter() - t0
+        if have_pg:
+            dist.barrier()
+            e = torch.tensor([pe], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            pe = float(e.item())
+        st2 = gm.last_stats()
+        assert st2["overflow"] == 0 and st2["errors"] == 0, st2
+        pipelined = {"streams": 2, "value": n * world * args.steps / pe, "ms_per_step": pe / args.steps * 1e3,
+                     "note": "same steps, consecutive batches alternating over two HIP streams (separate "
+                             "workspaces and output buffers)"}
+        bufs["ns"], bufs["k"] = nstreams, 0
     merged_ids = sum(exchange.last_totals) if exchange is not None else None
     if args.x_orders and exchange is None:
         order_experiment(args, gm, run_local, bufs, dev, n)
@@ -494,6 +527,7 @@ def main():
                         "deliveries_per_s": deliveries * world * args.steps / elapsed,
                         "bytes_per_launch": 12 * deliveries + 20 * n_ids + 8 * (n + 1)}
                        if fanout else None),
+            "pipelined": pipelined,
             "host_e2e": host,
             "cpu_baseline": cpu,
         }
@@ -516,28 +550,31 @@ def order_experiment(args, gm, run_local, bufs, dev, n):
         cs = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), cs])
         return row.clone(), cs[row]
 
-    saved = {k: os.environ.get(k) for k in ("EGM_WALK_KEY", "EGM_CHUNK_SLABS")}
+    saved = {k: os.environ.get(k) for k in ("EGM_WALK_KEY", "EGM_WALK_WINDOW")}
     bufs["k"] = 0
     run_local()
     torch.cuda.synchronize(dev)
     ref_row, ref_sig = rows_sig()
     for spec in args.x_orders.split(","):
-        shape, _, slabs = spec.partition("/")
-        os.environ["EGM_WALK_KEY"], os.environ["EGM_CHUNK_SLABS"] = shape, slabs or "1"
+        shape, _, win = spec.partition("/")
+        os.environ["EGM_WALK_KEY"], os.environ["EGM_WALK_WINDOW"] = shape, win or "0"
         for _ in range(2):
             bufs["k"] = 0
             run_local()
         torch.cuda.synchronize(dev)
         gm.set_timing(True)
+        bufs["k"] = 0
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            bufs["k"] = 0
-            run_local()
+            run_local()   # consecutive batches alternate over the bench's streams
         torch.cuda.synchronize(dev)
         dt = (time.perf_counter() - t0) / args.steps
         tim = gm.get_timing()
         gm.set_timing(False)
         wc = gm.walk_counters()
+        bufs["k"] = 0
+        run_local()
+        torch.cuda.synchronize(dev)
         row, sig = rows_sig()
         same = bool(torch.equal(row, ref_row) and torch.equal(sig, ref_sig))
         log(json.dumps({"order": spec, "ms_per_step": dt * 1e3,

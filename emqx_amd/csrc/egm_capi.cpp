@@ -107,7 +107,7 @@ constexpr size_t PIPE_MAX_SLOTS = 8;
 // One match workspace: the per-batch scratch of launch_match.
 struct MatchWs {
   DevBuf wid, lv, tfl, cnt, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats;
-  DevBuf skey, skey_out, sval, order, wfix, sort_tmp;   // walk-order sort (egm_kernels.hip walk_key)
+  DevBuf skey, skey_out, sval, order, wfix, inv, row_at, sort_tmp;   // walk-order sort (egm_kernels.hip walk_key)
   uint64_t pieces_cap = 0, ids_tmp_cap = 0;
   uint32_t heavy_cap = 0;        // stack items per heavy wave
   hipEvent_t ev = nullptr;       // recorded after its last batch
@@ -512,8 +512,15 @@ static int commit_locked(egm_ctx* c, uint64_t* epoch) {
 // knob for A/B runs (read at every batch); the default is the measured best.
 static uint32_t walk_key_shape() {
   const char* v = getenv("EGM_WALK_KEY");
-  const uint32_t shape = (v && *v) ? (uint32_t)strtoul(v, nullptr, 16) & 0xFFFFu : 0x8888u;   // KEY_LEVELS nibbles
-  return walk_key_bits(shape) <= 32 ? shape : 0x8888u;
+  const uint32_t shape = (v && *v) ? (uint32_t)strtoul(v, nullptr, 16) & 0xFFFFu : 0xa86u;   // KEY_LEVELS nibbles
+  return walk_key_bits(shape) <= 32 ? shape : 0xa86u;
+}
+
+// EGM_WALK_WINDOW: sort within windows of 2^k consecutive topics (0: the whole batch).
+static uint32_t walk_window_shift() {
+  const char* v = getenv("EGM_WALK_WINDOW");
+  const uint32_t k = (v && *v) ? (uint32_t)atoi(v) : 0u;
+  return k < 32 ? k : 0u;
 }
 
 // The workspace for a batch on stream s: the one that last ran on s (stream
@@ -566,7 +573,10 @@ static int ensure_work(egm_ctx* c, MatchWs& W, uint32_t n, uint64_t blob_bytes, 
     if ((e = W.sval.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "sort values");
     if ((e = W.order.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "walk order");
     if ((e = W.wfix.ensure(nn * 4 * FIX_WORDS)) != hipSuccess) return c->hip_fail(e, "fixed-stride words");
-    if ((e = W.sort_tmp.ensure(walk_sort_temp_bytes(n, shape))) != hipSuccess) return c->hip_fail(e, "sort scratch");
+    if ((e = W.row_at.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "walk-order rows");
+    if ((e = W.inv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "walk positions");
+    if ((e = W.sort_tmp.ensure(walk_sort_temp_bytes(n, shape, walk_window_shift()))) != hipSuccess)
+      return c->hip_fail(e, "sort scratch");
   }
   if (!W.ev && (e = hipEventCreateWithFlags(&W.ev, hipEventDisableTiming)) != hipSuccess)
     return c->hip_fail(e, "workspace event");
@@ -597,15 +607,15 @@ static MatchWork work_view(egm_ctx* c, MatchWs& W) {
     w.sval = W.sval.as<uint64_t>();
     w.order = W.order.as<uint64_t>();
     w.wfix = W.wfix.as<uint32_t>();
+    w.row_at = W.row_at.as<uint64_t>();
+    w.inv = W.inv.as<uint32_t>();
     w.sort_tmp = W.sort_tmp.p;
     w.sort_tmp_bytes = W.sort_tmp.cap;
+    w.window_shift = walk_window_shift();
   } else {
     w.key_shape = 0;
   }
-  {
-    const char* v = getenv("EGM_CHUNK_SLABS");   // A/B knob
-    w.chunk_slabs = (v && *v) ? (uint32_t)atoi(v) : 1u;
-  }
+
   return w;
 }
 

@@ -37,13 +37,13 @@ struct MatchStats {               // device-side counters, zeroed per batch
 };
 
 // A piece is one flush's run of a topic's ids in ids_tmp:
-// {topic, count, ids_tmp offset, offset inside the topic's CSR row}, so the
+// {topic's walk position, count, ids_tmp offset, offset inside the topic's CSR row}, so the
 // compaction places every run without atomics (count 0: an unused slot).
 // Each wave reserves its output space in slabs (one device-scope atomic per
 // slab): a single shared counter bumped per flush serialises across the 8
 // XCDs at the memory side.
 constexpr uint32_t SLAB_IDS = 4096;
-constexpr uint32_t SLAB_PIECES = 512;
+constexpr uint32_t SLAB_PIECES = 256;
 
 struct MatchWork {                // per-batch device workspace
   uint32_t* wid;                  // [blob_bytes + n] word ids, topic t at off[t] + t
@@ -73,7 +73,9 @@ struct MatchWork {                // per-batch device workspace
   void* sort_tmp;                 // radix sort scratch
   size_t sort_tmp_bytes;
   uint32_t key_shape;             // key bits per level, nibble l = level l (0: walk in input order)
-  uint32_t chunk_slabs;           // each chunk's pieces start a pieces slab (k_compact: a slab per wave)
+  uint32_t window_shift;          // sort within windows of 2^window_shift consecutive topics (0: the whole batch)
+  uint32_t* inv;                  // [n] walk position of topic t (written by the walk; sorted batches)
+  uint64_t* row_at;               // [n] row starts by walk position (the scan; k_compact reads them)
 };
 
 constexpr uint32_t KEY_LEVELS = 4;           // levels hashed into the walk-order key
@@ -83,6 +85,7 @@ struct WalkOrderOut {                        // what k_tokenise writes for the s
   uint64_t* val;
   uint32_t* wfix;
   uint32_t shape;
+  uint32_t wshift, wbits;                    // sorted within windows of 2^wshift topics (wbits: window index bits)
 };
 
 constexpr uint32_t DEBUG_FORCE_HEAVY = 1u;   // every chunk goes to k_heavy (test coverage)
@@ -91,7 +94,8 @@ constexpr uint32_t DEBUG_INPUT_ORDER = 4u;   // walk in input order (no locality
 // walk-order key: total bits of a key shape; radix sort scratch bytes for a
 // batch of n topics (hipcub)
 uint32_t walk_key_bits(uint32_t shape);
-size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape);
+uint32_t walk_window_bits(uint32_t n, uint32_t wshift);
+size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape, uint32_t wshift);
 
 struct MatchOut {                 // CSR result (device)
   uint64_t* row_ptr;              // [n + 1]
@@ -115,8 +119,7 @@ inline uint64_t ids_tmp_capacity(uint64_t ids, uint32_t n) {
 inline uint64_t pieces_capacity(uint64_t ids, uint32_t n) {
   uint64_t p = 2ull * n + 4096;
   if (ids / 2 > p) p = ids / 2;
-  // + a slab per wave and per chunk (each chunk's pieces start a slab)
-  return p + (uint64_t)(walk_grid_blocks(n) + 256 + (n + WALK_CHUNK - 1) / WALK_CHUNK) * SLAB_PIECES;
+  return p + (uint64_t)(walk_grid_blocks(n) + 256) * SLAB_PIECES;
 }
 
 // Timing hooks: when ev != nullptr, ev[0]/ev[1] bracket the walk kernel.

@@ -222,6 +222,14 @@ __device__ __forceinline__ uint32_t walk_key(const uint32_t* w4, uint32_t D, uin
   return used < 32 ? k << (32 - used) : k;
 }
 
+// Sorted within windows of 2^wshift consecutive topics: the window index in
+// the key's top wbits bits, the prefix key below it.  A window's rows span a
+// bounded region of the output, so the scattered writes of a sorted batch
+// stay within what the caches can merge.
+__device__ __forceinline__ uint32_t window_key(const WalkOrderOut& wo, uint32_t t, uint32_t k) {
+  return wo.wbits ? (((t >> wo.wshift) << (32 - wo.wbits)) | (k >> wo.wbits)) : k;
+}
+
 // the sort's value: topic | (levels | flags << 24 | words at the fixed stride << 31) << 32
 __device__ __forceinline__ uint64_t sort_val(uint32_t t, uint32_t D, uint32_t f, bool fixed) {
   return (uint64_t)t | ((uint64_t)(min(D, 0xFFFFFFu) | ((f & 0x7Fu) << 24) | (fixed ? 0x80000000u : 0u)) << 32);
@@ -276,7 +284,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         lv[t0] = l;
         tfl[t0] = fl;
         if (wo.key) {
-          wo.key[t0] = 0xFFFFFFFFu;
+          wo.key[t0] = window_key(wo, t0, 0xFFFFFFFFu);
           wo.val[t0] = sort_val(t0, l, fl, false);
         }
       }
@@ -326,7 +334,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         lv[t] = l;
         tfl[t] = f;
         if (wo.key) {
-          wo.key[t] = 0xFFFFFFFFu;
+          wo.key[t] = window_key(wo, t, 0xFFFFFFFFu);
           wo.val[t] = sort_val(t, l, f, false);
         }
       }
@@ -414,7 +422,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         uint32_t w4[KEY_LEVELS];
 #pragma unroll
         for (uint32_t k = 0; k < KEY_LEVELS; ++k) w4[k] = kw[tid][k];
-        wo.key[t] = walk_key(w4, D, wo.shape);
+        wo.key[t] = window_key(wo, t, walk_key(w4, D, wo.shape));
         wo.val[t] = sort_val(t, D, tflag[tid], D <= FIX_WORDS);
       }
     }
@@ -424,11 +432,9 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
 }
 
 // -------------------------------------------------------------- NFA walk ----
-// One wavefront walks two chunks of WALK_CHUNK topics at once (128 topic
-// slots): topics are admitted into the LDS work stack as it drains, and when
-// one chunk has been admitted and its last item retired, its counts are
-// written and the next chunk (taken from a global counter) fills its slots —
-// the stack never drains between chunks, so the lanes stay busy.
+// One wavefront walks one chunk of WALK_CHUNK topics at a time (a grid stride
+// over the chunks, in walk order when the batch is sorted): topics are
+// admitted into the LDS work stack 64 roots at a time as it drains.
 //
 // A work item is 16 B {node, meta, plus_child, word}:
 //   meta = level[0:17) | slot[17:24) | transitions to take[24:28) | took '+' << 28
@@ -535,7 +541,7 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
 // the wave's ids slab grouped by topic: one piece {topic, count, ids_tmp
 // offset, offset inside the topic's CSR row} per topic present, so the
 // compaction needs no atomics.
-__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t my_t, uint32_t lane,
+__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t pos, uint32_t lane,
                                             const MatchWork& w, Slab& sid, Slab& spc) {
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {
@@ -564,7 +570,7 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
   const unsigned long long pbase = slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
   const bool ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
   if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
-  if (fl && ok) w.pieces[pbase + pex] = make_uint4(my_t, fl, (uint32_t)(base + ex), L.cnt[lane]);
+  if (fl && ok) w.pieces[pbase + pex] = make_uint4(pos, fl, (uint32_t)(base + ex), L.cnt[lane]);
   L.fcnt[lane] = ex;   // the topic's start inside this flush
   L.cnt[lane] += fl;
   wave_sync();
@@ -760,7 +766,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
     bool fixed = false;
     if (ord) {
       const uint64_t r = rec;
-      rec = ord[min((c + gridDim.x) * WALK_CHUNK + lane, n - 1)];   // the next chunk's, in flight during this one
+      rec = ord[min((uint64_t)(c + gridDim.x) * WALK_CHUNK + lane, (uint64_t)n - 1)];   // the next chunk's, in flight now
       if (lane < nt) {
         my_t = (uint32_t)r;
         D = (uint32_t)(r >> 32) & 0xFFFFFFu;
@@ -790,10 +796,6 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
     uint32_t S = WALK_CHUNK;
     while (S > 1 && S * dmax > WALK_WORDS) S >>= 1;
     uint32_t nstage = 0;
-    if (w.chunk_slabs) {   // the chunk's pieces start a slab of their own (the abandoned tail is marked empty)
-      for (unsigned long long i = spc.cur + lane; i < spc.end && i < w.pieces_cap; i += 64) w.pieces[i] = empty_piece();
-      spc.end = spc.cur;
-    }
     wave_sync();
     for (uint32_t sub = 0; sub < nt; sub += S) {
       const uint32_t end = min(sub + S, nt);
@@ -825,7 +827,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         if (sp < 64u && next < end) {
           const uint32_t k = min(64u - sp, end - next);
           if (nstage + 64u > WALK_STAGE) {
-            flush_stage(L, nstage, my_t, lane, w, sid, spc);
+            flush_stage(L, nstage, t0 + lane, lane, w, sid, spc);
             nstage = 0;
           }
           bool has = false, em = false;
@@ -906,7 +908,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
         if (nstage + ne > WALK_STAGE) {
           wave_sync();
-          flush_stage(L, nstage, my_t, lane, w, sid, spc);
+          flush_stage(L, nstage, t0 + lane, lane, w, sid, spc);
           nstage = 0;
         }
         const uint8_t st = (uint8_t)tt;
@@ -934,8 +936,11 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         wave_sync();
       }
     }
-    if (nstage) flush_stage(L, nstage, my_t, lane, w, sid, spc);
-    if (lane < nt) w.cnt[my_t] = L.cnt[lane];
+    if (nstage) flush_stage(L, nstage, t0 + lane, lane, w, sid, spc);
+    if (lane < nt) {
+      w.cnt[my_t] = L.cnt[lane];
+      if (ord) w.inv[my_t] = t0 + lane;
+    }
     wave_sync();
   }
   for (unsigned long long i = spc.cur + lane; i < spc.end && i < w.pieces_cap; i += 64)
@@ -994,6 +999,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
     const uint32_t pos = w.deferred[idx / WALK_CHUNK] * WALK_CHUNK + idx % WALK_CHUNK;   // in walk order
     if (pos >= n) continue;
     const uint32_t t = uni(w.order ? (uint32_t)w.order[pos] : pos);
+    if (lane == 0 && w.order) w.inv[t] = pos;
     const uint32_t D = uni(w.lv[t]), tf = uni(w.tfl[t]), tb = uni(off[t] + t);
     if (tf & TF_WILDCARD) {   // no trie walk: TRIE mode matches nothing, ROUTES mode one exact lookup
       uint32_t fid = NONE;
@@ -1004,7 +1010,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
           const unsigned long long p = atomicAdd(&w.stats->pieces, 1ull);
           if (base < w.ids_cap && p < w.pieces_cap) {
             w.ids_tmp[base] = fid;
-            w.pieces[p] = make_uint4(t, 1, (uint32_t)base, 0);
+            w.pieces[p] = make_uint4(pos, 1, (uint32_t)base, 0);
           } else {
             atomicOr(&w.stats->overflow, 1u);
           }
@@ -1096,7 +1102,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
         if (lane == 0) {
           if (!fits) atomicOr(&w.stats->overflow, 1u);
           w.cnt[t] = count;
-          if (count && fits) w.pieces[pb] = make_uint4(t, count, (uint32_t)base, 0);
+          if (count && fits) w.pieces[pb] = make_uint4(pos, count, (uint32_t)base, 0);
           w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
         }
         if (!count || !fits) break;
@@ -1152,7 +1158,8 @@ __global__ __launch_bounds__(1024) void k_scan_top(uint64_t* __restrict__ tile_s
 
 __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__ cnt, uint32_t n,
                                                     const uint64_t* __restrict__ tile_sums, uint32_t ntiles,
-                                                    uint64_t* __restrict__ row_ptr, uint64_t* __restrict__ copy) {
+                                                    uint64_t* __restrict__ row_ptr, uint64_t* __restrict__ copy,
+                                                    const uint32_t* __restrict__ inv, uint64_t* __restrict__ row_at) {
   __shared__ uint64_t wsum[4];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t i0 = blockIdx.x * SCAN_TILE + threadIdx.x * 8;
@@ -1178,13 +1185,15 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
     if (i0 + k < n) {
       row_ptr[i0 + k] = pre;
       if (copy) copy[i0 + k] = pre;
+      if (inv) row_at[inv[i0 + k]] = pre;   // sorted batch: the row start by walk position (k_compact)
     }
     pre += v[k];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) row_ptr[n] = tile_sums[ntiles];
 }
 
-// Pieces -> CSR rows, no atomics.  One wave per window of 64 pieces: a wave
+// Pieces -> CSR rows, no atomics.  A piece names its topic by walk position
+// (row_at: the row starts in walk order).  One wave per window of 64 pieces: a wave
 // scan lays the window's ids out as one run [0, tot), and the lanes copy that
 // run with consecutive lanes on consecutive ids (a binary search over the
 // window's 64 scan values finds each id's piece).  The pieces of one flush
@@ -1204,8 +1213,8 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
                                                                 const uint32_t* __restrict__ ids_tmp, uint32_t n,
                                                                 const uint64_t* __restrict__ row_ptr,
                                                                 uint32_t* __restrict__ ids, uint64_t ids_cap,
-                                                                uint64_t pieces_cap, uint32_t slab_windows,
-                                                                MatchStats* stats) {
+                                                                const uint64_t* __restrict__ row_at,
+                                                                uint64_t pieces_cap, MatchStats* stats) {
   __shared__ uint32_t s_scan[COMPACT_WAVES][64];
   __shared__ uint32_t s_src[COMPACT_WAVES][64];
   __shared__ uint64_t s_dst[COMPACT_WAVES][64];
@@ -1220,19 +1229,14 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
   const uint64_t np = min((uint64_t)stats->pieces, pieces_cap);
   if (np == 0) return;
   const uint64_t nwin = (np + 63) / 64, nw = (uint64_t)gridDim.x * COMPACT_WAVES;
-  const uint64_t me = (uint64_t)blockIdx.x * COMPACT_WAVES + wave;
-  // a contiguous range of windows per wave; with per-chunk slabs, whole
-  // slabs (one chunk's pieces each) per wave, a grid stride over them
-  const uint64_t per = slab_windows ? slab_windows : (nwin + nw - 1) / nw;
-  const uint64_t stride = nw * per * 64;   // without slabs one range per wave covers every window
-  for (uint64_t r0 = me * per * 64; r0 < np; r0 += stride) {
-  const uint64_t wend = min(nwin * 64, r0 + per * 64);
-  uint64_t w0 = r0;
+  const uint64_t per = (nwin + nw - 1) / nw, me = (uint64_t)blockIdx.x * COMPACT_WAVES + wave;
+  const uint64_t wend = min(nwin, (me + 1) * per) * 64;
+  uint64_t w0 = me * per * 64;
   uint4 pc = pieces[min(w0 + lane, np - 1)];   // unconditional (a load under a branch is waited for at once)
   for (; w0 < wend; w0 += 64) {
     const uint64_t i = w0 + lane;
     const uint32_t c = i < np ? pc.y : 0u;
-    const uint64_t rp = row_ptr[c ? pc.x : 0u];
+    const uint64_t rp = row_at[c ? pc.x : 0u];   // the piece's topic by its walk position
     uint32_t tot;
     const uint32_t ex = wave_excl_scan(c, lane, &tot);
     s_scan[wave][lane] = ex;
@@ -1260,7 +1264,6 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
     }
     wave_sync();
   }
-  }
 }
 
 // ------------------------------------------------------------- launchers ----
@@ -1277,12 +1280,13 @@ uint32_t heavy_stack_items(uint64_t max_levels) { return (uint32_t)(max_levels +
 size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
 static void scan_counts(const uint32_t* cnt, uint32_t n, uint64_t* tile_sums, uint64_t* row_ptr,
-                        hipStream_t s, uint64_t* copy = nullptr) {
+                        hipStream_t s, uint64_t* copy = nullptr, const uint32_t* inv = nullptr,
+                        uint64_t* row_at = nullptr) {
   const uint32_t ntiles = (uint32_t)scan_tiles(n);
   if (ntiles) hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(256), 0, s, cnt, n, tile_sums);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, tile_sums, ntiles);
   hipLaunchKernelGGL(k_scan_apply, dim3(ntiles ? ntiles : 1), dim3(256), 0, s, cnt, n, tile_sums, ntiles, row_ptr,
-                     copy);
+                     copy, inv, row_at);
 }
 
 // EGM_TRACE_KERNELS=1: synchronise after every kernel of a batch and name it
@@ -1308,9 +1312,16 @@ uint32_t walk_key_bits(uint32_t shape) {
   return b;
 }
 
-size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape) {
+uint32_t walk_window_bits(uint32_t n, uint32_t wshift) {
+  if (!wshift || wshift >= 32) return 0;
+  uint32_t b = 0;
+  while (b < 31 && ((uint64_t)1 << (b + wshift)) < n) ++b;   // windows of 2^wshift topics: ceil(log2(n / 2^wshift))
+  return b;
+}
+
+size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape, uint32_t wshift) {
   size_t b = 0;
-  const int bits = (int)min(walk_key_bits(shape), 32u);
+  const int bits = (int)min(walk_key_bits(shape) + walk_window_bits(n, wshift), 32u);
   hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                      (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)n, 32 - bits, 32);
   return b;
@@ -1327,15 +1338,16 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
     return hipMemsetAsync(out.row_ptr, 0, sizeof(uint64_t), s);
   }
   MatchWork w = w_in;
-  const uint32_t kbits = min(walk_key_bits(w.key_shape), 32u);
+  const uint32_t wbits = walk_window_bits(n, w.window_shift);
+  const uint32_t kbits = walk_key_bits(w.key_shape) ? min(walk_key_bits(w.key_shape) + wbits, 32u) : 0u;
   const bool sorted = kbits && w.order && n >= SORT_MIN_TOPICS && !(w.debug & DEBUG_INPUT_ORDER);
   size_t tb = 0;
   if (sorted) {
-    tb = walk_sort_temp_bytes(n, w.key_shape);
+    tb = walk_sort_temp_bytes(n, w.key_shape, w.window_shift);
     if (tb > w.sort_tmp_bytes) return hipErrorInvalidValue;   // a host sizing bug: never sort into too little scratch
   }
   WalkOrderOut wo{};
-  if (sorted) wo = WalkOrderOut{w.skey, w.sval, w.wfix, w.key_shape};
+  if (sorted) wo = WalkOrderOut{w.skey, w.sval, w.wfix, w.key_shape, w.window_shift, wbits};
   hipLaunchKernelGGL(k_tokenise, dim3((n + TOK_BLOCK - 1) / TOK_BLOCK), dim3(TOK_BLOCK), 0, s, tab, blob,
                      off, n, w.wid, w.lv, w.tfl, wo);
   trace(s, "k_tokenise");
@@ -1353,14 +1365,15 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   trace(s, "k_walk");
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
   trace(s, "k_heavy");
-  scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);
+  scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s, nullptr, w.order ? w.inv : nullptr, w.row_at);
   trace(s, "scan");
   // shorter window ranges per wave keep more copies in flight; small batches
   // get a small grid (the piece count is only known on the device)
   const uint32_t cblocks =
       (uint32_t)std::min<uint64_t>(EGM_COMPACT_BLOCKS, std::max<uint64_t>(256, ((uint64_t)n + 63) / 64));
+  const uint64_t* row_at = w.order ? w.row_at : out.row_ptr;
   hipLaunchKernelGGL(k_compact, dim3(cblocks), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.ids_tmp, n, out.row_ptr,
-                     out.ids, out.ids_cap, w.pieces_cap, w.chunk_slabs ? SLAB_PIECES / 64 : 0u, w.stats);
+                     out.ids, out.ids_cap, row_at, w.pieces_cap, w.stats);
   return hipGetLastError();
 }
 

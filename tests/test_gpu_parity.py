@@ -211,11 +211,11 @@ def test_walk_orders_vs_cpp_oracle(gm, mode, monkeypatch):
     o.add(f.blob, f.off)
     row, ids = o.match(t.blob, t.off, threads=8)
     want = canonical(row, ids)
-    for bits, debug in (("8888", 0), ("444", 0), ("68a6", 0), ("0", 0), ("8888", 4), ("8888", 1), ("8888/0", 0),
-                        ("0/0", 0)):
-        shape, _, slabs = bits.partition("/")
+    for bits, debug in (("8888", 0), ("444", 0), ("68a6", 0), ("0", 0), ("8888", 4), ("8888", 1), ("a86/14", 0),
+                        ("8888/12", 0)):
+        shape, _, win = bits.partition("/")
         monkeypatch.setenv("EGM_WALK_KEY", shape)   # key bits per level (hex nibbles, level 0 lowest)
-        monkeypatch.setenv("EGM_CHUNK_SLABS", slabs or "1")   # each chunk's pieces in a slab of their own
+        monkeypatch.setenv("EGM_WALK_WINDOW", win or "0")   # log2 of the sort window (0: the whole batch)
         gm.set_debug(debug)   # 4: EGM_DEBUG_INPUT_ORDER, 1: EGM_DEBUG_FORCE_HEAVY
         try:
             res = gm.match(t.blob, t.off, mode)

@@ -15,6 +15,7 @@
 #   pmc        FETCH_SIZE and WRITE_SIZE passes over the C2 bench (one counter per pass)
 #   sq         SQ wait/active counters + TCC hit/miss over the C2 bench
 #   host       host-visible path (egm_match_batch, pinned staging) bench
+#   s2         the C2 bench with two streams (consecutive batches overlap), then sorted / input order
 #   orders     the C2 bench, then the walk-order A/B (sort key shapes) in the same process
 #   smoke      __graft_entry__.smoke()
 #   ab_V       the C2 bench on variant V (emqx_amd/libemqx_gpu_match_V.so, tools/build_variant.py)
@@ -45,7 +46,7 @@ for step in "$@"; do
   case $step in
     tests) run tests 900 python -u -m pytest tests -m "gpu and not slow" -x -v --timeout 300 --timeout-method thread ;;
     scale) run scale 1100 python -u -m pytest tests -m "gpu and slow" -x -v --timeout 600 --timeout-method thread ;;
-    bench) run bench 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o run --output-format csv -- $B --steps 20 --warmup 5 --host-e2e off ;;
+    bench) run bench 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o run --output-format csv -- $B --steps 20 --warmup 5 --host-e2e off --pipelined off ;;
     drv) run drv 600 python $R/bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench_presort[0-9])
       k=${step#bench_presort}
@@ -58,13 +59,14 @@ for step in "$@"; do
       run "$step" 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$cfg" -o run --output-format csv -- $B --config "$cfg" --steps 10 --warmup 2 --host-e2e off ;;
     shard1) run shard1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --mode shard --steps 10 --warmup 2 --cpu-baseline off ;;
     pmc)
-      run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off
-      run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc_write" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off ;;
+      run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
+      run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc_write" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
     sq)
       run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU -d "$R/gpurun_out/${TAG}_pmc_sq" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off
       run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off ;;
     host) run host 600 python tools/bench_host.py ;;
-    orders) run orders 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "8888/1,8888/0,0/1,0/0,a86/1,8664/1,4444/1,8888/1" ;;
+    s2) run s2 400 python $R/bench.py --steps 20 --warmup 3 --streams 2 --cpu-baseline off --host-e2e off --x-orders "a86,0" ;;
+    orders) run orders 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86,0,866/20,866/21,a86/20,866/22,866,a86" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     ab_*)   # A/B variant built by tools/build_variant.py: C2 bench under rocprof stats
       v=${step#ab_}
