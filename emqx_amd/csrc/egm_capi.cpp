@@ -107,7 +107,9 @@ constexpr size_t PIPE_MAX_SLOTS = 8;
 // One match workspace: the per-batch scratch of launch_match.
 struct MatchWs {
   DevBuf wid, lv, tfl, cnt, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats;
-  DevBuf skey, skey_out, sval, order, wfix, inv, row_at, sort_tmp;   // walk-order sort (egm_kernels.hip walk_key)
+  DevBuf skey, skey_out, sval, order, wfix, sort_tmp;   // walk-order sort
+  DevBuf inv, ids_fix;                                   // fixed per-topic id blocks (k_compact_fix)
+  uint32_t fix_cap = 0;   // walk-order sort (egm_kernels.hip walk_key)
   uint64_t pieces_cap = 0, ids_tmp_cap = 0;
   uint32_t heavy_cap = 0;        // stack items per heavy wave
   hipEvent_t ev = nullptr;       // recorded after its last batch
@@ -516,6 +518,14 @@ static uint32_t walk_key_shape() {
   return walk_key_bits(shape) <= 32 ? shape : 0xa86u;
 }
 
+// EGM_FIX_CAP: ids per topic in its fixed block (the rest spill as pieces);
+// 96 keeps 98.5 % of C2's ids (50 per topic on average) out of the spill.
+static uint32_t fix_cap_ids() {
+  const char* v = getenv("EGM_FIX_CAP");
+  const int k = (v && *v) ? atoi(v) : 96;
+  return (uint32_t)std::min(std::max(k, 1), 4096);
+}
+
 // EGM_WALK_WINDOW: sort within windows of 2^k consecutive topics (0: the whole batch).
 static uint32_t walk_window_shift() {
   const char* v = getenv("EGM_WALK_WINDOW");
@@ -552,6 +562,12 @@ static int ensure_work(egm_ctx* c, MatchWs& W, uint32_t n, uint64_t blob_bytes, 
   if ((e = W.lv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "lv");
   if ((e = W.tfl.ensure(nn)) != hipSuccess) return c->hip_fail(e, "tfl");
   if ((e = W.cnt.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "cnt");
+  if ((e = W.inv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "walk positions");
+  {
+    const uint32_t cap = fix_cap_ids();
+    if ((e = W.ids_fix.ensure(nn * cap * 4)) != hipSuccess) return c->hip_fail(e, "fixed id blocks");
+    W.fix_cap = cap;
+  }
   // ids in flush order and their pieces, plus the slack of per-wave slabs
   const uint64_t tcap = ids_tmp_capacity(ids_cap, n);
   if (tcap >= 0xFFFFFFF0ull) return c->fail(EGM_E_INVAL, "batch too large: > 4G matched ids (split it)");
@@ -573,8 +589,7 @@ static int ensure_work(egm_ctx* c, MatchWs& W, uint32_t n, uint64_t blob_bytes, 
     if ((e = W.sval.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "sort values");
     if ((e = W.order.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "walk order");
     if ((e = W.wfix.ensure(nn * 4 * FIX_WORDS)) != hipSuccess) return c->hip_fail(e, "fixed-stride words");
-    if ((e = W.row_at.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "walk-order rows");
-    if ((e = W.inv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "walk positions");
+
     if ((e = W.sort_tmp.ensure(walk_sort_temp_bytes(n, shape, walk_window_shift()))) != hipSuccess)
       return c->hip_fail(e, "sort scratch");
   }
@@ -589,6 +604,9 @@ static MatchWork work_view(egm_ctx* c, MatchWs& W) {
   w.lv = W.lv.as<uint32_t>();
   w.tfl = W.tfl.as<uint8_t>();
   w.cnt = W.cnt.as<uint32_t>();
+  w.inv = W.inv.as<uint32_t>();
+  w.ids_fix = W.ids_fix.as<uint32_t>();
+  w.fix_cap = W.fix_cap;
   w.ids_tmp = W.ids_tmp.as<uint32_t>();
   w.ids_cap = W.ids_tmp_cap;   // ids_tmp entries (the output capacity is MatchOut's)
   w.pieces = W.pieces.as<uint4>();
@@ -607,8 +625,7 @@ static MatchWork work_view(egm_ctx* c, MatchWs& W) {
     w.sval = W.sval.as<uint64_t>();
     w.order = W.order.as<uint64_t>();
     w.wfix = W.wfix.as<uint32_t>();
-    w.row_at = W.row_at.as<uint64_t>();
-    w.inv = W.inv.as<uint32_t>();
+
     w.sort_tmp = W.sort_tmp.p;
     w.sort_tmp_bytes = W.sort_tmp.cap;
     w.window_shift = walk_window_shift();

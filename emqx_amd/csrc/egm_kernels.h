@@ -36,8 +36,8 @@ struct MatchStats {               // device-side counters, zeroed per batch
   unsigned long long plus_reads;  // walk pops that read a '+' child's record (instrumentation)
 };
 
-// A piece is one flush's run of a topic's ids in ids_tmp:
-// {topic's walk position, count, ids_tmp offset, offset inside the topic's CSR row}, so the
+// A piece is one flush's run of a topic's spilled ids in ids_tmp:
+// {topic, count, ids_tmp offset, offset inside the topic's CSR row}, so the
 // compaction places every run without atomics (count 0: an unused slot).
 // Each wave reserves its output space in slabs (one device-scope atomic per
 // slab): a single shared counter bumped per flush serialises across the 8
@@ -50,6 +50,9 @@ struct MatchWork {                // per-batch device workspace
   uint32_t* lv;                   // [n] levels
   uint8_t* tfl;                   // [n] TF_* flags
   uint32_t* cnt;                  // [n] number of ids of topic t
+  uint32_t* inv;                  // [n] walk position of topic t = its fixed block (NONE: a heavy topic, no block)
+  uint32_t* ids_fix;              // [n * fix_cap] each walked topic's first fix_cap ids, by walk position
+  uint32_t fix_cap;               // ids per fixed block (the rest spill into ids_tmp as pieces)
   uint32_t* ids_tmp;              // [ids_cap] ids in flush order
   uint64_t ids_cap;
   uint4* pieces;                  // [pieces_cap]
@@ -74,8 +77,6 @@ struct MatchWork {                // per-batch device workspace
   size_t sort_tmp_bytes;
   uint32_t key_shape;             // key bits per level, nibble l = level l (0: walk in input order)
   uint32_t window_shift;          // sort within windows of 2^window_shift consecutive topics (0: the whole batch)
-  uint32_t* inv;                  // [n] walk position of topic t (written by the walk; sorted batches)
-  uint64_t* row_at;               // [n] row starts by walk position (the scan; k_compact reads them)
 };
 
 constexpr uint32_t KEY_LEVELS = 4;           // levels hashed into the walk-order key

@@ -485,6 +485,7 @@ constexpr uint32_t WALK_WORDS = EGM_WALK_WORDS;
 constexpr uint32_t LIGHT_DMAX = (WALK_STACK - 64) < WALK_WORDS ? (WALK_STACK - 64) : WALK_WORDS;
 static_assert(WALK_CHUNK == 64, "one topic per lane in the chunk prologue");
 static_assert(WALK_STAGE >= 256, "a step stages up to 4 emits x 64 lanes");
+static_assert(WALK_STAGE <= 0xFFFF, "flush slots and spill starts are packed as 16-bit halves");
 static_assert(LIGHT_DMAX >= 16, "stack too small");
 
 struct alignas(16) WaveLds {
@@ -537,11 +538,13 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
 
 // Write the stage out.  Entries are ranked within their topic by a
 // conflict-free multi-split (lanes holding the same topic find each other
-// with 6 ballots; one LDS add per topic per 64 entries), then scattered into
-// the wave's ids slab grouped by topic: one piece {topic, count, ids_tmp
-// offset, offset inside the topic's CSR row} per topic present, so the
-// compaction needs no atomics.
-__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t pos, uint32_t lane,
+// with 6 ballots; one LDS add per topic per 64 entries).  A topic's first
+// fix_cap ids go straight to its fixed block in ids_fix (walk position x
+// fix_cap; a chunk's blocks are one contiguous region); the rest spill into
+// the wave's ids slab grouped by topic, one piece
+// {topic, count, ids_tmp offset, offset inside the topic's CSR row} per topic
+// that spills, so neither compaction needs atomics.
+__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t my_t, uint32_t lane,
                                             const MatchWork& w, Slab& sid, Slab& spc) {
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {
@@ -562,24 +565,52 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
     if (act) L.stage_rank[i] = (uint16_t)(old + mbcnt(m));
   }
   wave_sync();
-  const uint32_t fl = L.fcnt[lane];   // topic t0 + lane
+  const uint32_t cap = w.fix_cap;
+  const uint32_t fl = L.fcnt[lane];   // the chunk's topic `lane`: ids in this flush
+  const uint32_t c0 = L.cnt[lane];    // ... and before it
+  const uint32_t nfix = c0 >= cap ? 0u : min(fl, cap - c0);
+  const uint32_t over = fl - nfix;    // ids past the fixed block: spilled
   uint32_t tot, ptot;
-  const uint32_t ex = wave_excl_scan(fl, lane, &tot);
-  const uint32_t pex = wave_excl_scan(fl ? 1u : 0u, lane, &ptot);
-  const unsigned long long base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
-  const unsigned long long pbase = slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
-  const bool ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
-  if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
-  if (fl && ok) w.pieces[pbase + pex] = make_uint4(pos, fl, (uint32_t)(base + ex), L.cnt[lane]);
-  L.fcnt[lane] = ex;   // the topic's start inside this flush
-  L.cnt[lane] += fl;
+  const uint32_t ex = wave_excl_scan(over, lane, &tot);
+  const uint32_t pex = wave_excl_scan(over ? 1u : 0u, lane, &ptot);
+  unsigned long long base = 0;
+  bool ok = true;
+  if (tot) {   // wave-uniform
+    base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
+    const unsigned long long pbase =
+        slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
+    ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
+    if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
+    if (over && ok) w.pieces[pbase + pex] = make_uint4(my_t, over, (uint32_t)(base + ex), c0 + nfix);
+  }
+  // Stores go out in topic order: slot q of the flush (topics in lane order,
+  // each topic's entries by rank) -> its entry, so consecutive lanes write
+  // consecutive ids of a block instead of one line per lane.
+  uint32_t gtot;
+  const uint32_t gx = wave_excl_scan(fl, lane, &gtot);
+  L.fcnt[lane] = ex | (gx << 16);   // spill start | first slot (both < WALK_STAGE)
   wave_sync();
-  if (ok) {
-#pragma unroll 1
-    for (uint32_t i = lane; i < nstage; i += 64)
-      w.ids_tmp[base + L.fcnt[L.stage_t[i]] + L.stage_rank[i]] = L.stage_fid[i];
+  constexpr uint32_t NQ = (WALK_STAGE + 63) / 64;
+  uint32_t qv[NQ];
+#pragma unroll
+  for (uint32_t r = 0; r < NQ; ++r) {
+    const uint32_t i = lane + 64 * r;
+    qv[r] = i < nstage ? (L.fcnt[L.stage_t[i]] >> 16) + L.stage_rank[i] : 0u;
   }
   wave_sync();
+#pragma unroll
+  for (uint32_t r = 0; r < NQ; ++r)
+    if (lane + 64 * r < nstage) L.stage_rank[qv[r]] = (uint16_t)(lane + 64 * r);   // now: slot -> entry
+  wave_sync();
+#pragma unroll 1
+  for (uint32_t q = lane; q < nstage; q += 64) {
+    const uint32_t i = L.stage_rank[q], tt = L.stage_t[i], f = L.fcnt[tt], cb = L.cnt[tt];
+    const uint32_t k = cb + (q - (f >> 16));
+    if (k < cap) w.ids_fix[(uint64_t)(t0 + tt) * cap + k] = L.stage_fid[i];
+    else if (ok) w.ids_tmp[base + (f & 0xFFFFu) + (k - max(cb, cap))] = L.stage_fid[i];
+  }
+  wave_sync();
+  L.cnt[lane] += fl;
   L.fcnt[lane] = 0;
   wave_sync();
 }
@@ -827,7 +858,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         if (sp < 64u && next < end) {
           const uint32_t k = min(64u - sp, end - next);
           if (nstage + 64u > WALK_STAGE) {
-            flush_stage(L, nstage, t0 + lane, lane, w, sid, spc);
+            flush_stage(L, nstage, t0, my_t, lane, w, sid, spc);
             nstage = 0;
           }
           bool has = false, em = false;
@@ -908,7 +939,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
         if (nstage + ne > WALK_STAGE) {
           wave_sync();
-          flush_stage(L, nstage, t0 + lane, lane, w, sid, spc);
+          flush_stage(L, nstage, t0, my_t, lane, w, sid, spc);
           nstage = 0;
         }
         const uint8_t st = (uint8_t)tt;
@@ -936,10 +967,10 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         wave_sync();
       }
     }
-    if (nstage) flush_stage(L, nstage, t0 + lane, lane, w, sid, spc);
+    if (nstage) flush_stage(L, nstage, t0, my_t, lane, w, sid, spc);
     if (lane < nt) {
       w.cnt[my_t] = L.cnt[lane];
-      if (ord) w.inv[my_t] = t0 + lane;
+      w.inv[my_t] = t0 + lane;   // its fixed block (k_compact_fix)
     }
     wave_sync();
   }
@@ -999,7 +1030,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
     const uint32_t pos = w.deferred[idx / WALK_CHUNK] * WALK_CHUNK + idx % WALK_CHUNK;   // in walk order
     if (pos >= n) continue;
     const uint32_t t = uni(w.order ? (uint32_t)w.order[pos] : pos);
-    if (lane == 0 && w.order) w.inv[t] = pos;
+    if (lane == 0) w.inv[t] = NONE;   // every id of a heavy topic is in its piece (no fixed block)
     const uint32_t D = uni(w.lv[t]), tf = uni(w.tfl[t]), tb = uni(off[t] + t);
     if (tf & TF_WILDCARD) {   // no trie walk: TRIE mode matches nothing, ROUTES mode one exact lookup
       uint32_t fid = NONE;
@@ -1010,7 +1041,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
           const unsigned long long p = atomicAdd(&w.stats->pieces, 1ull);
           if (base < w.ids_cap && p < w.pieces_cap) {
             w.ids_tmp[base] = fid;
-            w.pieces[p] = make_uint4(pos, 1, (uint32_t)base, 0);
+            w.pieces[p] = make_uint4(t, 1, (uint32_t)base, 0);
           } else {
             atomicOr(&w.stats->overflow, 1u);
           }
@@ -1102,7 +1133,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
         if (lane == 0) {
           if (!fits) atomicOr(&w.stats->overflow, 1u);
           w.cnt[t] = count;
-          if (count && fits) w.pieces[pb] = make_uint4(pos, count, (uint32_t)base, 0);
+          if (count && fits) w.pieces[pb] = make_uint4(t, count, (uint32_t)base, 0);
           w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
         }
         if (!count || !fits) break;
@@ -1158,8 +1189,7 @@ __global__ __launch_bounds__(1024) void k_scan_top(uint64_t* __restrict__ tile_s
 
 __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__ cnt, uint32_t n,
                                                     const uint64_t* __restrict__ tile_sums, uint32_t ntiles,
-                                                    uint64_t* __restrict__ row_ptr, uint64_t* __restrict__ copy,
-                                                    const uint32_t* __restrict__ inv, uint64_t* __restrict__ row_at) {
+                                                    uint64_t* __restrict__ row_ptr, uint64_t* __restrict__ copy) {
   __shared__ uint64_t wsum[4];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t i0 = blockIdx.x * SCAN_TILE + threadIdx.x * 8;
@@ -1185,46 +1215,72 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
     if (i0 + k < n) {
       row_ptr[i0 + k] = pre;
       if (copy) copy[i0 + k] = pre;
-      if (inv) row_at[inv[i0 + k]] = pre;   // sorted batch: the row start by walk position (k_compact)
     }
     pre += v[k];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) row_ptr[n] = tile_sums[ntiles];
 }
 
-// Pieces -> CSR rows, no atomics.  A piece names its topic by walk position
-// (row_at: the row starts in walk order).  One wave per window of 64 pieces: a wave
-// scan lays the window's ids out as one run [0, tot), and the lanes copy that
-// run with consecutive lanes on consecutive ids (a binary search over the
-// window's 64 scan values finds each id's piece).  The pieces of one flush
-// have contiguous sources and topics of one chunk, so the reads and the
-// row_ptr loads coalesce; a contiguous range of windows per wave (not a grid
-// stride) keeps a chunk's flushes — and so the cache lines of its rows — with
-// one wave.  Unused slab slots (count 0) are skipped.
+// Spilled pieces -> CSR rows, no atomics.  One wave per window of 64 pieces:
+// a wave scan lays the window's ids out as one run [0, tot), and the lanes
+// copy that run with consecutive lanes on consecutive ids (a binary search
+// over the window's 64 scan values finds each id's piece).  Unused slab slots
+// (count 0) are skipped.  Pieces hold the ids past a topic's fixed block (and
+// every id of a heavy topic): a few percent of the batch at C2.
 #ifndef EGM_COMPACT_WAVES
 #define EGM_COMPACT_WAVES 4
 #endif
 #ifndef EGM_COMPACT_BLOCKS
-#define EGM_COMPACT_BLOCKS 65536   // grid cap; A/B at C2: 8192 -> 2.07 ms, 32768 -> 1.80, 65536 -> 1.74
+#define EGM_COMPACT_BLOCKS 65536   // grid cap
 #endif
 constexpr int COMPACT_WAVES = EGM_COMPACT_WAVES;
 constexpr int COMPACT_IPL = 8;   // ids per lane per copy round in flight
+
+// The copy of one window of up to 64 runs (src, dst, count) laid out in LDS.
+__device__ __forceinline__ void copy_runs(const uint32_t* __restrict__ src_base, uint32_t* __restrict__ ids,
+                                          const uint32_t* s_scan, const uint64_t* s_src, const uint64_t* s_dst,
+                                          uint32_t tot, uint32_t lane) {
+  for (uint32_t q0 = lane; q0 < tot; q0 += 64 * COMPACT_IPL) {
+    uint32_t v[COMPACT_IPL];
+    uint64_t d[COMPACT_IPL];
+#pragma unroll
+    for (int r = 0; r < COMPACT_IPL; ++r) {
+      const uint32_t q = min(q0 + 64u * r, tot - 1);
+      uint32_t k = 0;
+#pragma unroll
+      for (uint32_t step = 32; step >= 1; step >>= 1)
+        if (s_scan[k + step] <= q) k += step;
+      const uint32_t o = q - s_scan[k];
+      d[r] = s_dst[k] + o;
+      v[r] = src_base[s_src[k] + o];
+    }
+#pragma unroll
+    for (int r = 0; r < COMPACT_IPL; ++r)
+      if (q0 + 64u * r < tot) ids[d[r]] = v[r];   // plain stores: nontemporal ones measured 2x slower here
+  }
+}
+
+__device__ __forceinline__ bool compact_checks(const uint64_t* row_ptr, uint32_t n, uint64_t ids_cap,
+                                               MatchStats* stats) {
+  const uint64_t total = row_ptr[n];
+  if (blockIdx.x == 0 && threadIdx.x == 0) stats->total_ids = total;
+  if (stats->overflow) return false;
+  if (total > ids_cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, 2u);
+    return false;
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __restrict__ pieces,
                                                                 const uint32_t* __restrict__ ids_tmp, uint32_t n,
                                                                 const uint64_t* __restrict__ row_ptr,
                                                                 uint32_t* __restrict__ ids, uint64_t ids_cap,
-                                                                const uint64_t* __restrict__ row_at,
                                                                 uint64_t pieces_cap, MatchStats* stats) {
   __shared__ uint32_t s_scan[COMPACT_WAVES][64];
-  __shared__ uint32_t s_src[COMPACT_WAVES][64];
+  __shared__ uint64_t s_src[COMPACT_WAVES][64];
   __shared__ uint64_t s_dst[COMPACT_WAVES][64];
-  const uint64_t total = row_ptr[n];
-  if (blockIdx.x == 0 && threadIdx.x == 0) stats->total_ids = total;
-  if (stats->overflow) return;
-  if (total > ids_cap) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, 2u);
-    return;
-  }
+  if (!compact_checks(row_ptr, n, ids_cap, stats)) return;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t np = min((uint64_t)stats->pieces, pieces_cap);
   if (np == 0) return;
@@ -1236,7 +1292,7 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
   for (; w0 < wend; w0 += 64) {
     const uint64_t i = w0 + lane;
     const uint32_t c = i < np ? pc.y : 0u;
-    const uint64_t rp = row_at[c ? pc.x : 0u];   // the piece's topic by its walk position
+    const uint64_t rp = row_ptr[c ? pc.x : 0u];
     uint32_t tot;
     const uint32_t ex = wave_excl_scan(c, lane, &tot);
     s_scan[wave][lane] = ex;
@@ -1244,24 +1300,41 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
     s_dst[wave][lane] = rp + pc.w;
     wave_sync();
     pc = pieces[min(i + 64, np - 1)];   // the next window's piece, in flight during the copy
-    for (uint32_t q0 = lane; q0 < tot; q0 += 64 * COMPACT_IPL) {
-      uint32_t v[COMPACT_IPL];
-      uint64_t d[COMPACT_IPL];
-#pragma unroll
-      for (int r = 0; r < COMPACT_IPL; ++r) {
-        const uint32_t q = min(q0 + 64u * r, tot - 1);
-        uint32_t k = 0;
-#pragma unroll
-        for (uint32_t step = 32; step >= 1; step >>= 1)
-          if (s_scan[wave][k + step] <= q) k += step;
-        const uint32_t o = q - s_scan[wave][k];
-        d[r] = s_dst[wave][k] + o;
-        v[r] = ids_tmp[s_src[wave][k] + o];
-      }
-#pragma unroll
-      for (int r = 0; r < COMPACT_IPL; ++r)
-        if (q0 + 64u * r < tot) ids[d[r]] = v[r];   // plain stores: nontemporal ones measured 2x slower here
-    }
+    copy_runs(ids_tmp, ids, s_scan[wave], s_src[wave], s_dst[wave], tot, lane);
+    wave_sync();
+  }
+}
+
+// Fixed blocks -> CSR rows in input order: one wave per 64 consecutive
+// topics, whose rows are one contiguous run of the output (whole lines
+// written), each topic's block a contiguous run of ids_fix (its walk position
+// x fix_cap): the same windowed copy as k_compact with the topics as the runs.
+// (A chunk-major variant — rank-major blocks staged through LDS and rows
+// written scattered — measured 6x slower: DESIGN.md §4.1.)
+__global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact_fix(const uint32_t* __restrict__ cnt,
+                                                                    const uint32_t* __restrict__ inv,
+                                                                    const uint32_t* __restrict__ ids_fix,
+                                                                    uint32_t cap, uint32_t n,
+                                                                    const uint64_t* __restrict__ row_ptr,
+                                                                    uint32_t* __restrict__ ids, uint64_t ids_cap,
+                                                                    MatchStats* stats) {
+  __shared__ uint32_t s_scan[COMPACT_WAVES][64];
+  __shared__ uint64_t s_src[COMPACT_WAVES][64];
+  __shared__ uint64_t s_dst[COMPACT_WAVES][64];
+  if (!compact_checks(row_ptr, n, ids_cap, stats)) return;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t ngroups = (n + 63) / 64;
+  for (uint32_t g = blockIdx.x * COMPACT_WAVES + wave; g < ngroups; g += gridDim.x * COMPACT_WAVES) {
+    const uint32_t t = min(g * 64 + lane, n - 1);
+    const uint32_t p = inv[t];
+    const uint32_t c = (g * 64 + lane < n && p != NONE) ? min(cnt[t], cap) : 0u;
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan(c, lane, &tot);
+    s_scan[wave][lane] = ex;
+    s_src[wave][lane] = (uint64_t)(p != NONE ? p : 0u) * cap;
+    s_dst[wave][lane] = row_ptr[t];
+    wave_sync();
+    copy_runs(ids_fix, ids, s_scan[wave], s_src[wave], s_dst[wave], tot, lane);
     wave_sync();
   }
 }
@@ -1280,13 +1353,12 @@ uint32_t heavy_stack_items(uint64_t max_levels) { return (uint32_t)(max_levels +
 size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
 static void scan_counts(const uint32_t* cnt, uint32_t n, uint64_t* tile_sums, uint64_t* row_ptr,
-                        hipStream_t s, uint64_t* copy = nullptr, const uint32_t* inv = nullptr,
-                        uint64_t* row_at = nullptr) {
+                        hipStream_t s, uint64_t* copy = nullptr) {
   const uint32_t ntiles = (uint32_t)scan_tiles(n);
   if (ntiles) hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(256), 0, s, cnt, n, tile_sums);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, tile_sums, ntiles);
   hipLaunchKernelGGL(k_scan_apply, dim3(ntiles ? ntiles : 1), dim3(256), 0, s, cnt, n, tile_sums, ntiles, row_ptr,
-                     copy, inv, row_at);
+                     copy);
 }
 
 // EGM_TRACE_KERNELS=1: synchronise after every kernel of a batch and name it
@@ -1365,15 +1437,19 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   trace(s, "k_walk");
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
   trace(s, "k_heavy");
-  scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s, nullptr, w.order ? w.inv : nullptr, w.row_at);
+  scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);
   trace(s, "scan");
   // shorter window ranges per wave keep more copies in flight; small batches
   // get a small grid (the piece count is only known on the device)
   const uint32_t cblocks =
       (uint32_t)std::min<uint64_t>(EGM_COMPACT_BLOCKS, std::max<uint64_t>(256, ((uint64_t)n + 63) / 64));
-  const uint64_t* row_at = w.order ? w.row_at : out.row_ptr;
+  const uint32_t fblocks = (uint32_t)std::min<uint64_t>(
+      65536, std::max<uint64_t>(1, (((uint64_t)n + 63) / 64 + COMPACT_WAVES - 1) / COMPACT_WAVES));
+  hipLaunchKernelGGL(k_compact_fix, dim3(fblocks), dim3(64 * COMPACT_WAVES), 0, s, w.cnt, w.inv, w.ids_fix, w.fix_cap,
+                     n, out.row_ptr, out.ids, out.ids_cap, w.stats);
+  trace(s, "k_compact_fix");
   hipLaunchKernelGGL(k_compact, dim3(cblocks), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.ids_tmp, n, out.row_ptr,
-                     out.ids, out.ids_cap, row_at, w.pieces_cap, w.stats);
+                     out.ids, out.ids_cap, w.pieces_cap, w.stats);
   return hipGetLastError();
 }
 
