@@ -214,9 +214,8 @@ def main():
                          "would save the walk")
     ap.add_argument("--x-orders", default="",
                     help="experiment: after the timed steps, time the same steps under each walk order "
-                         "'shape[/window[/cap]],...' (EGM_WALK_KEY: key bits per level as hex nibbles, level 0 lowest, "
-                         "0 = input order; EGM_WALK_WINDOW: log2 of the sort window, 0 = whole batch; EGM_FIX_CAP: ids "
-                         "per fixed block) and check "
+                         "'shape[/cap],...' (EGM_WALK_KEY: key bits per level as hex nibbles, level 0 lowest, 0 = "
+                         "input order; EGM_FIX_CAP: ids per fixed block) and check "
                          "that every order gives the same rows (stderr)")
     ap.add_argument("--pipelined", default="on", choices=["on", "off"],
                     help="after the timed steps, time them again with consecutive batches over two streams "
@@ -551,14 +550,14 @@ def order_experiment(args, gm, run_local, bufs, dev, n):
         cs = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), cs])
         return row.clone(), cs[row]
 
-    saved = {k: os.environ.get(k) for k in ("EGM_WALK_KEY", "EGM_WALK_WINDOW", "EGM_FIX_CAP")}
+    saved = {k: os.environ.get(k) for k in ("EGM_WALK_KEY", "EGM_FIX_CAP")}
     bufs["k"] = 0
     run_local()
     torch.cuda.synchronize(dev)
     ref_row, ref_sig = rows_sig()
     for spec in args.x_orders.split(","):
-        shape, win, cap = (spec.split("/") + ["", ""])[:3]
-        os.environ["EGM_WALK_KEY"], os.environ["EGM_WALK_WINDOW"] = shape, win or "0"
+        shape, _, cap = spec.partition("/")
+        os.environ["EGM_WALK_KEY"] = shape
         if cap:
             os.environ["EGM_FIX_CAP"] = cap
         else:

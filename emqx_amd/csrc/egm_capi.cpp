@@ -526,13 +526,6 @@ static uint32_t fix_cap_ids() {
   return (uint32_t)std::min(std::max(k, 1), 4096);
 }
 
-// EGM_WALK_WINDOW: sort within windows of 2^k consecutive topics (0: the whole batch).
-static uint32_t walk_window_shift() {
-  const char* v = getenv("EGM_WALK_WINDOW");
-  const uint32_t k = (v && *v) ? (uint32_t)atoi(v) : 0u;
-  return k < 32 ? k : 0u;
-}
-
 // The workspace for a batch on stream s: the one that last ran on s (stream
 // order protects it), else the least recently used one, ordered after its
 // last batch on the other stream.
@@ -590,8 +583,7 @@ static int ensure_work(egm_ctx* c, MatchWs& W, uint32_t n, uint64_t blob_bytes, 
     if ((e = W.order.ensure(nn * 8)) != hipSuccess) return c->hip_fail(e, "walk order");
     if ((e = W.wfix.ensure(nn * 4 * FIX_WORDS)) != hipSuccess) return c->hip_fail(e, "fixed-stride words");
 
-    if ((e = W.sort_tmp.ensure(walk_sort_temp_bytes(n, shape, walk_window_shift()))) != hipSuccess)
-      return c->hip_fail(e, "sort scratch");
+    if ((e = W.sort_tmp.ensure(walk_sort_temp_bytes(n, shape))) != hipSuccess) return c->hip_fail(e, "sort scratch");
   }
   if (!W.ev && (e = hipEventCreateWithFlags(&W.ev, hipEventDisableTiming)) != hipSuccess)
     return c->hip_fail(e, "workspace event");
@@ -628,7 +620,6 @@ static MatchWork work_view(egm_ctx* c, MatchWs& W) {
 
     w.sort_tmp = W.sort_tmp.p;
     w.sort_tmp_bytes = W.sort_tmp.cap;
-    w.window_shift = walk_window_shift();
   } else {
     w.key_shape = 0;
   }

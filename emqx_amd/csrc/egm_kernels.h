@@ -76,7 +76,6 @@ struct MatchWork {                // per-batch device workspace
   void* sort_tmp;                 // radix sort scratch
   size_t sort_tmp_bytes;
   uint32_t key_shape;             // key bits per level, nibble l = level l (0: walk in input order)
-  uint32_t window_shift;          // sort within windows of 2^window_shift consecutive topics (0: the whole batch)
 };
 
 constexpr uint32_t KEY_LEVELS = 4;           // levels hashed into the walk-order key
@@ -86,7 +85,6 @@ struct WalkOrderOut {                        // what k_tokenise writes for the s
   uint64_t* val;
   uint32_t* wfix;
   uint32_t shape;
-  uint32_t wshift, wbits;                    // sorted within windows of 2^wshift topics (wbits: window index bits)
 };
 
 constexpr uint32_t DEBUG_FORCE_HEAVY = 1u;   // every chunk goes to k_heavy (test coverage)
@@ -95,8 +93,7 @@ constexpr uint32_t DEBUG_INPUT_ORDER = 4u;   // walk in input order (no locality
 // walk-order key: total bits of a key shape; radix sort scratch bytes for a
 // batch of n topics (hipcub)
 uint32_t walk_key_bits(uint32_t shape);
-uint32_t walk_window_bits(uint32_t n, uint32_t wshift);
-size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape, uint32_t wshift);
+size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape);
 
 struct MatchOut {                 // CSR result (device)
   uint64_t* row_ptr;              // [n + 1]

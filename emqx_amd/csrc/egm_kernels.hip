@@ -222,14 +222,6 @@ __device__ __forceinline__ uint32_t walk_key(const uint32_t* w4, uint32_t D, uin
   return used < 32 ? k << (32 - used) : k;
 }
 
-// Sorted within windows of 2^wshift consecutive topics: the window index in
-// the key's top wbits bits, the prefix key below it.  A window's rows span a
-// bounded region of the output, so the scattered writes of a sorted batch
-// stay within what the caches can merge.
-__device__ __forceinline__ uint32_t window_key(const WalkOrderOut& wo, uint32_t t, uint32_t k) {
-  return wo.wbits ? (((t >> wo.wshift) << (32 - wo.wbits)) | (k >> wo.wbits)) : k;
-}
-
 // the sort's value: topic | (levels | flags << 24 | words at the fixed stride << 31) << 32
 __device__ __forceinline__ uint64_t sort_val(uint32_t t, uint32_t D, uint32_t f, bool fixed) {
   return (uint64_t)t | ((uint64_t)(min(D, 0xFFFFFFu) | ((f & 0x7Fu) << 24) | (fixed ? 0x80000000u : 0u)) << 32);
@@ -284,7 +276,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         lv[t0] = l;
         tfl[t0] = fl;
         if (wo.key) {
-          wo.key[t0] = window_key(wo, t0, 0xFFFFFFFFu);
+          wo.key[t0] = 0xFFFFFFFFu;   // sorted last
           wo.val[t0] = sort_val(t0, l, fl, false);
         }
       }
@@ -334,7 +326,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         lv[t] = l;
         tfl[t] = f;
         if (wo.key) {
-          wo.key[t] = window_key(wo, t, 0xFFFFFFFFu);
+          wo.key[t] = 0xFFFFFFFFu;
           wo.val[t] = sort_val(t, l, f, false);
         }
       }
@@ -422,7 +414,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         uint32_t w4[KEY_LEVELS];
 #pragma unroll
         for (uint32_t k = 0; k < KEY_LEVELS; ++k) w4[k] = kw[tid][k];
-        wo.key[t] = window_key(wo, t, walk_key(w4, D, wo.shape));
+        wo.key[t] = walk_key(w4, D, wo.shape);
         wo.val[t] = sort_val(t, D, tflag[tid], D <= FIX_WORDS);
       }
     }
@@ -1384,16 +1376,9 @@ uint32_t walk_key_bits(uint32_t shape) {
   return b;
 }
 
-uint32_t walk_window_bits(uint32_t n, uint32_t wshift) {
-  if (!wshift || wshift >= 32) return 0;
-  uint32_t b = 0;
-  while (b < 31 && ((uint64_t)1 << (b + wshift)) < n) ++b;   // windows of 2^wshift topics: ceil(log2(n / 2^wshift))
-  return b;
-}
-
-size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape, uint32_t wshift) {
+size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape) {
   size_t b = 0;
-  const int bits = (int)min(walk_key_bits(shape) + walk_window_bits(n, wshift), 32u);
+  const int bits = (int)min(walk_key_bits(shape), 32u);
   hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                      (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)n, 32 - bits, 32);
   return b;
@@ -1410,16 +1395,15 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
     return hipMemsetAsync(out.row_ptr, 0, sizeof(uint64_t), s);
   }
   MatchWork w = w_in;
-  const uint32_t wbits = walk_window_bits(n, w.window_shift);
-  const uint32_t kbits = walk_key_bits(w.key_shape) ? min(walk_key_bits(w.key_shape) + wbits, 32u) : 0u;
+  const uint32_t kbits = min(walk_key_bits(w.key_shape), 32u);
   const bool sorted = kbits && w.order && n >= SORT_MIN_TOPICS && !(w.debug & DEBUG_INPUT_ORDER);
   size_t tb = 0;
   if (sorted) {
-    tb = walk_sort_temp_bytes(n, w.key_shape, w.window_shift);
+    tb = walk_sort_temp_bytes(n, w.key_shape);
     if (tb > w.sort_tmp_bytes) return hipErrorInvalidValue;   // a host sizing bug: never sort into too little scratch
   }
   WalkOrderOut wo{};
-  if (sorted) wo = WalkOrderOut{w.skey, w.sval, w.wfix, w.key_shape, w.window_shift, wbits};
+  if (sorted) wo = WalkOrderOut{w.skey, w.sval, w.wfix, w.key_shape};
   hipLaunchKernelGGL(k_tokenise, dim3((n + TOK_BLOCK - 1) / TOK_BLOCK), dim3(TOK_BLOCK), 0, s, tab, blob,
                      off, n, w.wid, w.lv, w.tfl, wo);
   trace(s, "k_tokenise");

@@ -203,7 +203,7 @@ def test_walk_orders_vs_cpp_oracle(gm, mode, monkeypatch):
     """The walk's locality order (the key k_tokenise computes, the radix sort,
     the walk reading sorted topic records and fixed-stride words) and the
     output layout (fixed per-topic blocks + spilled pieces) never change a
-    result: several key shapes, windowed sorts, input order, a partial last
+    result: several key shapes, input order, a partial last
     chunk, sorted + every chunk through k_heavy, and fixed blocks of 1-3 ids
     (nearly every id spilled), all bit-exact against the C++ oracle
     (egm_kernels.hip launch_match)."""
@@ -213,12 +213,9 @@ def test_walk_orders_vs_cpp_oracle(gm, mode, monkeypatch):
     o.add(f.blob, f.off)
     row, ids = o.match(t.blob, t.off, threads=8)
     want = canonical(row, ids)
-    for bits, debug, cap in (("8888", 0, 96), ("444", 0, 96), ("68a6", 0, 96), ("0", 0, 96), ("8888", 4, 96),
-                             ("8888", 1, 96), ("a86/14", 0, 96), ("8888/12", 0, 96), ("a86", 0, 1), ("a86", 0, 3),
-                             ("0", 0, 2), ("a86", 1, 1)):
-        shape, _, win = bits.partition("/")
-        monkeypatch.setenv("EGM_WALK_KEY", shape)   # key bits per level (hex nibbles, level 0 lowest)
-        monkeypatch.setenv("EGM_WALK_WINDOW", win or "0")   # log2 of the sort window (0: the whole batch)
+    for bits, debug, cap in (("a86", 0, 96), ("8888", 0, 96), ("444", 0, 96), ("68a6", 0, 96), ("0", 0, 96),
+                             ("a86", 4, 96), ("a86", 1, 96), ("a86", 0, 1), ("a86", 0, 3), ("0", 0, 2), ("a86", 1, 1)):
+        monkeypatch.setenv("EGM_WALK_KEY", bits)   # key bits per level (hex nibbles, level 0 lowest)
         monkeypatch.setenv("EGM_FIX_CAP", str(cap))   # ids per fixed block: small caps spill most ids into pieces
         gm.set_debug(debug)   # 4: EGM_DEBUG_INPUT_ORDER, 1: EGM_DEBUG_FORCE_HEAVY
         try:

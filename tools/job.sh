@@ -56,7 +56,7 @@ for step in "$@"; do
       run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_s$k" -o run --output-format csv -- $B --steps 20 --warmup 5 --streams "$k" --cpu-baseline off --host-e2e off ;;
     bench_c1|bench_c3|bench_c4)
       cfg=${step#bench_}
-      run "$step" 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$cfg" -o run --output-format csv -- $B --config "$cfg" --steps 10 --warmup 2 --host-e2e off ;;
+      run "$step" 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$cfg" -o run --output-format csv -- $B --config "$cfg" --steps 10 --warmup 2 --host-e2e off --pipelined off ;;
     shard1) run shard1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --mode shard --steps 10 --warmup 2 --cpu-baseline off ;;
     pmc)
       run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
@@ -66,7 +66,7 @@ for step in "$@"; do
       run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off ;;
     host) run host 600 python tools/bench_host.py ;;
     s2) run s2 400 python $R/bench.py --steps 20 --warmup 3 --streams 2 --cpu-baseline off --host-e2e off --x-orders "a86,0" ;;
-    orders) run orders 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86,0,a86/0/64,a86/0/128,a86/0/48,0/0/64,a86" ;;
+    orders) run orders 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86,0,a86/128,a86" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     ab_*)   # A/B variant built by tools/build_variant.py: C2 bench under rocprof stats
       v=${step#ab_}
