@@ -209,6 +209,7 @@ def test_walk_orders_vs_cpp_oracle(gm, mode, monkeypatch):
     (egm_kernels.hip launch_match)."""
     f, t = synth.config("c0", n_topics=70_001)
     gm.build(f.blob, f.off)
+    monkeypatch.setenv("EGM_WALK_SORT_MIN_BYTES", "0")   # sort whatever the table size
     o = OracleTrie(True, mode)
     o.add(f.blob, f.off)
     row, ids = o.match(t.blob, t.off, threads=8)
