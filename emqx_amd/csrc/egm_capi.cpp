@@ -183,7 +183,7 @@ struct egm_ctx {
   DevBuf m_srow, m_tiles, m_tot;
 
   // fan-out
-  DevBuf sub_row, sub_ids, f_dc, f_ds0, f_dpos, f_tiles, f_ovf, f_mrow, f_mids, f_drow, f_dfid, f_dsub;
+  DevBuf sub_row, sub_rp, sub_ids, f_dc, f_ds0, f_dpos, f_tiles, f_ovf, f_mrow, f_mids, f_drow, f_dfid, f_dsub;
   uint32_t n_fid_slots = 0;
 
   // timing
@@ -1160,6 +1160,10 @@ int egm_subs_build(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint
     return c->hip_fail(e, "H2D sub_row");
   if (ns && (e = hipMemcpy(c->sub_ids.p, subs, ns * 4, hipMemcpyHostToDevice)) != hipSuccess)
     return c->hip_fail(e, "H2D subs");
+  if ((e = c->sub_rp.ensure(((uint64_t)n_slots + 1) * 16)) != hipSuccess) return c->hip_fail(e, "sub_rp");
+  if ((e = launch_sub_pairs(c->sub_row.as<uint64_t>(), n_slots, c->sub_rp.as<uint4>(), c->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+    return c->hip_fail(e, "sub pairs");
   c->n_fid_slots = n_slots;
   return EGM_OK;
 }
@@ -1178,7 +1182,7 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   if ((e = c->f_dpos.ensure((nids + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_dpos");
   if ((e = c->f_tiles.ensure((scan_tiles((uint32_t)nids) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_tiles");
   if ((e = c->f_ovf.ensure(16)) != hipSuccess) return c->hip_fail(e, "f_ovf");
-  SubTable st{c->sub_row.as<uint64_t>(), c->sub_ids.as<uint32_t>(), c->n_fid_slots};
+  SubTable st{c->sub_row.as<uint64_t>(), c->sub_ids.as<uint32_t>(), c->n_fid_slots, c->sub_rp.as<uint4>()};
   hipEvent_t evp[2] = {nullptr, nullptr};
   if (c->timing) {
     evp[0] = c->take_event();

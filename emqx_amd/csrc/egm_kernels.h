@@ -131,7 +131,9 @@ struct SubTable {
   const uint64_t* row;            // [n_fid_slots + 1] indexed by filter id
   const uint32_t* subs;           // subscriber ids; bit 31 set = shared group id
   uint32_t n_fid_slots;
+  const uint4* rp;                // [n_fid_slots] {row start lo, hi, count, 0} (launch_sub_pairs)
 };
+hipError_t launch_sub_pairs(const uint64_t* row, uint32_t n_slots, uint4* rp, hipStream_t s);
 hipError_t launch_fanout(const SubTable& st, const uint64_t* match_row, const uint32_t* match_ids,
                          uint32_t n, uint64_t nids, uint64_t* deliv_row, uint32_t* deliv_fid,
                          uint32_t* deliv_sub, uint64_t deliv_cap, uint32_t* dcount, uint64_t* dsrc,

@@ -1446,20 +1446,45 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
 // match entries, whose deliveries are contiguous in the output (the scan), and
 // its lanes write them in order — coalesced stores, and a 2 000-subscriber
 // filter is spread over 64 lanes instead of looping in one.
+// One aligned 16-B record per filter {row start lo, hi, subscriber count, 0}
+// (k_sub_pairs, at egm_subs_build): a matched id costs one line request
+// instead of two 8-B row-pointer reads; four ids per thread in flight.
+__global__ __launch_bounds__(256) void k_sub_pairs(const uint64_t* __restrict__ row, uint32_t n_slots,
+                                                   uint4* __restrict__ rp) {
+  const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+  if (f < n_slots) {
+    const uint64_t r0 = row[f], r1 = row[f + 1];
+    rp[f] = make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)(r1 - r0), 0u);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_fan_count(const uint32_t* __restrict__ mids, uint64_t nids,
                                                    SubTable st, uint32_t* __restrict__ dc,
                                                    uint64_t* __restrict__ ds0) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nids;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t f = mids[i];
-    uint64_t r0 = 0, r1 = 0;
-    if (f < st.n_fid_slots) {
-      r0 = st.row[f];
-      r1 = st.row[f + 1];
+  constexpr uint32_t U = 4;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nids; i0 += stride * U) {
+    uint32_t f[U];
+    uint4 r[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) f[u] = mids[min(i0 + u * stride, nids - 1)];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) r[u] = st.rp[f[u] < st.n_fid_slots ? f[u] : 0u];   // unconditional
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint64_t i = i0 + u * stride;
+      if (i < nids) {
+        const bool ok = f[u] < st.n_fid_slots;
+        dc[i] = ok ? r[u].z : 0u;
+        ds0[i] = ok ? ((uint64_t)r[u].y << 32 | r[u].x) : 0ull;   // the fill reads this coalesced
+      }
     }
-    dc[i] = (uint32_t)(r1 - r0);
-    ds0[i] = r0;   // the fill reads this coalesced instead of re-probing the row table
   }
+}
+
+hipError_t launch_sub_pairs(const uint64_t* row, uint32_t n_slots, uint4* rp, hipStream_t s) {
+  if (n_slots) hipLaunchKernelGGL(k_sub_pairs, dim3((n_slots + 255) / 256), dim3(256), 0, s, row, n_slots, rp);
+  return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void k_fan_rows(const uint64_t* __restrict__ mrow, uint32_t n,
