@@ -66,6 +66,7 @@ for step in "$@"; do
       run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off ;;
     host) run host 600 python tools/bench_host.py ;;
     s2) run s2 400 python $R/bench.py --steps 20 --warmup 3 --streams 2 --cpu-baseline off --host-e2e off --x-orders "a86,0" ;;
+    cap128) EGM_FIX_CAP=128 run cap128 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86/128,a86/96,a86/128" ;;
     orders) run orders 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86,0,a86/128,a86" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     ab_*)   # A/B variant built by tools/build_variant.py: C2 bench under rocprof stats
