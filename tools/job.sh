@@ -18,6 +18,7 @@
 #   s2         the C2 bench with two streams (consecutive batches overlap), then sorted / input order
 #   orders     the C2 bench, then the walk-order A/B (sort key shapes) in the same process
 #   smoke      __graft_entry__.smoke()
+#   c4m, c4m_V C4's shape at 10M filters (match + fan-out), default library / variant V
 #   ab_V       the C2 bench on variant V (emqx_amd/libemqx_gpu_match_V.so, tools/build_variant.py)
 # An ordinary failure (exit 1..5) moves on; a fault, abort or timeout ends the job.
 set -u
@@ -69,6 +70,10 @@ for step in "$@"; do
     cap128) EGM_FIX_CAP=128 run cap128 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86/128,a86/96,a86/128" ;;
     orders) run orders 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86,0,a86/128,a86" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    c4m) run c4m 400 python $R/bench.py --config c4 --filters 10000000 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
+    c4m_*)  # the same on variant V (tools/build_variant.py)
+      v=${step#c4m_}
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 400 python $R/bench.py --config c4 --filters 10000000 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
     ab_*)   # A/B variant built by tools/build_variant.py: C2 bench under rocprof stats
       v=${step#ab_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$v" -o run --output-format csv -- $B --steps 10 --warmup 2 --cpu-baseline off --host-e2e off ;;
