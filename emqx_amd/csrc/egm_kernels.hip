@@ -8,7 +8,7 @@
 //   emqx_broker:dispatch/2        apps/emqx/src/emqx_broker.erl:283-324  -> k_fanout_*
 //
 // The walk is an NFA frontier expansion over the word-level trie (egm_common.h):
-// topics sorted into a locality order (k_sort_key + a radix sort), then one
+// topics sorted into a locality order (a key from k_tokenise + a radix sort), then one
 // wavefront per chunk of 64 of them, walking from an LDS work stack (pop up to
 // 64 items, issue their reads together, compact children and emits back with
 // __ballot / mbcnt), staging emits per topic and flushing them as pieces;
