@@ -15,7 +15,11 @@
  *                      emqx_router:match_routes/1 — emqx_router.erl:129-141 — for a
  *                      list of publish topics; returns [[FilterId]])
  *   submit/3, wait/2 -> egm_match_submit / egm_match_wait (the batcher's pipeline:
- *                      submit returns a ticket at once, wait blocks for its rows)
+ *                      submit returns a ticket at once, wait blocks for its rows).
+ *                      The ticket is a resource: collected unwaited (its waiter
+ *                      died), its destructor calls egm_match_cancel, so a dead
+ *                      waiter never keeps a pipeline slot busy.
+ *   cancel/2        -> egm_match_cancel
  *   subs_build/2    -> egm_subs_build      (filter id -> subscriber ids: the
  *                      emqx_subscriber bag flattened, emqx_broker.erl:116-162)
  *   publish_batch/2 -> egm_match_batch (routes mode) + egm_fanout_batch: the
@@ -43,6 +47,14 @@ typedef struct {
 } egm_res_t;
 
 static ErlNifResourceType* EGM_RES;
+static ErlNifResourceType* EGM_TICKET;
+
+/* A submitted batch: keeps its context alive until it is waited or cancelled. */
+typedef struct {
+  egm_res_t* owner;   /* enif_keep_resource'd */
+  uint64_t ticket;
+  int live;           /* not yet waited or cancelled */
+} egm_ticket_t;
 static ERL_NIF_TERM ATOM_OK, ATOM_ERROR;
 
 static void egm_res_dtor(ErlNifEnv* env, void* obj) {
@@ -52,14 +64,25 @@ static void egm_res_dtor(ErlNifEnv* env, void* obj) {
   r->ctx = NULL;
 }
 
+static void egm_ticket_dtor(ErlNifEnv* env, void* obj) {
+  (void)env;
+  egm_ticket_t* t = (egm_ticket_t*)obj;
+  if (t->live && t->owner && t->owner->ctx) egm_match_cancel(t->owner->ctx, t->ticket);
+  t->live = 0;
+  if (t->owner) enif_release_resource(t->owner);
+  t->owner = NULL;
+}
+
 static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   (void)priv;
   (void)info;
   EGM_RES = enif_open_resource_type(env, NULL, "emqx_gpu_match_ctx", egm_res_dtor,
                                     ERL_NIF_RT_CREATE | ERL_NIF_RT_TAKEOVER, NULL);
+  EGM_TICKET = enif_open_resource_type(env, NULL, "emqx_gpu_match_ticket", egm_ticket_dtor,
+                                       ERL_NIF_RT_CREATE | ERL_NIF_RT_TAKEOVER, NULL);
   ATOM_OK = enif_make_atom(env, "ok");
   ATOM_ERROR = enif_make_atom(env, "error");
-  return EGM_RES ? 0 : -1;
+  return (EGM_RES && EGM_TICKET) ? 0 : -1;
 }
 
 static ERL_NIF_TERM error_tuple(ErlNifEnv* env, egm_ctx* ctx, int rc) {
@@ -215,7 +238,7 @@ static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM
 }
 
 /* submit(Ctx, [Topic], Mode) -> {ok, Ticket} | {error, _}: the topics are
-   staged in pinned memory before it returns. */
+   staged in pinned memory before it returns; Ticket is a resource. */
 static ERL_NIF_TERM nif_submit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   egm_res_t* r;
   int mode;
@@ -229,17 +252,28 @@ static ERL_NIF_TERM nif_submit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   free(blob);
   free(off);
   if (rc) return error_tuple(env, r->ctx, rc);
-  return enif_make_tuple2(env, ATOM_OK, enif_make_uint64(env, ticket));
+  egm_ticket_t* t = (egm_ticket_t*)enif_alloc_resource(EGM_TICKET, sizeof(egm_ticket_t));
+  enif_keep_resource(r);
+  t->owner = r;
+  t->ticket = ticket;
+  t->live = 1;
+  ERL_NIF_TERM term = enif_make_resource(env, t);
+  enif_release_resource(t);
+  return enif_make_tuple2(env, ATOM_OK, term);
 }
 
-/* wait(Ctx, Ticket) -> {ok, [[Id]]} | {error, _} */
+static int get_ticket(ErlNifEnv* env, ERL_NIF_TERM term, egm_res_t* r, egm_ticket_t** t) {
+  return enif_get_resource(env, term, EGM_TICKET, (void**)t) && (*t)->live && (*t)->owner == r;
+}
+
+/* wait(Ctx, Ticket) -> {ok, [[Id]]} | {error, _} (a ticket is waited once) */
 static ERL_NIF_TERM nif_wait(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   egm_res_t* r;
-  ErlNifUInt64 ticket;
-  if (argc != 2 || !get_ctx(env, argv[0], &r) || !enif_get_uint64(env, argv[1], &ticket))
-    return enif_make_badarg(env);
+  egm_ticket_t* t;
+  if (argc != 2 || !get_ctx(env, argv[0], &r) || !get_ticket(env, argv[1], r, &t)) return enif_make_badarg(env);
+  t->live = 0;   /* from here the library owns the outcome: no cancel in the destructor */
   egm_result* res = NULL;
-  int rc = egm_match_wait(r->ctx, ticket, &res);
+  int rc = egm_match_wait(r->ctx, t->ticket, &res);
   if (rc) {
     if (res) egm_result_free(res);
     return error_tuple(env, r->ctx, rc);
@@ -247,6 +281,16 @@ static ERL_NIF_TERM nif_wait(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   ERL_NIF_TERM rows = rows_term(env, res);
   egm_result_free(res);
   return enif_make_tuple2(env, ATOM_OK, rows);
+}
+
+/* cancel(Ctx, Ticket) -> ok | {error, _}: give the batch up without its rows */
+static ERL_NIF_TERM nif_cancel(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  egm_res_t* r;
+  egm_ticket_t* t;
+  if (argc != 2 || !get_ctx(env, argv[0], &r) || !get_ticket(env, argv[1], r, &t)) return enif_make_badarg(env);
+  t->live = 0;
+  int rc = egm_match_cancel(r->ctx, t->ticket);
+  return rc ? error_tuple(env, r->ctx, rc) : ATOM_OK;
 }
 
 /* subs_build(Ctx, [[Sub]]) -> ok | {error, _}: list position = filter id; a
@@ -334,6 +378,7 @@ static ErlNifFunc nif_funcs[] = {
     {"match_batch", 3, nif_match_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"submit", 3, nif_submit, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"wait", 2, nif_wait, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"cancel", 2, nif_cancel, 0},
     {"subs_build", 2, nif_subs_build, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"publish_batch", 2, nif_publish_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
 };

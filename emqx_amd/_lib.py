@@ -29,6 +29,13 @@ EGM_TF_DOLLAR = 2
 EGM_TF_HEAVY = 4
 EGM_TF_ERROR = 8
 
+EGM_DEBUG_FORCE_HEAVY = 1
+EGM_DEBUG_FAIL_COMMIT = 2
+EGM_DEBUG_INPUT_ORDER = 4
+EGM_DEBUG_FORCE_GUARD = 8
+EGM_GUARD_STACK = 4
+EGM_GUARD_LOOP = 8
+
 NONE_ID = 0xFFFFFFFF
 GROUP_BIT = 0x80000000
 
@@ -89,8 +96,10 @@ SIGNATURES = {
     "egm_match_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_int, C.POINTER(C.POINTER(egm_result))]),
     "egm_match_submit": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_int, _u64p]),
     "egm_match_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(C.POINTER(egm_result))]),
+    "egm_match_cancel": (C.c_int, [_P, C.c_uint64]),
     "egm_match_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, _P, _P, C.c_uint64, _P]),
     "egm_last_stats": (C.c_int, [_P, _u64p, _u64p, _u32p, _u32p, _u32p]),
+    "egm_last_guard": (C.c_int, [_P, _u32p]),
     "egm_last_walk_counters": (C.c_int, [_P, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "egm_set_timing": (C.c_int, [_P, C.c_int]),
     "egm_set_debug": (C.c_int, [_P, C.c_uint32]),

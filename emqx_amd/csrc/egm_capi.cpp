@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -86,9 +87,12 @@ struct PinBuf {
 // pinned input copy, device input and output, and the pinned result the
 // caller reads until egm_result_free.
 struct PipeSlot {
-  bool busy = false;     // submitted, not yet waited for
-  bool waiting = false;  // a thread is in egm_match_wait for it
-  bool held = false;     // its result is with the caller
+  bool busy = false;       // submitted, not yet waited for
+  bool waiting = false;    // a thread is in egm_match_wait for it
+  bool held = false;       // its result is with the caller
+  bool sync = false;       // taken by egm_match_batch (not a ticket of egm_match_submit)
+  bool abandoned = false;  // egm_match_cancel: reclaimed once its batch has finished
+  uint32_t gen = 0;        // bumped at every submit: part of the ticket, so a stale ticket is refused
   uint32_t n = 0;
   int mode = 0;
   uint64_t bytes = 0, maxlen = 0, cap = 0;
@@ -102,7 +106,14 @@ struct PipeSlot {
     if (ev_out) hipEventDestroy(ev_out);
   }
 };
-constexpr size_t PIPE_MAX_SLOTS = 8;
+constexpr size_t PIPE_MAX_SLOTS = 8;     // tickets of egm_match_submit busy or held at once
+constexpr size_t PIPE_HARD_SLOTS = 64;   // all slots, egm_match_batch's included (then it waits)
+constexpr int PIPE_BATCH_WAIT_MS = 30000;   // egm_match_batch's longest wait for a slot
+
+// ticket = generation << 16 | (slot index + 1)
+inline uint64_t make_ticket(size_t k, uint32_t gen) { return ((uint64_t)gen << 16) | (uint64_t)(k + 1); }
+inline size_t ticket_slot(uint64_t t) { return (size_t)(t & 0xFFFFu) - 1; }
+inline uint32_t ticket_gen(uint64_t t) { return (uint32_t)(t >> 16); }
 
 // One match workspace: the per-batch scratch of launch_match.
 struct MatchWs {
@@ -209,6 +220,7 @@ struct egm_ctx {
   }
   // host pipeline (egm_match_submit / egm_match_wait)
   std::vector<std::unique_ptr<PipeSlot>> pipe;
+  std::condition_variable_any pipe_cv;   // a slot was freed (wait done, result freed, ticket cancelled)
   hipStream_t copy_stream = nullptr;   // pipeline host->device copies
   hipStream_t d2h_stream = nullptr;    // pipeline device->host copies (PCIe is full duplex)
   // last fan-out (egm_last_fanout)
@@ -903,6 +915,18 @@ int egm_last_stats(egm_ctx* c, uint64_t* n_ids, uint64_t* visited, uint32_t* n_d
   if (n_def) *n_def = c->last.n_deferred;
   if (overflow) *overflow = c->last.overflow;
   if (n_error) *n_error = c->last.errors;
+  if (c->last.guard)   // a kernel invariant failed: the batch's rows are not valid (never a capacity problem)
+    return c->fail(EGM_E_DEVICE, "walk guard tripped (bits " + std::to_string(c->last.guard) +
+                                     "): kernel invariant failed, batch not matched");
+  return EGM_OK;
+}
+
+int egm_last_guard(egm_ctx* c, uint32_t* guard) {
+  if (!c || !guard) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  int r = sync_last(c);
+  if (r) return r;
+  *guard = c->last.guard;
   return EGM_OK;
 }
 
@@ -988,35 +1012,73 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   return EGM_OK;
 }
 
-int egm_match_submit(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, int mode, uint64_t* ticket) {
-  if (!c || !ticket || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES)) return EGM_E_INVAL;
-  if (n && (!off || !valid_offsets(off, n) || (!blob && off[n] > off[0]))) return EGM_E_INVAL;
-  std::lock_guard<std::recursive_mutex> g(c->mu);
+// A free pipeline slot for a batch (index into c->pipe), or -1.  Slots whose
+// ticket was cancelled are reclaimed here once their batch has finished.
+static long pipe_free_slot(egm_ctx* c) {
+  for (size_t k = 0; k < c->pipe.size(); ++k) {
+    PipeSlot& S = *c->pipe[k];
+    if (S.busy && S.abandoned && !S.waiting && hipEventQuery(S.ev_done) == hipSuccess) {
+      S.busy = S.abandoned = false;   // a cancelled ticket whose batch is done
+    }
+    if (!S.busy && !S.held) return (long)k;
+  }
+  return -1;
+}
+
+static int pipe_new_slot(egm_ctx* c, long* k) {
+  c->pipe.emplace_back(new PipeSlot());
+  PipeSlot& N = *c->pipe.back();
+  if (hipEventCreateWithFlags(&N.ev_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&N.ev_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&N.ev_out, hipEventDisableTiming) != hipSuccess) {
+    c->pipe.pop_back();
+    return c->fail(EGM_E_DEVICE, "pipe events");
+  }
+  *k = (long)c->pipe.size() - 1;
+  return EGM_OK;
+}
+
+// Submit with the context lock held once by the caller (g).  A ticket of
+// egm_match_submit (sync = false) is refused when PIPE_MAX_SLOTS tickets are
+// busy or unreleased; egm_match_batch (sync = true) takes any free slot, adds
+// slots up to PIPE_HARD_SLOTS and beyond that waits for one to be freed, so
+// concurrent synchronous callers queue instead of failing.
+static int submit_locked(egm_ctx* c, std::unique_lock<std::recursive_mutex>& g, const uint8_t* blob,
+                         const uint32_t* off, uint32_t n, int mode, bool sync, uint64_t* ticket) {
   if (set_device(c)) return EGM_E_DEVICE;
   hipError_t e;
   if (!c->copy_stream && (e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking)) != hipSuccess)
     return c->hip_fail(e, "copy stream");
   if (!c->d2h_stream && (e = hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking)) != hipSuccess)
     return c->hip_fail(e, "d2h stream");
-  size_t k = 0;
-  while (k < c->pipe.size() && (c->pipe[k]->busy || c->pipe[k]->held)) ++k;
-  if (k == c->pipe.size()) {
-    if (k == PIPE_MAX_SLOTS) return c->fail(EGM_E_STATE, "pipeline full: wait for a ticket or free its result");
-    c->pipe.emplace_back(new PipeSlot());
-    PipeSlot& N = *c->pipe.back();
-    if (hipEventCreateWithFlags(&N.ev_in, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&N.ev_done, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&N.ev_out, hipEventDisableTiming) != hipSuccess)
-      return c->fail(EGM_E_DEVICE, "pipe events");
+  if (!sync) {
+    size_t tickets = 0;
+    for (auto& p : c->pipe) tickets += (!p->sync && (p->busy || p->held)) ? 1u : 0u;
+    if (tickets >= PIPE_MAX_SLOTS) return c->fail(EGM_E_STATE, "pipeline full: wait for a ticket or free its result");
   }
-  PipeSlot& S = *c->pipe[k];
+  long k = pipe_free_slot(c);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(PIPE_BATCH_WAIT_MS);
+  while (k < 0) {
+    if (c->pipe.size() < PIPE_HARD_SLOTS) {
+      const int r = pipe_new_slot(c, &k);
+      if (r) return r;
+      break;
+    }
+    if (!sync) return c->fail(EGM_E_STATE, "pipeline full: wait for a ticket or free its result");
+    // every slot busy: wait for a release (polling too, for cancelled tickets)
+    if (std::chrono::steady_clock::now() > deadline)
+      return c->fail(EGM_E_STATE, "no pipeline slot freed within 30 s (results not released?)");
+    c->pipe_cv.wait_for(g, std::chrono::milliseconds(2));
+    k = pipe_free_slot(c);
+  }
+  PipeSlot& S = *c->pipe[(size_t)k];
   // stage the caller's (borrowed) batch in pinned memory, offsets rebased to 0
   const uint32_t base0 = n ? off[0] : 0;
   const uint64_t bytes = n ? (uint64_t)off[n] - base0 : 0;
   const uint64_t o_off = (bytes + 15) & ~15ull, in_sz = o_off + ((uint64_t)n + 1) * 4;
-  if ((e = S.h_in.ensure(in_sz)) != hipSuccess) return c->hip_fail(e, "pipe pinned input");
   // the previous use of this slot's staging must be finished (its H2D)
   if ((e = hipEventSynchronize(S.ev_in)) != hipSuccess) return c->hip_fail(e, "pipe input reuse");
+  if ((e = S.h_in.ensure(in_sz)) != hipSuccess) return c->hip_fail(e, "pipe pinned input");
   uint8_t* hin = (uint8_t*)S.h_in.p;
   if (bytes) par_copy(hin, blob + base0, bytes);
   uint32_t* hoff = (uint32_t*)(hin + o_off);
@@ -1038,8 +1100,28 @@ int egm_match_submit(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint3
   int r = pipe_launch(c, S);
   if (r) return r;
   S.busy = true;
-  *ticket = (uint64_t)k + 1;
+  S.sync = sync;
+  S.abandoned = false;
+  S.gen = (S.gen + 1) & 0x7FFFFFFFu;
+  if (S.gen == 0) S.gen = 1;
+  *ticket = make_ticket((size_t)k, S.gen);
   return EGM_OK;
+}
+
+int egm_match_submit(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, int mode, uint64_t* ticket) {
+  if (!c || !ticket || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES)) return EGM_E_INVAL;
+  if (n && (!off || !valid_offsets(off, n) || (!blob && off[n] > off[0]))) return EGM_E_INVAL;
+  std::unique_lock<std::recursive_mutex> g(c->mu);
+  return submit_locked(c, g, blob, off, n, mode, false, ticket);
+}
+
+// The slot of a live ticket (submitted, not yet waited for or cancelled), or null.
+static PipeSlot* ticket_slot_of(egm_ctx* c, uint64_t ticket) {
+  const size_t k = ticket_slot(ticket);
+  if (ticket == 0 || k >= c->pipe.size()) return nullptr;
+  PipeSlot& S = *c->pipe[k];
+  if (!S.busy || S.waiting || S.abandoned || S.gen != ticket_gen(ticket)) return nullptr;
+  return &S;
 }
 
 // The device syncs happen without the context lock, so another thread can
@@ -1048,14 +1130,15 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   if (!c || !out || ticket == 0) return EGM_E_INVAL;
   *out = nullptr;
   std::unique_lock<std::recursive_mutex> g(c->mu);
-  if (ticket > c->pipe.size() || !c->pipe[ticket - 1]->busy || c->pipe[ticket - 1]->waiting)
-    return c->fail(EGM_E_STATE, "unknown ticket");
+  PipeSlot* sp = ticket_slot_of(c, ticket);
+  if (!sp) return c->fail(EGM_E_STATE, "unknown, stale or already waited ticket");
   if (set_device(c)) return EGM_E_DEVICE;
-  PipeSlot& S = *c->pipe[ticket - 1];
+  PipeSlot& S = *sp;
   S.waiting = true;
   auto done = [&](int rc) {   // the slot is free again (its result, if any, held by the caller)
     if (!g.owns_lock()) g.lock();
     S.busy = S.waiting = false;
+    c->pipe_cv.notify_all();
     return rc;
   };
   hipError_t e;
@@ -1066,8 +1149,13 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
     g.lock();
     if (e != hipSuccess) return done(c->hip_fail(e, "pipe wait"));
     st = *(const MatchStats*)S.h_stats.p;
+    if (st.guard) {   // a kernel invariant failed: a bug, never a capacity problem (no retry)
+      c->last = st;
+      return done(c->fail(EGM_E_DEVICE, "walk guard tripped (bits " + std::to_string(st.guard) +
+                                             "): kernel invariant failed, batch not matched"));
+    }
     if (!st.overflow) break;
-    if (attempt == 2 || (st.overflow & ~3u)) return done(c->fail(EGM_E_NOMEM, "ids capacity"));
+    if (attempt == 2) return done(c->fail(EGM_E_NOMEM, "ids capacity"));
     // the exact total is known even on overflow: rerun the staged batch once with room for it
     S.cap = st.total_ids + st.total_ids / 8 + 1024;
     const int r = pipe_launch(c, S);
@@ -1113,7 +1201,7 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   res->n_heavy = heavy;
   hdr->magic = RES_PIPE;
   hdr->owner = c;
-  hdr->slot = ticket - 1;
+  hdr->slot = ticket_slot(ticket);
   S.held = true;
   done(EGM_OK);
   *out = res;
@@ -1124,16 +1212,34 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   return EGM_OK;
 }
 
-// One synchronous batch: the pipeline with a single ticket.  Host buffers are
-// staged in pinned memory and the result is read in place from pinned memory
-// (released by egm_result_free).
+// Give up a ticket without its result: the slot is reclaimed as soon as its
+// batch has finished (no wait here).  For a waiter that will never call
+// egm_match_wait (e.g. the NIF ticket resource collected unwaited).
+int egm_match_cancel(egm_ctx* c, uint64_t ticket) {
+  if (!c || ticket == 0) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  PipeSlot* sp = ticket_slot_of(c, ticket);
+  if (!sp) return c->fail(EGM_E_STATE, "unknown, stale or already waited ticket");
+  sp->abandoned = true;
+  c->pipe_cv.notify_all();
+  return EGM_OK;
+}
+
+// One synchronous batch: submit + wait on a pipeline slot of its own.  Host
+// buffers are staged in pinned memory and the result is read in place from
+// pinned memory (released by egm_result_free).  Concurrent callers never get
+// "pipeline full": they take extra slots, then wait for one to be released.
 int egm_match_batch(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, int mode,
                     egm_result** out) {
-  if (!c || !out) return EGM_E_INVAL;
+  if (!c || !out || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES)) return EGM_E_INVAL;
   *out = nullptr;
+  if (n && (!off || !valid_offsets(off, n) || (!blob && off[n] > off[0]))) return EGM_E_INVAL;
   uint64_t t = 0;
-  int r = egm_match_submit(c, blob, off, n, mode, &t);
-  if (r) return r;
+  {
+    std::unique_lock<std::recursive_mutex> g(c->mu);
+    const int r = submit_locked(c, g, blob, off, n, mode, true, &t);
+    if (r) return r;
+  }
   return egm_match_wait(c, t, out);
 }
 
@@ -1141,6 +1247,7 @@ int egm_match_batch(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32
 static void pipe_release(egm_ctx* c, uint64_t slot) {
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (slot < c->pipe.size()) c->pipe[slot]->held = false;
+  c->pipe_cv.notify_all();
 }
 
 // ---------------------------------------------------------------- fan-out --

@@ -26,9 +26,11 @@ struct MatchStats {               // device-side counters, zeroed per batch
   unsigned long long total_ids;   // matched ids in the batch (= row_ptr[n])
   unsigned int n_deferred;        // chunks handed to the heavy kernel
   unsigned int heavy_next;        // heavy work counter
-  unsigned int overflow;          // bit 0: ids_tmp/pieces full, bit 1: output ids full, bit 2: heavy stack,
-                                  // bit 3: a loop guard fired (a bug: reported, never a hung GPU)
+  unsigned int overflow;          // capacity only: bit 0 ids_tmp/pieces full, bit 1 output ids full (rerun bigger)
   unsigned int errors;            // topics the heavy kernel could not walk (never for legal topics)
+  unsigned int guard;             // GUARD_* bits: a kernel invariant failed (a bug, never a capacity
+                                  // problem; reported instead of hanging the GPU, rows not assembled)
+  unsigned int pad_;
   unsigned long long iters;       // walk iterations (instrumentation)
   unsigned long long popped;      // items popped by the walk (lane occupancy = popped / (iters * 64))
   unsigned long long bounded;     // walk iterations whose pop was cut by the stack-room bound (DFS regime)
@@ -87,8 +89,12 @@ struct WalkOrderOut {                        // what k_tokenise writes for the s
   uint32_t shape;
 };
 
+constexpr uint32_t GUARD_STACK = 4u;         // a push would have overrun a work stack (the pop bound makes it impossible)
+constexpr uint32_t GUARD_LOOP = 8u;          // a walk loop ran past its iteration guard
+
 constexpr uint32_t DEBUG_FORCE_HEAVY = 1u;   // every chunk goes to k_heavy (test coverage)
 constexpr uint32_t DEBUG_INPUT_ORDER = 4u;   // walk in input order (no locality sort)
+constexpr uint32_t DEBUG_FORCE_GUARD = 8u;   // loop guards of 2 iterations: trips the guard (error-path test)
 
 // walk-order key: total bits of a key shape; radix sort scratch bytes for a
 // batch of n topics (hipcub)

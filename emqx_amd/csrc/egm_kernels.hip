@@ -467,9 +467,14 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #ifndef EGM_WALK_WORDS
 #define EGM_WALK_WORDS 448   // staged topic word ids per wave (a chunk's topics, [topic][level])
 #endif
+#ifndef EGM_PROBE_SLOTS
+#define EGM_PROBE_SLOTS 2    // edge slots a literal probe reads up front (2 x 16-B loads each); the rest on a miss
+#endif
 constexpr uint32_t WALK_STACK = EGM_WALK_STACK;
 constexpr uint32_t WALK_STAGE = EGM_WALK_STAGE;
 constexpr uint32_t WALK_WORDS = EGM_WALK_WORDS;
+constexpr int PROBE_SLOTS = EGM_PROBE_SLOTS;
+static_assert(PROBE_SLOTS == 1 || PROBE_SLOTS == 2, "probe width");
 // The pop bound (below) keeps room >= dmax after every iteration and a refill
 // fills the stack to at most 64 items, so the stack cannot overflow while
 // 64 + dmax <= WALK_STACK; the words of one topic must fit the word stage.
@@ -598,6 +603,9 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
   for (uint32_t q = lane; q < nstage; q += 64) {
     const uint32_t i = L.stage_rank[q], tt = L.stage_t[i], f = L.fcnt[tt], cb = L.cnt[tt];
     const uint32_t k = cb + (q - (f >> 16));
+#ifdef EGM_AB_NO_ID_STORES   // measurement only (tools/build_variant.py): the walk without its id stores
+    if (L.stage_fid[i] != 0x7FFFFFF1u) continue;
+#endif
     if (k < cap) w.ids_fix[(uint64_t)(t0 + tt) * cap + k] = L.stage_fid[i];
     else if (ok) w.ids_tmp[base + (f & 0xFFFFu) + (k - max(cb, cap))] = L.stage_fid[i];
   }
@@ -652,8 +660,13 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* words
   const uint8_t* bp = (const uint8_t*)(tab.edges + (size_t)(p.lit ? bkt : 0u) * EDGE_BUCKET);
   p.l0 = ld16(bp);
   p.h0 = ld16(bp + 16);
-  p.l1 = ld16(bp + 32);
-  p.h1 = ld16(bp + 48);
+  if (PROBE_SLOTS == 2) {
+    p.l1 = ld16(bp + 32);
+    p.h1 = ld16(bp + 48);
+  } else {   // slot 1 unread: a key that is not in slot 0 goes to the slot search from slot 1
+    p.l1 = make_uint4(TOMB, WID_NONE, 0, 0);
+    p.h1 = make_uint4(0, 0, 0, 0);
+  }
   // the next level's word (clamped; used only if level + 1 < D)
   const uint32_t nl = min((meta & LEVEL_MAX) + 1, p.D - 1);
   p.nw = words ? words[nl] : wid[p.act ? gbase + nl : 0u];
@@ -695,9 +708,9 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend
   uint32_t hx = (p.h0.x & ~s1) | (p.h1.x & s1), hy = (p.h0.y & ~s1) | (p.h1.y & s1);
   uint32_t hz = (p.h0.z & ~s1) | (p.h1.z & s1);
   bool found = p.lit && (m0 || m1);
-  if (p.lit && !m0 && !z0 && !m1 && !z1) {   // both first slots hold other keys: keep probing (rare)
+  if (p.lit && !m0 && !z0 && !m1 && !z1) {   // the slots read hold other keys: keep probing
     uint4 lo, hi;
-    found = edge_probe_from(tab, edge_bucket(node, p.it.w, tab.edge_mask), 2, node, p.it.w, &lo, &hi);
+    found = edge_probe_from(tab, edge_bucket(node, p.it.w, tab.edge_mask), PROBE_SLOTS, node, p.it.w, &lo, &hi);
     cz = lo.z;
     cw = lo.w;
     hx = hi.x;
@@ -777,6 +790,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
   uint32_t created = 0;
   unsigned long long iters = 0, popped = 0, bounded = 0, lit_probes = 0, plus_reads = 0;
   Slab sid{0, 0}, spc{0, 0};
+  const uint32_t guard_lim = (w.debug & DEBUG_FORCE_GUARD) ? 2u : (1u << EGM_GUARD_BITS);
   // sorted batch: the record of the chunk's j-th topic in walk order, loaded
   // one chunk ahead (a grid stride: the wave's next chunk is c + gridDim.x)
   const uint64_t* ord = w.order;
@@ -840,8 +854,8 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
       uint32_t next = sub, sp = 0;
       uint32_t guard = 0;   // every loop of the kernel is bounded: a bug reports, it never hangs the GPU
       for (;;) {
-        if (++guard > (1u << EGM_GUARD_BITS)) {
-          if (lane == 0) atomicOr(&w.stats->overflow, 8u);
+        if (++guard > guard_lim) {
+          if (lane == 0) atomicOr(&w.stats->guard, GUARD_LOOP);
           break;
         }
         // ---- admit new topics while the stack is short: their root '#'
@@ -921,7 +935,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
         const uint32_t m0 = popc(c0b), nc = m0 + popc(c1b);
         if (sp + nc > WALK_STACK) {   // guard only: the pop bound keeps sp + pushes <= WALK_STACK
-          if (lane == 0) atomicOr(&w.stats->overflow, 4u);
+          if (lane == 0) atomicOr(&w.stats->guard, GUARD_STACK);
           break;
         }
         if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
@@ -1013,6 +1027,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
   const uint32_t total = w.stats->n_deferred * (uint32_t)WALK_CHUNK;
   uint4* stk = w.heavy_stack + (uint64_t)blockIdx.x * w.heavy_cap;
   const uint32_t cap = w.heavy_cap;
+  const uint32_t guard_lim = (w.debug & DEBUG_FORCE_GUARD) ? 2u : (1u << EGM_GUARD_BITS);
   unsigned long long created = 0;
   for (;;) {
     uint32_t idx = 0;
@@ -1072,8 +1087,8 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
       heavy_fence();
       uint32_t guard = 0;
       while (sp) {
-        if (++guard > (1u << EGM_GUARD_BITS)) {
-          if (lane == 0) atomicOr(&w.stats->overflow, 8u);
+        if (++guard > guard_lim) {
+          if (lane == 0) atomicOr(&w.stats->guard, GUARD_LOOP);
           break;
         }
         const uint32_t room = cap - sp;
@@ -1094,7 +1109,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
         if (sp + m0 + popc(c1b) > cap) {   // guard only: the pop bound keeps sp + pushes <= cap
           count = 0;
           fits = false;
-          if (lane == 0) atomicOr(&w.stats->overflow, 4u);
+          if (lane == 0) atomicOr(&w.stats->guard, GUARD_STACK);
           break;
         }
         heavy_fence();   // every lane's pop load is done before the pushes overwrite those entries
@@ -1256,7 +1271,7 @@ __device__ __forceinline__ bool compact_checks(const uint64_t* row_ptr, uint32_t
                                                MatchStats* stats) {
   const uint64_t total = row_ptr[n];
   if (blockIdx.x == 0 && threadIdx.x == 0) stats->total_ids = total;
-  if (stats->overflow) return false;
+  if (stats->overflow || stats->guard) return false;   // a guard trip: no rows are assembled
   if (total > ids_cap) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, 2u);
     return false;

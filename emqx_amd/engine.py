@@ -212,13 +212,26 @@ class GpuMatcher:
         self._check(self.lib.egm_match_device(self.ctx, d_blob, blob_bytes, d_off, n, mode, stream or None, d_row,
                                               d_ids, ids_cap, d_flags or None), "egm_match_device")
 
+    def cancel(self, ticket: int):
+        """Give a submitted ticket up without its result (egm_match_cancel)."""
+        self._check(self.lib.egm_match_cancel(self.ctx, ticket), "egm_match_cancel")
+
     def last_stats(self) -> dict:
+        """Counters of the last batch.  `overflow` is capacity only (rerun with
+        a bigger id buffer); a walk guard trip — a kernel invariant failed —
+        raises EgmError(EGM_E_DEVICE) instead (see last_guard)."""
         a, b = C.c_uint64(), C.c_uint64()
         c, d, e = C.c_uint32(), C.c_uint32(), C.c_uint32()
         self._check(self.lib.egm_last_stats(self.ctx, C.byref(a), C.byref(b), C.byref(c), C.byref(d),
                                             C.byref(e)), "egm_last_stats")
         return {"n_ids": a.value, "visited": b.value, "deferred_chunks": c.value, "overflow": d.value,
                 "errors": e.value}
+
+    def last_guard(self) -> int:
+        """Walk guard bits of the last batch (0 = none; EGM_GUARD_STACK / EGM_GUARD_LOOP)."""
+        g = C.c_uint32()
+        self._check(self.lib.egm_last_guard(self.ctx, C.byref(g)), "egm_last_guard")
+        return g.value
 
     def walk_counters(self) -> dict:
         a, b, c, d, e = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()

@@ -5,18 +5,31 @@
 %% The reference looks routes up one message at a time in the publisher's
 %% process (emqx_broker:publish/1 -> emqx_router:match_routes/1,
 %% apps/emqx/src/emqx_broker.erl:200-209).  A GPU batch pays off only for many
-%% topics at once, so publishers call match_routes/1 here: the topic is pushed
-%% into an emqx_batch (apps/emqx/src/emqx_batch.erl: commit on batch_size
-%% items or linger_ms after the first), a commit submits the whole batch to the
-%% GPU pipeline (emqx_gpu_match:submit/3 stages it in pinned memory and
-%% returns a ticket at once), and one waiter process per ticket blocks in
-%% emqx_gpu_match:wait/2 (dirty I/O scheduler) and answers the batch's callers.
-%% Up to `depth` tickets are in flight, so batch k's copy back overlaps batch
-%% k+1's match; further commits queue here.  Any NIF error is handed to the
-%% callers, which fall back to emqx_router:match_routes/1: semantics never
-%% change.
+%% topics at once, so publishers call match_routes/1 here: the topic joins the
+%% pending batch (committed at batch_size topics or linger_ms after the first,
+%% the policy of apps/emqx/src/emqx_batch.erl:50-81, with an item counter
+%% instead of emqx_batch's length/1 per push), a commit submits the whole batch
+%% to the GPU pipeline (emqx_gpu_match:submit/3 stages it in pinned memory and
+%% returns a ticket at once), and one monitored waiter process per ticket blocks
+%% in emqx_gpu_match:wait/2 (dirty I/O scheduler) and answers the batch's
+%% callers.  Up to `depth` tickets are in flight, so batch k's copy back
+%% overlaps batch k+1's match; further commits queue here.
 %%
-%% Not compiled in this repository's CI (no ERTS in the build image).
+%% Result = emqx_router:match_routes/1 exactly (emqx_router.erl:129-134):
+%% the GPU table mirrors emqx_trie (the wildcard filters that have routes,
+%% kept by emqx_gpu_routes after each route transaction commits), the batch is
+%% matched in TRIE mode (emqx_trie:match/1), and the caller expands
+%% [Topic | Matched] with lookup_routes/1, so the topic's own exact routes are
+%% included just as the reference includes them.
+%%
+%% Semantics never change on failure: a NIF error, a dead or absent server, a
+%% killed waiter or a timeout all end in emqx_router:match_routes/1.  Late
+%% replies are dropped (gen_server:call uses a process alias, OTP >= 24).
+%% A ticket is a NIF resource: if its waiter dies before wait/2, the resource's
+%% destructor cancels it (egm_match_cancel) and the slot is reclaimed.
+%%
+%% Not compiled in this repository's CI (no ERTS in the build image);
+%% emqx_amd/gpu_batch.py mirrors this logic and is tested.
 %%--------------------------------------------------------------------
 -module(emqx_gpu_batch).
 -behaviour(gen_server).
@@ -24,9 +37,17 @@
 -export([start_link/1, match_routes/1, match_routes/2]).
 -export([init/1, handle_call/3, handle_cast/2, handle_info/2, terminate/2]).
 
--define(MODE_ROUTES, 1).
+-define(MODE_TRIE, 0).
 
--record(st, {ctx, batch, depth, inflight = 0, queue = queue:new()}).
+-record(st, {ctx,
+             size,                    %% commit at this many topics
+             linger,                  %% ... or this many ms after the first
+             depth,                   %% tickets in flight
+             items = [],              %% pending [{From, Topic}], newest first
+             n = 0,                   %% length(items), kept instead of recounted
+             timer,                   %% linger timer of the pending batch
+             waiters = #{},           %% MonitorRef -> Items of that ticket
+             queue = queue:new()}).   %% committed batches waiting for a ticket
 
 start_link(Opts) when is_map(Opts) ->
     gen_server:start_link({local, ?MODULE}, ?MODULE, Opts, []).
@@ -35,40 +56,52 @@ start_link(Opts) when is_map(Opts) ->
 match_routes(Topic) -> match_routes(Topic, 5000).
 
 match_routes(Topic, Timeout) when is_binary(Topic) ->
-    case gen_server:call(?MODULE, {match, Topic}, Timeout) of
+    Res = try gen_server:call(?MODULE, {match, Topic}, Timeout)
+          catch exit:_ -> {error, unavailable}   %% noproc, timeout, server down
+          end,
+    case Res of
         {ok, Ids} ->
-            lists:append([emqx_router:lookup_routes(emqx_gpu_match:filter_of(Id)) || Id <- Ids]);
+            Matched = emqx_gpu_match:filters_of(Ids),
+            lists:append([emqx_router:lookup_routes(To) || To <- [Topic | Matched]]);
         {error, _} ->
             emqx_router:match_routes(Topic)
     end.
 
 init(Opts) ->
-    process_flag(trap_exit, true),
-    Server = self(),
-    Batch = emqx_batch:init(#{batch_size => maps:get(batch_size, Opts, 65536),
-                              linger_ms => maps:get(linger_ms, Opts, 1),
-                              commit_fun => fun(Items) -> Server ! {commit, Items} end}),
-    {ok, #st{ctx = emqx_gpu_match:ctx(), batch = Batch, depth = maps:get(depth, Opts, 2)}}.
+    {ok, #st{ctx = emqx_gpu_match:ctx(),
+             size = maps:get(batch_size, Opts, 4096),
+             linger = maps:get(linger_ms, Opts, 1),
+             depth = maps:get(depth, Opts, 2)}}.
 
-handle_call({match, Topic}, From, St = #st{batch = B}) ->
-    {noreply, St#st{batch = emqx_batch:push({From, Topic}, B)}};
+handle_call({match, Topic}, From, St = #st{items = Items, n = N, size = Size, linger = Ms}) ->
+    St1 = St#st{items = [{From, Topic} | Items], n = N + 1},
+    St2 = case N of
+              0 -> St1#st{timer = erlang:send_after(Ms, self(), linger)};
+              _ -> St1
+          end,
+    case N + 1 >= Size of
+        true -> {noreply, commit(St2)};
+        false -> {noreply, St2}
+    end;
 handle_call(_Req, _From, St) ->
     {reply, ignored, St}.
 
 handle_cast(_Msg, St) ->
     {noreply, St}.
 
-handle_info(batch_linger_expired, St = #st{batch = B}) ->
-    {noreply, St#st{batch = emqx_batch:commit(B)}};
-handle_info({commit, Items}, St = #st{inflight = N, depth = D}) when N < D ->
-    {noreply, submit(Items, St)};
-handle_info({commit, Items}, St = #st{queue = Q}) ->
-    {noreply, St#st{queue = queue:in(Items, Q)}};
-handle_info({'EXIT', _Waiter, _Reason}, St = #st{inflight = N, queue = Q}) ->
-    St1 = St#st{inflight = N - 1},
-    case queue:out(Q) of
-        {{value, Items}, Q1} -> {noreply, submit(Items, St1#st{queue = Q1})};
-        {empty, _} -> {noreply, St1}
+handle_info(linger, St = #st{n = 0}) ->
+    {noreply, St#st{timer = undefined}};
+handle_info(linger, St) ->
+    {noreply, commit(St#st{timer = undefined})};
+handle_info({'DOWN', Ref, process, _Pid, Reason}, St = #st{waiters = W}) ->
+    case maps:take(Ref, W) of
+        {Items, W1} ->
+            %% a waiter answers before it exits normally; any other exit leaves
+            %% its callers unanswered: they fall back to the reference
+            Reason =:= normal orelse answer(Items, {error, {waiter_down, Reason}}),
+            {noreply, next(St#st{waiters = W1})};
+        error ->
+            {noreply, St}
     end;
 handle_info(_Info, St) ->
     {noreply, St}.
@@ -76,13 +109,25 @@ handle_info(_Info, St) ->
 terminate(_Reason, _St) ->
     ok.
 
-%% Submit one committed batch and start its waiter.
-submit(Items, St = #st{ctx = Ctx, inflight = N}) ->
+%% The pending batch is committed: submitted now, or queued behind `depth`
+%% tickets in flight.
+commit(St = #st{items = Items, timer = T, queue = Q}) ->
+    _ = T =:= undefined orelse erlang:cancel_timer(T),
+    next(St#st{items = [], n = 0, timer = undefined, queue = queue:in(lists:reverse(Items), Q)}).
+
+next(St = #st{waiters = W, depth = D, queue = Q}) ->
+    case map_size(W) < D andalso queue:out(Q) of
+        {{value, Items}, Q1} -> next(submit(Items, St#st{queue = Q1}));
+        _ -> St
+    end.
+
+%% Submit one committed batch and start its (monitored) waiter.
+submit(Items, St = #st{ctx = Ctx, waiters = W}) ->
     Topics = [T || {_From, T} <- Items],
-    case emqx_gpu_match:submit(Ctx, Topics, ?MODE_ROUTES) of
+    case emqx_gpu_match:submit(Ctx, Topics, ?MODE_TRIE) of
         {ok, Ticket} ->
-            _ = spawn_link(fun() -> answer(Items, emqx_gpu_match:wait(Ctx, Ticket)) end),
-            St#st{inflight = N + 1};
+            {_Pid, Ref} = spawn_monitor(fun() -> answer(Items, emqx_gpu_match:wait(Ctx, Ticket)) end),
+            St#st{waiters = W#{Ref => Items}};
         {error, _} = Err ->
             answer(Items, Err),
             St

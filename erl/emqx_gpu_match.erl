@@ -10,13 +10,16 @@
 %% below fall back to the reference implementation, so semantics never change.
 %%
 %% Not compiled in this repository's CI (no ERTS in the build image); see
-%% INTEGRATION.md for the build line; emqx_gpu_batch is the batching process
-%% that turns per-message publish calls into pipelined GPU batches.
+%% INTEGRATION.md for the build line.  emqx_gpu_batch is the batching process
+%% that turns per-message publish calls into pipelined GPU batches;
+%% emqx_gpu_routes keeps the table equal to emqx_trie after each route
+%% transaction commits (never inside it).
 %%--------------------------------------------------------------------
 -module(emqx_gpu_match).
 
--export([open/1, build/2, apply_delta/3, match_batch/3, submit/3, wait/2, subs_build/2, publish_batch/2]).
--export([init/0, ctx/0, filter_of/1, insert/1, delete/1, match/1, match_routes/1]).
+-export([open/1, build/2, apply_delta/3, match_batch/3, submit/3, wait/2, cancel/2, subs_build/2,
+         publish_batch/2]).
+-export([init/0, ctx/0, filter_of/1, filters_of/1, build/1, sync/2, match/1, match_routes/1]).
 
 -on_load(load_nif/0).
 
@@ -38,6 +41,7 @@ apply_delta(_Ctx, _Inserts, _Deletes) -> erlang:nif_error(nif_not_loaded).
 match_batch(_Ctx, _Topics, _Mode) -> erlang:nif_error(nif_not_loaded).
 submit(_Ctx, _Topics, _Mode) -> erlang:nif_error(nif_not_loaded).
 wait(_Ctx, _Ticket) -> erlang:nif_error(nif_not_loaded).
+cancel(_Ctx, _Ticket) -> erlang:nif_error(nif_not_loaded).
 subs_build(_Ctx, _SubsByFilterId) -> erlang:nif_error(nif_not_loaded).
 publish_batch(_Ctx, _Topics) -> erlang:nif_error(nif_not_loaded).
 
@@ -54,43 +58,52 @@ init() ->
 
 ctx() -> persistent_term:get(?MODULE).
 
-%% Filter binary of a filter id (ids are assigned by insert/1).
+%% Filter binary of a filter id (ids are assigned by build/1 and sync/2).
 filter_of(Id) -> ets:lookup_element(?TAB, Id, 2).
 
-%% emqx_trie:insert/1 — idempotent (emqx_trie.erl:82-87)
-insert(Filter) when is_binary(Filter) ->
-    case ets:lookup(?TAB, {filter, Filter}) of
-        [_] -> ok;
-        [] ->
-            Id = ets:update_counter(?TAB, next_id, 1) - 1,
-            ets:insert(?TAB, [{Id, Filter}, {{filter, Filter}, Id}]),
-            {ok, _Epoch} = apply_delta(ctx(), [{Filter, Id}], []),
-            ok
-    end.
+%% Filter binaries of matched ids; an id deleted since its batch was matched
+%% is skipped (its filter has no routes left; ids are never reused).
+filters_of(Ids) -> [F || Id <- Ids, {_, F} <- ets:lookup(?TAB, Id)].
 
-%% emqx_trie:delete/1 — no-op when absent (emqx_trie.erl:91-96)
-delete(Filter) when is_binary(Filter) ->
-    case ets:lookup(?TAB, {filter, Filter}) of
-        [] -> ok;
-        [{_, Id}] ->
-            {ok, _Epoch} = apply_delta(ctx(), [], [Filter]),
-            ets:delete(?TAB, Id),
-            ets:delete(?TAB, {filter, Filter}),
+%% The whole table: the wildcard filters that have routes (emqx_trie's
+%% content, emqx_trie.erl:82-87 applied to each).  Called by emqx_gpu_routes.
+build(Filters) when is_list(Filters) ->
+    ets:match_delete(?TAB, {'_', '_'}),
+    ets:insert(?TAB, {next_id, length(Filters)}),
+    {_, Rows} = lists:foldl(fun(F, {I, Acc}) -> {I + 1, [{I, F}, {{filter, F}, I} | Acc]} end,
+                            {0, []}, Filters),
+    ets:insert(?TAB, Rows),
+    ok = build(ctx(), Filters).
+
+%% One epoch for a batch of trie changes, applied after their route
+%% transactions committed (emqx_gpu_routes): inserts are idempotent
+%% (emqx_trie.erl:84-85), deletes of absent filters are no-ops (:93-95).
+sync(Inserts, Deletes) ->
+    New = [F || F <- Inserts, ets:lookup(?TAB, {filter, F}) =:= []],
+    Gone = [{F, Id} || F <- Deletes, {_, Id} <- ets:lookup(?TAB, {filter, F})],
+    case New =:= [] andalso Gone =:= [] of
+        true -> ok;
+        false ->
+            Ins = [{F, ets:update_counter(?TAB, next_id, 1) - 1} || F <- New],
+            ets:insert(?TAB, lists:append([[{Id, F}, {{filter, F}, Id}] || {F, Id} <- Ins])),
+            {ok, _Epoch} = apply_delta(ctx(), Ins, [F || {F, _} <- Gone]),
+            %% ids leave the map only after the epoch without them is published
+            lists:foreach(fun({F, Id}) -> ets:delete(?TAB, Id), ets:delete(?TAB, {filter, F}) end, Gone),
             ok
     end.
 
 %% emqx_trie:match/1 — one topic; production callers go through the batcher
 match(Topic) when is_binary(Topic) ->
     case match_batch(ctx(), [Topic], ?MODE_TRIE) of
-        {ok, [Ids]} -> [ets:lookup_element(?TAB, Id, 2) || Id <- Ids];
+        {ok, [Ids]} -> filters_of(Ids);
         {error, _} -> emqx_trie:match(Topic)
     end.
 
-%% The filter set of emqx_router:match_routes/1 (exact ∪ wildcard); the
-%% router expands each filter to its #route{} entries with lookup_routes/1.
+%% emqx_router:match_routes/1 (emqx_router.erl:129-134) for one topic: the
+%% topic's own routes, then the routes of every trie match.
 match_routes(Topic) when is_binary(Topic) ->
-    case match_batch(ctx(), [Topic], ?MODE_ROUTES) of
+    case match_batch(ctx(), [Topic], ?MODE_TRIE) of
         {ok, [Ids]} ->
-            lists:append([emqx_router:lookup_routes(ets:lookup_element(?TAB, Id, 2)) || Id <- Ids]);
+            lists:append([emqx_router:lookup_routes(To) || To <- [Topic | filters_of(Ids)]]);
         {error, _} -> emqx_router:match_routes(Topic)
     end.

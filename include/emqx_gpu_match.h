@@ -146,10 +146,18 @@ int egm_match_batch(egm_ctx* ctx, const uint8_t* topics_blob, const uint32_t* to
    egm_result_free.  With two tickets in flight, batch k's device->host copy
    overlaps batch k+1's match.  At most 8 tickets or unreleased results per
    context (EGM_E_STATE beyond); free pipeline results before egm_close.
-   egm_match_batch is submit + wait. */
+   A ticket carries a generation: a stale, repeated or cancelled ticket is
+   refused with EGM_E_STATE (never answered with another batch's result).
+   egm_match_cancel gives a ticket up without waiting: its slot is reclaimed
+   once its batch has finished (for a waiter that will never call wait).
+   egm_match_batch is submit + wait on a slot of its own: concurrent callers
+   never see "pipeline full" (extra slots up to 64, then they queue for one).
+   A walk guard trip (a kernel invariant failed, egm_last_guard) makes wait
+   return EGM_E_DEVICE; only a capacity overflow is retried. */
 int egm_match_submit(egm_ctx* ctx, const uint8_t* topics_blob, const uint32_t* topic_offsets, uint32_t n_topics,
                      int mode, uint64_t* ticket);
 int egm_match_wait(egm_ctx* ctx, uint64_t ticket, egm_result** out);
+int egm_match_cancel(egm_ctx* ctx, uint64_t ticket);
 
 /* Device-resident variant: d_blob (4-byte aligned, blob_bytes >= d_offsets[n])
    and d_offsets are device pointers (d_offsets[0] == 0); results stay in device buffers owned by the caller
@@ -160,9 +168,16 @@ int egm_match_device(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes, c
                      uint32_t n_topics, int mode, void* hip_stream, uint64_t* d_row_ptr, uint32_t* d_ids,
                      uint64_t ids_cap, uint8_t* d_flags);
 /* Synchronises the last device batch and reports its counters.  overflow != 0
-   means ids_cap was too small (rerun with a larger buffer). */
+   means ids_cap was too small (rerun with a larger buffer) — capacity only.
+   Returns EGM_E_DEVICE (counters still filled) when a walk guard tripped:
+   a kernel invariant failed, the batch's rows were not assembled, and a
+   larger buffer would not help (egm_last_guard has the bits). */
 int egm_last_stats(egm_ctx* ctx, uint64_t* n_ids, uint64_t* visited, uint32_t* n_deferred_chunks,
                    uint32_t* overflow, uint32_t* n_error);
+/* Guard bits of the last batch (0 = none): 4 = a work stack would have
+   overrun (impossible by the pop bound: a bug), 8 = a walk loop ran past its
+   iteration guard (reported instead of hanging the GPU). */
+int egm_last_guard(egm_ctx* ctx, uint32_t* guard);
 /* Instrumentation: walk iterations and items popped of the last batch (lane
    occupancy = popped / (iters*64)), the iterations whose pop the stack-room
    bound cut short (the depth-first regime of deep, wide frontiers), and the
@@ -179,6 +194,7 @@ int egm_set_timing(egm_ctx* ctx, int enable);
 #define EGM_DEBUG_FORCE_HEAVY 1u
 #define EGM_DEBUG_FAIL_COMMIT 2u
 #define EGM_DEBUG_INPUT_ORDER 4u   /* walk the batch in input order (no locality sort; A/B and tests) */
+#define EGM_DEBUG_FORCE_GUARD 8u   /* loop guards of 2 iterations: trips the walk guard (error-path test) */
 int egm_set_debug(egm_ctx* ctx, uint32_t flags);
 int egm_get_timing(egm_ctx* ctx, double* walk_ms, uint64_t* walk_launches, double* fanout_ms,
                    uint64_t* fanout_launches);

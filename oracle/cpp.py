@@ -33,6 +33,8 @@ def _load():
         lib.ot_match_count.argtypes = [P, P, P, C.c_uint32, C.c_int]
         lib.ot_match_counts.restype = C.c_uint64
         lib.ot_match_counts.argtypes = [P, P, P, C.c_uint32, C.c_int, P]
+        lib.ot_visited_counts.restype = C.c_uint64
+        lib.ot_visited_counts.argtypes = [P, P, P, C.c_uint32, C.c_int, P]
         lib.ot_n_keys.restype = C.c_uint64
         lib.ot_n_keys.argtypes = [P]
         lib.ot_free_ptr.argtypes = [P]
@@ -92,6 +94,16 @@ class OracleTrie:
         counts = np.zeros(n, dtype=np.uint32)
         self.lib.ot_match_counts(self.h, _p(blob), _p(off), n, threads, _p(counts))
         return counts
+
+    def visited_counts(self, blob, off, threads: int = 1):
+        """SURVEY §8d V_t per topic (u64[n]) and its sum: the root plus every
+        prefix of a filter (up to a '#') that the NFA over the topic reaches —
+        counted from string prefixes, independently of the GPU table."""
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        n = len(off) - 1
+        counts = np.zeros(n, dtype=np.uint64)
+        tot = self.lib.ot_visited_counts(self.h, _p(blob), _p(off), n, threads, _p(counts))
+        return int(tot), counts
 
     def n_keys(self) -> int:
         return int(self.lib.ot_n_keys(self.h))

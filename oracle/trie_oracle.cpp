@@ -19,6 +19,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace {
@@ -213,7 +214,63 @@ struct Oracle {
   Trie trie;
   int mode = 0;  // 0 = emqx_trie:match/1, 1 = emqx_router:match_routes/1 filter set
   std::unordered_map<std::string, uint32_t> ids;  // filter -> id (the route table keys)
+  // every word-prefix of every filter up to (not including) a '#' word, '+'
+  // spelled "+": the states an NFA over the filter set can be in (built on
+  // first use by ot_visited_counts; SURVEY §8d's V_t)
+  std::unordered_set<std::string> prefixes;
+  bool prefixes_built = false;
 };
+
+// SURVEY §8d V_t, counted from string prefixes independently of the GPU
+// table: per topic without a '+'/'#' word, the root plus every prefix P of
+// length l = 1..D that is a prefix of some filter and matches the topic's
+// first l words word by word ('+' any word; a '$' first word never under a
+// root '+', emqx_trie.erl:208-215).  These are the states the kernels create
+// (a literal or '+' child that exists); '#' children are emitted, not states.
+void build_prefixes(Oracle* o) {
+  if (o->prefixes_built) return;
+  for (const auto& kv : o->ids) {
+    auto ws = words(kv.first.data(), kv.first.size());
+    std::string p;
+    for (size_t i = 0; i < ws.size(); ++i) {
+      if (ws[i].kind == Word::HASH) break;
+      if (i) p += '/';
+      p += bin_of(ws[i]);
+      o->prefixes.insert(p);
+    }
+  }
+  o->prefixes_built = true;
+}
+
+uint64_t visited_one(const Oracle* o, const char* t, size_t len) {
+  auto ws = words(t, len);
+  if (wildcard(ws)) return 0;
+  const bool dollar = ws[0].kind == Word::BIN && ws[0].bin[0] == '$';
+  uint64_t v = 1;   // the root
+  std::vector<std::string> cur, nxt;
+  for (size_t l = 0; l < ws.size(); ++l) {
+    nxt.clear();
+    auto step = [&](const std::string* s, const std::string& w) {
+      std::string c = s ? *s + "/" + w : w;
+      if (o->prefixes.count(c)) {
+        ++v;
+        nxt.push_back(std::move(c));
+      }
+    };
+    if (l == 0) {
+      step(nullptr, bin_of(ws[0]));
+      if (!dollar) step(nullptr, "+");
+    } else {
+      for (const auto& s : cur) {
+        step(&s, bin_of(ws[l]));
+        step(&s, "+");
+      }
+    }
+    cur.swap(nxt);
+    if (cur.empty()) break;
+  }
+  return v;
+}
 
 }  // namespace
 
@@ -238,8 +295,10 @@ int ot_add(void* h, const uint8_t* blob, const uint32_t* off, uint32_t n, const 
     if (o->ids.count(f)) continue;
     uint32_t id = ids ? ids[i] : (uint32_t)o->ids.size();
     o->ids.emplace(f, id);
+    o->prefixes_built = false;
     if (o->mode == 0 || wildcard(words(f.data(), f.size()))) o->trie.insert(f);
   }
+  if (!o->prefixes_built) std::unordered_set<std::string>().swap(o->prefixes);   // rebuilt on next use
   return 0;
 }
 
@@ -251,7 +310,9 @@ int ot_remove(void* h, const uint8_t* blob, const uint32_t* off, uint32_t n) {
     if (it == o->ids.end()) continue;
     o->ids.erase(it);
     o->trie.remove(f);
+    o->prefixes_built = false;
   }
+  if (!o->prefixes_built) std::unordered_set<std::string>().swap(o->prefixes);
   return 0;
 }
 
@@ -351,6 +412,32 @@ uint64_t ot_match_counts(void* h, const uint8_t* blob, const uint32_t* off, uint
         match_one(o, (const char*)blob + off[i], off[i + 1] - off[i], tmp);
         counts[i] = (uint32_t)tmp.size();
         s += tmp.size();
+      }
+      tot[k] = s;
+    });
+  }
+  for (auto& t : th) t.join();
+  uint64_t s = 0;
+  for (auto v : tot) s += v;
+  return s;
+}
+
+// Per-topic V_t (counts may be null) and their sum over n topics.
+uint64_t ot_visited_counts(void* h, const uint8_t* blob, const uint32_t* off, uint32_t n, int threads,
+                           uint64_t* counts) {
+  Oracle* o = (Oracle*)h;
+  build_prefixes(o);
+  if (threads < 1) threads = 1;
+  std::vector<uint64_t> tot(threads, 0);
+  std::vector<std::thread> th;
+  for (int k = 0; k < threads; ++k) {
+    th.emplace_back([&, k]() {
+      uint32_t a = (uint32_t)((uint64_t)n * k / threads), b = (uint32_t)((uint64_t)n * (k + 1) / threads);
+      uint64_t s = 0;
+      for (uint32_t i = a; i < b; ++i) {
+        const uint64_t v = visited_one(o, (const char*)blob + off[i], off[i + 1] - off[i]);
+        if (counts) counts[i] = v;
+        s += v;
       }
       tot[k] = s;
     });

@@ -408,6 +408,40 @@ class Router:
         return out
 
 
+def visited_states(topic: bytes, filters: Iterable[bytes]) -> int:
+    """SURVEY §8d V_t of one topic: the NFA states a walk over ``filters``
+    creates — the root plus every filter prefix (word prefixes up to a
+    ``'#'``) of length l = 1..D that matches the topic's first l words
+    (``'+'`` any word; never a root ``'+'`` under a ``'$'`` first word,
+    emqx_trie.erl:208-215).  0 for a topic with a wildcard word (match/1
+    returns [] at once, :102-111).  The roofline's byte model charges 32 B per
+    state; this count is independent of the GPU table's layout."""
+    ws = words(topic)
+    if wildcard(ws):
+        return 0
+    prefixes = set()
+    for f in filters:
+        fw = words(f)
+        for k in range(1, len(fw) + 1):
+            if fw[k - 1] is HASH:
+                break
+            prefixes.add(tuple(bin_(w) for w in fw[:k]))
+    dollar = isinstance(ws[0], bytes) and ws[0][:1] == b"$"
+    v, cur = 1, [()]
+    for l, w in enumerate(ws):
+        nxt = []
+        for p in cur:
+            for x in (bin_(w), b"+"):
+                if x == b"+" and l == 0 and dollar:
+                    continue
+                q = p + (x,)
+                if q in prefixes:
+                    v += 1
+                    nxt.append(q)
+        cur = nxt
+    return v
+
+
 def routes_semantics(topic: bytes, filters: Iterable[bytes]) -> List[bytes]:
     """Filter set whose routes ``match_routes/1`` returns (closed form).
 

@@ -47,6 +47,7 @@ int enif_get_tuple(ErlNifEnv*, ERL_NIF_TERM, int*, const ERL_NIF_TERM**);
 int enif_get_resource(ErlNifEnv*, ERL_NIF_TERM, ErlNifResourceType*, void**);
 void* enif_alloc_resource(ErlNifResourceType*, size_t);
 void enif_release_resource(void*);
+int enif_keep_resource(void*);
 #define ERL_NIF_INIT(name, funcs, load, reload, upgrade, unload) \
   const ErlNifFunc* name##_nif_table(void) { return funcs; } \
   int (*name##_nif_load)(ErlNifEnv*, void**, ERL_NIF_TERM) = load;

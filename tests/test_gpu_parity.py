@@ -177,7 +177,10 @@ def test_config_c0_vs_cpp_oracle(gm, mode):
     row, ids = o.match(t.blob, t.off, threads=8)
     assert np.array_equal(res.row_ptr, row)
     assert np.array_equal(canonical(res.row_ptr, res.ids), canonical(row, ids))
-    assert res.visited > 0
+    # the roofline numerator's V_t: the kernels' count of states created equals
+    # the oracle's independent count (string prefixes; tests/test_oracle_visited.py)
+    vt, _ = o.visited_counts(t.blob, t.off, threads=8)
+    assert res.visited == vt > 0
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -196,6 +199,7 @@ def test_config_c0_heavy_path_vs_cpp_oracle(gm, mode):
     row, ids = o.match(t.blob, t.off, threads=8)
     assert np.array_equal(res.row_ptr, row)
     assert np.array_equal(canonical(res.row_ptr, res.ids), canonical(row, ids))
+    assert res.visited == o.visited_counts(t.blob, t.off, threads=8)[0]   # k_heavy counts V_t too
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -243,6 +247,7 @@ def test_config_c3_vs_cpp_oracle(gm, mode):
     row, ids = o.match(t.blob, t.off, threads=8)
     assert np.array_equal(res.row_ptr, row)
     assert np.array_equal(canonical(res.row_ptr, res.ids), canonical(row, ids))
+    assert res.visited == o.visited_counts(t.blob, t.off, threads=8)[0]
 
 
 def test_golden_fixture(gm):

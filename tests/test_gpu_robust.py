@@ -207,3 +207,111 @@ def test_pipeline_submit_wait(gm):
         gm.lib.egm_result_free(r)
     again = gm.wait(gm.submit(parts[3].blob, parts[3].off, L.EGM_MODE_ROUTES))
     assert np.array_equal(again.row_ptr, want[3].row_ptr)
+
+
+def test_pipeline_tickets_are_generational_and_cancellable(gm):
+    """a ticket carries a generation (a stale or repeated ticket is
+    refused, never answered with another batch's result) and can be given up
+    with egm_match_cancel (its slot is reclaimed once the batch finished)."""
+    f, t = synth.config("c0", n_topics=30_000)
+    gm.build(f.blob, f.off)
+    a, b = t.subset(np.arange(0, 10_000)), t.subset(np.arange(10_000, 30_000))
+    o = OracleTrie(True, L.EGM_MODE_ROUTES)
+    o.add(f.blob, f.off)
+    t1 = gm.submit(a.blob, a.off, L.EGM_MODE_ROUTES)
+    r1 = gm.wait(t1)
+    row, ids = o.match(a.blob, a.off, threads=4)
+    assert np.array_equal(r1.row_ptr, row) and np.array_equal(canonical(r1.row_ptr, r1.ids), canonical(row, ids))
+    with pytest.raises(L.EgmError) as e:
+        gm.wait(t1)                         # waited already
+    assert e.value.code == L.EGM_E_STATE
+    t2 = gm.submit(b.blob, b.off, L.EGM_MODE_ROUTES)   # same slot, next generation
+    assert (t2 & 0xFFFF) == (t1 & 0xFFFF) and t2 != t1
+    with pytest.raises(L.EgmError):
+        gm.wait(t1)                         # stale: must not return t2's rows
+    r2 = gm.wait(t2)
+    row, ids = o.match(b.blob, b.off, threads=4)
+    assert np.array_equal(r2.row_ptr, row) and np.array_equal(canonical(r2.row_ptr, r2.ids), canonical(row, ids))
+    # 8 abandoned tickets: cancelled, their slots come back (the 8-ticket limit would refuse otherwise)
+    for _round in range(3):
+        tks = [gm.submit(a.blob, a.off, L.EGM_MODE_ROUTES) for _ in range(8)]
+        for tk in tks:
+            gm.cancel(tk)
+        with pytest.raises(L.EgmError):
+            gm.wait(tks[0])                 # a cancelled ticket has no result
+    r3 = gm.wait(gm.submit(a.blob, a.off, L.EGM_MODE_ROUTES))
+    assert np.array_equal(r3.row_ptr, r1.row_ptr)
+
+
+def test_match_batch_many_threads_never_pipeline_full(gm):
+    """more than 8 concurrent egm_match_batch callers (dirty
+    schedulers) queue for pipeline slots instead of failing, also while the
+    caller holds 8 unreleased ticket results; every row equals the oracle's."""
+    import ctypes as C
+    import threading
+    f, t = synth.config("c0", n_topics=48_000)
+    gm.build(f.blob, f.off)
+    parts = [t.subset(np.arange(k * 2_000, (k + 1) * 2_000)) for k in range(24)]
+    o = OracleTrie(True, L.EGM_MODE_ROUTES)
+    o.add(f.blob, f.off)
+    want = [o.match(p.blob, p.off, threads=2) for p in parts]
+    held = []
+    for _ in range(8):   # the 8 tickets of egm_match_submit, results not released
+        r = C.POINTER(L.egm_result)()
+        tk = gm.submit(parts[0].blob, parts[0].off, L.EGM_MODE_ROUTES)
+        assert gm.lib.egm_match_wait(gm.ctx, tk, C.byref(r)) == 0
+        held.append(r)
+    errors, got = [], [None] * len(parts)
+
+    def worker(k):
+        try:
+            for _ in range(3):
+                got[k] = gm.match(parts[k].blob, parts[k].off, L.EGM_MODE_ROUTES)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(len(parts))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    for r in held:
+        gm.lib.egm_result_free(r)
+    assert not errors, errors[:3]
+    for g, (row, ids) in zip(got, want):
+        assert np.array_equal(g.row_ptr, row)
+        assert np.array_equal(canonical(g.row_ptr, g.ids), canonical(row, ids))
+
+
+def test_walk_guard_trip_is_a_device_error_not_overflow(gm):
+    """a tripped walk guard (a kernel invariant failed) is
+    EGM_E_DEVICE from wait/batch and from egm_last_stats, reported in its own
+    bits (egm_last_guard), never as the capacity `overflow` a caller would
+    answer with a bigger buffer."""
+    import torch
+    f, t = synth.config("c0", n_topics=20_000)
+    gm.build(f.blob, f.off)
+    good = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    gm.set_debug(L.EGM_DEBUG_FORCE_GUARD)
+    try:
+        with pytest.raises(L.EgmError) as e:
+            gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+        assert e.value.code == L.EGM_E_DEVICE and "guard" in str(e.value)
+        dev = torch.device("cuda:0")
+        d_blob = torch.from_numpy(t.blob).to(dev)
+        d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+        d_row = torch.zeros(t.n + 1, dtype=torch.int64, device=dev)
+        d_ids = torch.zeros(64 * t.n, dtype=torch.int32, device=dev)
+        s = torch.cuda.current_stream().cuda_stream
+        gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), t.n, L.EGM_MODE_ROUTES, s,
+                        d_row.data_ptr(), d_ids.data_ptr(), 64 * t.n)
+        torch.cuda.synchronize()
+        with pytest.raises(L.EgmError) as e:
+            gm.last_stats()
+        assert e.value.code == L.EGM_E_DEVICE
+        assert gm.last_guard() & L.EGM_GUARD_LOOP
+    finally:
+        gm.set_debug(0)
+    again = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    assert gm.last_guard() == 0 and gm.last_stats()["overflow"] == 0
+    assert np.array_equal(again.row_ptr, good.row_ptr)

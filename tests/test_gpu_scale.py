@@ -86,6 +86,10 @@ def test_c2_full_sampled_rows_exact(c2):
     assert np.array_equal(grow, row)
     assert np.array_equal(canonical(grow, gids), canonical(row, ids))
     assert int(res.row_ptr[-1]) > 40 * t.n   # ~50 matches per C2 topic
+    # the bench line's V_t (32 B per state of its 22.4 GB model): the sample's
+    # kernel count equals the oracle's independent count
+    vt, _ = o.visited_counts(sub.blob, sub.off, threads=THREADS)
+    assert c2["gm"].match(sub.blob, sub.off, L.EGM_MODE_ROUTES).visited == vt
 
 
 def test_c2_full_determinism(c2):

@@ -69,6 +69,7 @@ class Emul:
         dollar = topic[:1] == b"$"
         D = len(ws)
         out = []
+        self.states = 0
         if wild:
             if mode == 0:
                 return out
@@ -90,8 +91,10 @@ class Emul:
                 out.append(term)
             return out
         stack = [(0, 0, self.rec(0), 0)]
+        self.states = 0   # states created (the kernels' `visited`, SURVEY §8d V_t)
         while stack:
             node, level, (plus, hsh, term, fl), wc = stack.pop()
+            self.states += 1
             atend = level == D
             rootd = level == 0 and dollar
             if (fl & F_HASH) and not rootd:

@@ -70,6 +70,9 @@ for step in "$@"; do
     cap128) EGM_FIX_CAP=128 run cap128 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86/128,a86/96,a86/128" ;;
     orders) run orders 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86,0,a86/128,a86" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    granule)   # random-read granule (tools/granule.hip): timing, then FETCH_SIZE per kernel
+      run granule 120 "$R/tools/granule"
+      run granule_pmc 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$R/gpurun_out/${TAG}_granule_pmc" -o run --output-format csv -- "$R/tools/granule" ;;
     c4m) run c4m 400 python $R/bench.py --config c4 --filters 10000000 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
     c4m_*)  # the same on variant V (tools/build_variant.py)
       v=${step#c4m_}
