@@ -72,7 +72,7 @@ def walk_traffic(config: str, filters: int, topics: int):
     passes), or None.  bench.py cannot collect counters itself: PMC passes
     need their own rocprofv3 runs."""
     import glob
-    best = None
+    found = []
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_walk_pmc.json"))):
         try:
             with open(p) as fh:
@@ -81,8 +81,16 @@ def walk_traffic(config: str, filters: int, topics: int):
             continue
         if (r.get("workload") == config and r.get("filters") == filters and r.get("topics") == topics
                 and r.get("kernel_src_sha") == kernel_src_sha()):
-            best = (r, os.path.relpath(p, ROOT))
-    return best
+            found.append((r, os.path.relpath(p, ROOT)))
+    if not found:
+        return None
+    # several records of one source must agree (the last one in glob
+    # order won silently); disagreeing records give no traffic at all
+    tr = [r["traffic_bytes_per_launch"] for r, _ in found]
+    if max(tr) > 1.03 * min(tr):
+        log(f"PMC records of this kernel source disagree ({[p for _, p in found]}): traffic not reported")
+        return None
+    return found[-1]
 
 
 def cpu_baseline(f, t, match_mode: int, seconds: float) -> dict:
@@ -177,11 +185,141 @@ LAYOUTS = {
 }
 
 
+class ShardLeg:
+    """The filter-sharded layout (BASELINE C2 as worded: "10M
+    filters sharded across 8xMI355X, topic batch broadcast, RCCL gather of
+    match IDs over xGMI") on this rank: its shard of the filters
+    (word_hash(filter) mod N, global ids), rank 0's batch broadcast every step.
+    Without fan-out each step gathers counts and ids to rank 0 and merges them
+    on the GPU (dist.ShardExchange); with fan-out every rank expands its own
+    matches through the subscriber rows of its own filters and only the
+    per-topic delivery totals are reduced to rank 0 (dist.ShardFanout)."""
+
+    def __init__(self, gm, f, t, rank, world, dev, stream, mode, fanout, seed, sizes=None):
+        import torch
+        from emqx_amd import synth
+        from emqx_amd.dist import ShardExchange, ShardFanout, gpu_merge, shard_of
+        self.gm, self.rank, self.world, self.dev, self.sp, self.mode = gm, rank, world, dev, stream, mode
+        idx = np.nonzero(shard_of(f, world) == rank)[0].astype(np.uint32)
+        sub = f.subset(idx)
+        gm.build(sub.blob, sub.off, idx)
+        self.n_filters = len(idx)
+        del sub
+        self.sizes = sizes if sizes is not None else (t.n, len(t.blob))   # (topics, blob bytes) of rank 0's batch
+        n = self.n = self.sizes[0]
+        self.d_blob = torch.from_numpy(t.blob).to(dev) if rank == 0 else None
+        self.d_off = torch.from_numpy(t.off.view(np.int32)).to(dev) if rank == 0 else None
+        self.cap = max(4 * n // max(1, world) + 4096, 1 << 20)
+        self.row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        self.ids = torch.zeros(self.cap, dtype=torch.int32, device=dev)
+        self.fanout = fanout
+        self.sub_entries = 0
+        if fanout:
+            # the subscriber rows of this shard's filters only (empty rows elsewhere)
+            srow, ssubs = synth.subscribers(f.n, lam=1.0, p_big=0.001, n_big=2000, p_share=0.1, groups=64, seed=seed)
+            per = np.diff(srow)
+            mine = np.zeros(f.n, bool)
+            mine[idx] = True
+            lrow = np.zeros(f.n + 1, np.uint64)
+            np.cumsum(np.where(mine, per, 0), out=lrow[1:])
+            keep = np.repeat(mine, per.astype(np.int64))
+            lsubs = ssubs[keep]
+            del srow, ssubs, per, keep
+            gm.subs_build(lrow, lsubs)
+            self.sub_entries = len(lsubs)
+            del lrow, lsubs
+            self.fcap = max(8 * n // max(1, world), 1 << 20)
+            self.drow = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            self.dfid = torch.zeros(self.fcap, dtype=torch.int32, device=dev)
+            self.dsub = torch.zeros(self.fcap, dtype=torch.int32, device=dev)
+            self.ex = ShardFanout(rank, world, dev, self._local_fanout)
+        else:
+            self.mcap = max(4 * n, 1 << 20) if rank == 0 else 0
+            self.mrow = torch.zeros(n + 1, dtype=torch.int64, device=dev) if rank == 0 else None
+            self.mids = torch.zeros(max(1, self.mcap), dtype=torch.int32, device=dev) if rank == 0 else None
+            self.ex = self._exchange()
+
+    def _exchange(self):
+        from emqx_amd.dist import ShardExchange, gpu_merge
+        mg = gpu_merge(self.gm, self.sp, self.mrow, self.mids) if self.rank == 0 else None
+        return ShardExchange(self.rank, self.world, self.dev, self._local_match, mg)
+
+    def _local_match(self, tb, to, nn):
+        self.gm.match_device(tb.data_ptr(), tb.numel(), to.data_ptr(), nn, self.mode, self.sp, self.row.data_ptr(),
+                             self.ids.data_ptr(), self.cap)
+        st = self.gm.last_stats()   # syncs: the id count is needed on the host for the gather
+        return self.row, self.ids, int(st["n_ids"]), bool(st["overflow"])
+
+    def _local_fanout(self, tb, to, nn):
+        self.gm.match_device(tb.data_ptr(), tb.numel(), to.data_ptr(), nn, self.mode, self.sp, self.row.data_ptr(),
+                             self.ids.data_ptr(), self.cap)
+        st = self.gm.last_stats()
+        self.last_ids = int(st["n_ids"])
+        if st["overflow"]:
+            return self.row, True
+        self.gm.fanout_device(self.row.data_ptr(), self.ids.data_ptr(), self.cap, nn, self.sp, self.drow.data_ptr(),
+                              self.dfid.data_ptr(), self.dsub.data_ptr(), self.fcap)
+        fo = self.gm.last_fanout()
+        self.last_deliveries = int(fo["deliveries"])
+        return self.drow, bool(fo["overflow"])
+
+    def step(self):
+        if self.rank == 0:
+            return self.ex.step(self.d_blob, self.d_off, sizes=self.sizes)
+        return self.ex.step(sizes=self.sizes)
+
+    def size(self):
+        """Untimed steps until no rank overflows (buffers grown from the totals)."""
+        import torch
+        import torch.distributed as dist
+        for _ in range(6):
+            self.step()
+            torch.cuda.synchronize(self.dev)
+            if not self.ex.last_overflow:
+                return
+            if self.fanout:
+                # grow both local buffers from this rank's own counts, in step on every rank
+                mine = torch.tensor([self.last_ids, getattr(self, "last_deliveries", 0)], dtype=torch.int64,
+                                    device=self.dev)
+                if self.last_ids > self.cap:
+                    self.cap = int(self.last_ids * 1.25) + 1024
+                    self.ids = torch.zeros(self.cap, dtype=torch.int32, device=self.dev)
+                d = getattr(self, "last_deliveries", 0)
+                if d > self.fcap:
+                    self.fcap = int(d * 1.1) + 1024
+                    self.dfid = torch.zeros(self.fcap, dtype=torch.int32, device=self.dev)
+                    self.dsub = torch.zeros(self.fcap, dtype=torch.int32, device=self.dev)
+                del mine
+                continue
+            tots = self.ex.last_totals
+            if tots[self.rank] > self.cap:
+                self.cap = int(tots[self.rank] * 1.25) + 1024
+                self.ids = torch.zeros(self.cap, dtype=torch.int32, device=self.dev)
+            if self.rank == 0 and sum(tots) > self.mcap:
+                self.mcap = int(sum(tots) * 1.25) + 1024
+                self.mids = torch.zeros(self.mcap, dtype=torch.int32, device=self.dev)
+            self.ex = self._exchange()
+        raise RuntimeError("shard leg: buffers did not settle")
+
+    def merged_ids(self):
+        return None if self.fanout else sum(self.ex.last_totals)
+
+
+def shard_cost_model(n, blob_bytes, world, merged_ids):
+    """Bytes one sharded step moves over xGMI: the broadcast
+    of the batch to N-1 ranks, the gather of N-1 shards' counts and ids to
+    rank 0 (ids: (N-1)/N of the merged total on average)."""
+    bcast = blob_bytes + 4 * (n + 1)
+    gather_ids = int(4 * merged_ids * (world - 1) / world) if merged_ids is not None else 0
+    return {"broadcast_bytes": bcast, "gather_bytes": 4 * n * (world - 1) + gather_ids,
+            "merge_bytes_on_rank0": (8 * merged_ids + 4 * n * world + 16 * n) if merged_ids is not None else 0}
+
+
 def _init_dist(args, rank, world, dev):
     """A process group whenever the layout exchanges data (shard mode runs its
     collectives at every world size, world 1 included)."""
     import torch.distributed as dist
-    if world > 1 or args.mode == "shard":
+    if world > 1 or args.mode == "shard" or args.sharded_leg == "on":
         if "MASTER_ADDR" not in os.environ:   # plain `python bench.py --mode shard`: a world of one
             import socket
             so = socket.socket()
@@ -224,10 +362,13 @@ def main():
                     help="also time the host-visible path (pinned staging, H2D, match, D2H) at N=1")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--sharded-leg", default="auto", choices=["auto", "on", "off"],
+                    help="replicate mode at N>1 (auto) or any N (on): also time the filter-sharded layout "
+                         "(BASELINE C2 as worded: broadcast + RCCL gather + GPU merge; with fan-out, fan-out on "
+                         "the owner shard + a reduce of per-topic delivery totals), reported as the line's "
+                         "`sharded`")
     args = ap.parse_args()
     fanout = args.fanout == "on" or (args.fanout == "auto" and args.config in ("c3", "c4"))
-    if fanout and args.mode == "shard":
-        ap.error("--fanout runs with --mode replicate (a shard's fan-out would precede the id gather)")
     _heartbeat()
 
     rank = int(os.environ.get("RANK", 0))
@@ -272,21 +413,22 @@ def main():
 
     gm = GpuMatcher(local, max_batch=nt)
     t0 = time.time()
+    nstreams = 1 if shard else max(1, args.streams)
+    piped = args.pipelined == "on" and not shard and not fanout and nstreams == 1
+    nbuf = 2 if piped else nstreams
+    streams = [torch.cuda.Stream(dev) for _ in range(nbuf)]
+    stream = streams[0]
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+    leg = None
     if shard:
-        from emqx_amd.dist import shard_of
-        from emqx_amd.engine import pack_strings
-        idx = np.nonzero(shard_of(f, world) == rank)[0]
-        fl = f.to_list()
-        blob, off = pack_strings([fl[i] for i in idx])
-        del fl
-        gm.build(blob, off, idx.astype(np.uint32))
-        del blob, off
+        leg = ShardLeg(gm, f, t, rank, world, dev, sp, mode, fanout, seed)
     else:
         gm.build(f.blob, f.off)
     tstats = gm.stats()
     log(f"[rank {rank}] table built in {time.time() - t0:.1f}s: {tstats}")
-    sub_entries = 0
-    if fanout:
+    sub_entries = leg.sub_entries if leg is not None else 0
+    if fanout and not shard:
         # filter id -> subscriber CSR (emqx_subscriber bag, shards flattened)
         t0 = time.time()
         srow, ssubs = synth.subscribers(f.n, lam=1.0, p_big=0.001, n_big=2000, p_share=0.1, groups=64, seed=seed)
@@ -296,15 +438,8 @@ def main():
         log(f"[rank {rank}] subscriber table: {sub_entries} entries in {time.time() - t0:.1f}s")
 
     # one explicit stream for every kernel and copy of the step (the library
-    # and torch share one HIP runtime: emqx_amd._lib loads torch first)
-    nstreams = 1 if shard else max(1, args.streams)
+    # and torch share one HIP runtime: emqx_amd._lib loads torch first);
     # the pipelined leg (after the timed steps): consecutive batches over two streams
-    piped = args.pipelined == "on" and not shard and not fanout and nstreams == 1
-    nbuf = 2 if piped else nstreams
-    streams = [torch.cuda.Stream(dev) for _ in range(nbuf)]
-    stream = streams[0]
-    torch.cuda.set_stream(stream)
-    sp = stream.cuda_stream
     n = t.n
     nbytes = int(t.off[-1])
     d_blob = torch.from_numpy(t.blob).to(dev)
@@ -333,61 +468,28 @@ def main():
             gm.fanout_device(row.data_ptr(), ids.data_ptr(), bufs["cap"], n, s_i, d_drow.data_ptr(),
                              d_fid.data_ptr(), d_sub.data_ptr(), fcap)
 
-    exchange = None
-    if shard:
-        from emqx_amd.dist import ShardExchange, gpu_merge
-
-        def local_match(tb, to, nn):
-            gm.match_device(tb.data_ptr(), tb.numel(), to.data_ptr(), nn, mode, sp, bufs["row"].data_ptr(),
-                            bufs["ids"].data_ptr(), bufs["cap"])
-            st = gm.last_stats()   # syncs: the id count is needed on the host for the gather
-            return bufs["row"], bufs["ids"], int(st["n_ids"]), bool(st["overflow"])
-
-        bufs["mcap"] = max(4 * n, 1 << 20) if rank == 0 else 0
-        bufs["mrow"] = torch.zeros(n + 1, dtype=torch.int64, device=dev) if rank == 0 else None
-        bufs["mids"] = torch.zeros(max(1, bufs["mcap"]), dtype=torch.int32, device=dev) if rank == 0 else None
-
-        def make_exchange():
-            mg = gpu_merge(gm, sp, bufs["mrow"], bufs["mids"]) if rank == 0 else None
-            return ShardExchange(rank, world, dev, local_match, mg)
-
-        exchange = make_exchange()
-
     def step():
-        if exchange is None:
+        if leg is None:
             run_local()
         else:
-            exchange.step(d_blob if rank == 0 else None, d_off if rank == 0 else None, sizes=(n, d_blob.numel()))
+            leg.step()
 
     # size the id buffers (untimed), then warm up
-    for _ in range(4):
-        step()
-        torch.cuda.synchronize(dev)
-        st = gm.last_stats()
-        if exchange is not None:
-            if not exchange.last_overflow:
-                tot = sum(exchange.last_totals)
-                if rank == 0 and tot > bufs["mcap"]:
-                    raise RuntimeError("merge buffer too small")   # gpu_merge refuses before writing
+    if leg is not None:
+        leg.size()
+    else:
+        for _ in range(4):
+            step()
+            torch.cuda.synchronize(dev)
+            st = gm.last_stats()
+            if not st["overflow"]:
                 break
-            mine = exchange.last_totals[rank]
-            if mine > bufs["cap"]:
-                bufs["cap"] = int(mine * 1.25) + 1024
-                bufs["ids"] = torch.zeros(bufs["cap"], dtype=torch.int32, device=dev)
-            if rank == 0:
-                bufs["mcap"] = int(sum(exchange.last_totals) * 1.25) + 1024
-                bufs["mids"] = torch.zeros(bufs["mcap"], dtype=torch.int32, device=dev)
-            exchange = make_exchange()
-            log(f"[rank {rank}] grew id buffers: local {bufs['cap']}")
-            continue
-        if not st["overflow"]:
-            break
-        bufs["cap"] = int(st["n_ids"] * 1.25) + 1024
-        bufs["idss"] = [torch.zeros(bufs["cap"], dtype=torch.int32, device=dev) for _ in range(nbuf)]
-        bufs["ids"] = bufs["idss"][0]
-        bufs["k"] = 0
-        log(f"[rank {rank}] grew id buffers to {bufs['cap']}")
-    if fanout:
+            bufs["cap"] = int(st["n_ids"] * 1.25) + 1024
+            bufs["idss"] = [torch.zeros(bufs["cap"], dtype=torch.int32, device=dev) for _ in range(nbuf)]
+            bufs["ids"] = bufs["idss"][0]
+            bufs["k"] = 0
+            log(f"[rank {rank}] grew id buffers to {bufs['cap']}")
+    if fanout and leg is None:
         fan_on = True
         bufs["k"] = 0
         step()
@@ -404,8 +506,8 @@ def main():
     torch.cuda.synchronize(dev)
     st = gm.last_stats()
     assert st["overflow"] == 0 and st["errors"] == 0, st
-    if exchange is not None:
-        assert not exchange.last_overflow
+    if leg is not None:
+        assert not leg.ex.last_overflow
 
     gm.set_timing(True)
     if have_pg:
@@ -423,8 +525,13 @@ def main():
         elapsed = float(e.item())
     tim = gm.get_timing()
     st = gm.last_stats()
-    deliveries = int(d_drow[n].item()) if fanout else None
-    if fanout:
+    deliveries = int(d_drow[n].item()) if (fanout and leg is None) else None
+    if fanout and leg is not None:   # every rank's own part of the batch's deliveries, summed
+        dt = torch.tensor([leg.last_deliveries], dtype=torch.int64, device=dev)
+        if have_pg:
+            dist.all_reduce(dt)
+        deliveries = int(dt.item())
+    if fanout and leg is None:
         assert deliveries <= fcap, (deliveries, fcap)
     wc = gm.walk_counters()
     gm.set_timing(False)
@@ -467,9 +574,12 @@ def main():
                      "note": "same steps, consecutive batches alternating over two HIP streams (separate "
                              "workspaces and output buffers)"}
         bufs["ns"], bufs["k"] = nstreams, 0
-    merged_ids = sum(exchange.last_totals) if exchange is not None else None
-    if args.x_orders and exchange is None:
+    merged_ids = leg.merged_ids() if leg is not None else None
+    if args.x_orders and leg is None:
         order_experiment(args, gm, run_local, bufs, dev, n)
+    sharded = None
+    if leg is None and (args.sharded_leg == "on" or (args.sharded_leg == "auto" and world > 1)):
+        sharded = sharded_leg(args, f, t, rank, world, dev, mode, fanout, seed, have_pg)
 
     units_per_step = n if shard else n * world
     value = units_per_step * args.steps / elapsed
@@ -511,6 +621,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic[0]["traffic_bytes_per_launch"] if traffic else None,
                          "traffic_source": traffic[1] if traffic else None,
+                         # the counters' bytes over the same time (beside, not instead of,
+                         # the algorithmic `frac` the contract prescribes)
+                         "frac_measured": (traffic[0]["traffic_bytes_per_launch"] / (walk_ms * 1e-3) / 1e9 /
+                                           HBM_PEAK_GBS) if traffic else None,
                          "kernel": "k_walk", "kernel_ms": walk_ms, "bytes_per_launch": walk_bytes,
                          "kernel_src_sha": kernel_src_sha(),
                          "kernel_ms_isolated": iso_ms,
@@ -524,10 +638,12 @@ def main():
                       "walk_plus_record_reads": wc["plus_reads"]},
             "fanout": ({"deliveries_per_step": deliveries, "subscriber_entries": sub_entries,
                         "fanout_ms": tim["fanout_ms"] / max(1, tim["fanout_launches"]),
-                        "deliveries_per_s": deliveries * world * args.steps / elapsed,
+                        "deliveries_per_s": deliveries * (1 if shard else world) * args.steps / elapsed,
                         "bytes_per_launch": 12 * deliveries + 20 * n_ids + 8 * (n + 1)}
                        if fanout else None),
             "pipelined": pipelined,
+            "sharded": sharded,
+            "xgmi_model": (shard_cost_model(n, nbytes, world, merged_ids) if shard else None),
             "host_e2e": host,
             "cpu_baseline": cpu,
         }
@@ -535,6 +651,59 @@ def main():
     gm.close()
     if have_pg:
         dist.destroy_process_group()
+
+
+def sharded_leg(args, f, t, rank, world, dev, mode, fanout, seed, have_pg):
+    """The filter-sharded layout timed beside the replicate `value` (VERDICT
+    r2 item 5): a second context per rank holds this rank's filter shard, rank
+    0's batch (its own replicate batch) is broadcast each step.  value =
+    topics of the broadcast batch per second for the whole node."""
+    import torch
+    import torch.distributed as dist
+    from emqx_amd.engine import GpuMatcher
+    meta = torch.tensor([t.n, len(t.blob)] if rank == 0 else [0, 0], dtype=torch.int64, device=dev)
+    if have_pg:
+        dist.broadcast(meta, 0)
+    sizes = (int(meta[0].item()), int(meta[1].item()))
+    gm2 = GpuMatcher(dev.index, max_batch=sizes[0])
+    s = torch.cuda.Stream(dev)
+    try:
+        t0 = time.time()
+        leg = ShardLeg(gm2, f, t if rank == 0 else None, rank, world, dev, s.cuda_stream, mode, fanout, seed, sizes)
+        log(f"[rank {rank}] sharded leg: {leg.n_filters} filters on this rank, built in {time.time() - t0:.1f}s")
+        with torch.cuda.stream(s):
+            leg.size()
+            for _ in range(args.warmup):
+                leg.step()
+            torch.cuda.synchronize(dev)
+            if have_pg:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                leg.step()
+            torch.cuda.synchronize(dev)
+            el = time.perf_counter() - t0
+        if have_pg:
+            dist.barrier()
+            e = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = float(e.item())
+        merged = leg.merged_ids()
+        out = {"value": sizes[0] * args.steps / el, "unit": "topics/s", "ms_per_step": el / args.steps * 1e3,
+               "scaling": "strong", "filters_per_rank": leg.n_filters,
+               "layout": LAYOUTS["shard"] + (" — fan-out on the owner shard, per-topic delivery totals reduced to "
+                                             "rank 0" if fanout else ""),
+               "merged_ids_per_step": merged,
+               "xgmi_model": shard_cost_model(sizes[0], sizes[1], world, merged)}
+        if fanout:
+            dtot = torch.tensor([leg.last_deliveries], dtype=torch.int64, device=dev)
+            if have_pg:
+                dist.all_reduce(dtot)
+            out["deliveries_per_step"] = int(dtot.item())
+        return out
+    finally:
+        gm2.close()
 
 
 def order_experiment(args, gm, run_local, bufs, dev, n):

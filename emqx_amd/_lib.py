@@ -126,6 +126,7 @@ SIGNATURES = {
     "egm_image_insert": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32]),
     "egm_image_remove": (C.c_int, [_P, _P, C.c_uint32]),
     "egm_image_relayout": (None, [_P]),
+    "egm_image_build": (C.c_int, [_P, _P, _P, C.c_uint32, _P, C.c_uint32]),
     "egm_image_get_view": (C.c_int, [_P, C.POINTER(egm_image_view)]),
     "egm_image_take_dirty": (C.c_int, [_P, C.POINTER(egm_dirty_view)]),
     "egm_shard_assign": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P]),

@@ -59,7 +59,7 @@ def build_lib(verbose=False, force=False) -> str:
         _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result", "-Wno-unused-value",
               "-c", hip_src, "-o", o], verbose)
     objs.append(o)
-    for name in ("egm_table.cpp", "egm_capi.cpp", "egm_retain.cpp"):
+    for name in ("egm_table.cpp", "egm_bulk.cpp", "egm_capi.cpp", "egm_retain.cpp"):
         src = os.path.join(CSRC, name)
         o = os.path.join(BUILD, name.replace(".cpp", ".o"))
         if force or _stale(o, [src] + HEADERS):

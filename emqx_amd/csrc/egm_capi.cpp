@@ -720,6 +720,18 @@ static bool validate_inserts(const HostTable& t, const uint8_t* blob, const uint
   return true;
 }
 
+// egm_table_build uses the parallel bulk build from EGM_BULK_MIN filters on
+// (default 65 536; 0 = always), unless an id asks to be assigned (NONE).
+static bool use_bulk_build(uint32_t n, const uint32_t* ids) {
+  const char* e = getenv("EGM_BULK_MIN");
+  const uint64_t lim = (e && *e) ? strtoull(e, nullptr, 10) : 65536;
+  if (n < lim) return false;
+  if (ids)
+    for (uint32_t i = 0; i < n; ++i)
+      if (ids[i] == NONE) return false;
+  return true;
+}
+
 extern "C" {
 
 const char* egm_version(void) { return "emqx_gpu_match 0.1 (gfx950)"; }
@@ -785,6 +797,13 @@ int egm_table_build(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32
   if (set_device(c)) return EGM_E_DEVICE;
   std::string why;
   if (!validate_inserts(c->table, blob, off, n, ids, true, &why)) return c->fail(EGM_E_INVAL, why);
+  if (use_bulk_build(n, ids)) {   // parallel: the same image as the insert loop below (egm_bulk.cpp)
+    if (c->table.bulk_build(blob, off, n, ids, 0) < 0) {
+      c->table.clear();
+      return c->fail(EGM_E_INVAL, "table too large (node ids exhausted)");
+    }
+    return commit_locked(c, nullptr);
+  }
   c->table.clear();
   for (uint32_t i = 0; i < n; ++i) {
     int r = c->table.insert(blob + off[i], off[i + 1] - off[i], ids ? ids[i] : i, nullptr);
@@ -1053,7 +1072,8 @@ static int submit_locked(egm_ctx* c, std::unique_lock<std::recursive_mutex>& g, 
     return c->hip_fail(e, "d2h stream");
   if (!sync) {
     size_t tickets = 0;
-    for (auto& p : c->pipe) tickets += (!p->sync && (p->busy || p->held)) ? 1u : 0u;
+    for (auto& p : c->pipe)   // a cancelled ticket no longer counts (its slot comes back when its batch is done)
+      tickets += (!p->sync && !p->abandoned && (p->busy || p->held)) ? 1u : 0u;
     if (tickets >= PIPE_MAX_SLOTS) return c->fail(EGM_E_STATE, "pipeline full: wait for a ticket or free its result");
   }
   long k = pipe_free_slot(c);
@@ -1448,6 +1468,16 @@ int egm_image_remove(egm_image* im, const uint8_t* f, uint32_t len) {
 }
 void egm_image_relayout(egm_image* im) {
   if (im) im->t.relayout();
+}
+int egm_image_build(egm_image* im, const uint8_t* blob, const uint32_t* off, uint32_t n, const uint32_t* ids,
+                    uint32_t threads) {
+  if (!im || (n && (!blob || !valid_offsets(off, n)))) return EGM_E_INVAL;
+  std::string why;
+  if (!validate_inserts(im->t, blob, off, n, ids, true, &why)) return EGM_E_INVAL;
+  if (ids)
+    for (uint32_t i = 0; i < n; ++i)
+      if (ids[i] == NONE) return EGM_E_INVAL;
+  return im->t.bulk_build(blob, off, n, ids, threads) < 0 ? EGM_E_INVAL : EGM_OK;
 }
 int egm_image_take_dirty(egm_image* im, egm_dirty_view* v) {
   if (!im || !v) return EGM_E_INVAL;

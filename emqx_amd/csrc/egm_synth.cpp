@@ -10,6 +10,7 @@
 // splitmix64 (SURVEY names PCG64; any fixed PRNG is equivalent for these
 // distributions — the seed convention 0xE3C00000 + config index is kept).
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -17,6 +18,7 @@
 #include <cmath>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
@@ -77,10 +79,22 @@ struct Vocab {
   }
 };
 
+// "w{l}_{k}" (formatted by hand: snprintf dominated generation time)
+void put_uint(std::string& out, uint32_t v) {
+  char buf[12];
+  int i = 12;
+  do {
+    buf[--i] = (char)('0' + v % 10);
+    v /= 10;
+  } while (v);
+  out.append(buf + i, 12 - i);
+}
+
 void put_word(std::string& out, int l, uint32_t k) {
-  char buf[32];
-  int n = snprintf(buf, sizeof buf, "w%d_%u", l, k);
-  out.append(buf, n);
+  out += 'w';
+  put_uint(out, (uint32_t)l);
+  out += '_';
+  put_uint(out, k);
 }
 
 struct Strings {
@@ -122,12 +136,143 @@ void egs_free(egs_strings* s) {
   s->off = nullptr;
 }
 
+// One candidate filter (the distribution of egs_filters).
+static void gen_filter(Rng& r, Vocab& voc, std::string& f, int dmin, int dmax, double wc_frac, double p_plus,
+                       double p_hash, double p_empty) {
+  f.clear();
+  int d = r.range(dmin, dmax);
+  bool wild = r.uni() < wc_frac, any = false;
+  for (int l = 0; l < d; ++l) {
+    if (l) f += '/';
+    if (wild && l == d - 1 && (r.uni() < p_hash || !any)) {
+      f += '#';
+      any = true;
+    } else if (wild && r.uni() < p_plus) {
+      f += '+';
+      any = true;
+    } else if (r.uni() < p_empty) {
+      // '' level
+    } else {
+      put_word(f, l, voc.sample(r, l));
+    }
+  }
+}
+
+static unsigned synth_threads() {
+  const char* e = getenv("EGM_BUILD_THREADS");
+  if (e && *e) return (unsigned)std::max(1, atoi(e));
+  unsigned n = std::max(1u, std::thread::hardware_concurrency());
+  if (FILE* fp = fopen("/sys/fs/cgroup/cpu.max", "r")) {   // the cgroup CPU quota
+    char q[64] = {0};
+    unsigned long long period = 0;
+    if (fscanf(fp, "%63s %llu", q, &period) == 2 && strcmp(q, "max") != 0 && period)
+      n = std::min<unsigned>(n, (unsigned)std::max<unsigned long long>(1, (strtoull(q, nullptr, 10) + period - 1) / period));
+    fclose(fp);
+  }
+  return std::min(n, 64u);
+}
+
+// Large sets (n > PAR_MIN): candidates in blocks of PAR_BLOCK, block k from
+// its own stream (seed, k), generated in parallel; duplicates dropped in
+// candidate order (first occurrence kept) by hash partitions in parallel;
+// rounds of blocks until n filters are unique.  Deterministic for any thread
+// count.  Smaller sets keep the single-stream generator (the C0-C3 sets of
+// earlier rounds are unchanged).
+constexpr uint32_t PAR_MIN = 16u << 20;
+constexpr uint32_t PAR_BLOCK = 1u << 20;
+
+static int egs_filters_par(uint64_t seed, uint32_t n, int dmin, int dmax, double wc_frac, double p_plus,
+                           double p_hash, double p_empty, double zipf_s, uint32_t vmax, egs_strings* out) {
+  const unsigned T = synth_threads();
+  struct Block {
+    std::string blob;
+    std::vector<uint32_t> off{0};
+    std::vector<uint64_t> h;
+    std::vector<uint8_t> keep;
+  };
+  std::vector<Block> blocks;
+  std::vector<std::unordered_set<std::string_view>> part(T);
+  uint64_t have = 0;
+  uint32_t next_block = 0;
+  while (have < n) {
+    if ((uint64_t)next_block * PAR_BLOCK > (uint64_t)n * 50) return -1;   // the sequential bound on attempts
+    const uint32_t want = (uint32_t)std::max<uint64_t>(1, ((n - have) * 103 / 100 + PAR_BLOCK - 1) / PAR_BLOCK);
+    const size_t b0 = blocks.size();
+    blocks.resize(b0 + want);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        Vocab voc(zipf_s, vmax);
+        std::string f;
+        for (size_t k = b0 + t; k < blocks.size(); k += T) {
+          Block& B = blocks[k];
+          Rng r(seed ^ (0x9E3779B97F4A7C15ull * (next_block + (k - b0) + 1)));
+          B.blob.reserve((size_t)PAR_BLOCK * (dmax * 6 + 4));
+          B.off.reserve(PAR_BLOCK + 1);
+          B.h.resize(PAR_BLOCK);
+          for (uint32_t i = 0; i < PAR_BLOCK; ++i) {
+            gen_filter(r, voc, f, dmin, dmax, wc_frac, p_plus, p_hash, p_empty);
+            B.blob += f;
+            B.off.push_back((uint32_t)B.blob.size());
+            B.h[i] = std::hash<std::string_view>()(std::string_view(f));
+          }
+          B.keep.assign(PAR_BLOCK, 0);
+        }
+      });
+    for (auto& x : th) x.join();
+    th.clear();
+    // dedup: partition t owns the hashes = t mod T, walks the candidates in order
+    for (unsigned t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        for (size_t k = b0; k < blocks.size(); ++k) {
+          Block& B = blocks[k];
+          for (uint32_t i = 0; i < PAR_BLOCK; ++i) {
+            if (B.h[i] % T != t) continue;
+            std::string_view v(B.blob.data() + B.off[i], B.off[i + 1] - B.off[i]);
+            if (part[t].insert(v).second) B.keep[i] = 1;
+          }
+        }
+      });
+    for (auto& x : th) x.join();
+    for (size_t k = b0; k < blocks.size(); ++k) {
+      for (uint32_t i = 0; i < PAR_BLOCK; ++i) have += blocks[k].keep[i];
+      std::vector<uint64_t>().swap(blocks[k].h);
+    }
+    next_block += want;
+  }
+  // the first n unique candidates, in candidate order
+  Strings res;
+  uint64_t total = 0, taken = 0;
+  for (auto& B : blocks)
+    for (uint32_t i = 0; i < PAR_BLOCK && taken < n; ++i)
+      if (B.keep[i]) {
+        total += B.off[i + 1] - B.off[i];
+        ++taken;
+      }
+  if (total > 0xFFFFFFF0ull) return -1;   // offsets are u32 (the C-ABI's egm_table_build)
+  std::vector<std::unordered_set<std::string_view>>().swap(part);
+  res.blob.reserve(total);
+  res.off.reserve((size_t)n + 1);
+  taken = 0;
+  for (auto& B : blocks) {
+    for (uint32_t i = 0; i < PAR_BLOCK && taken < n; ++i)
+      if (B.keep[i]) {
+        res.blob.append(B.blob.data() + B.off[i], B.off[i + 1] - B.off[i]);
+        res.off.push_back((uint32_t)res.blob.size());
+        ++taken;
+      }
+    std::string().swap(B.blob);
+  }
+  return export_strings(res, out);
+}
+
 // n unique filters.  A "wildcard" filter (fraction wc_frac) has each level '+'
 // with p_plus and its last level '#' with p_hash, forced to carry at least one
 // wildcard; the rest are all-literal.  p_empty: a literal level is ''.
 int egs_filters(uint64_t seed, uint32_t n, int dmin, int dmax, double wc_frac, double p_plus, double p_hash,
                 double p_empty, double zipf_s, uint32_t vmax, egs_strings* out) {
   if (!out || dmin < 1 || dmax < dmin) return -1;
+  if (n > PAR_MIN) return egs_filters_par(seed, n, dmin, dmax, wc_frac, p_plus, p_hash, p_empty, zipf_s, vmax, out);
   Rng r(seed);
   Vocab voc(zipf_s, vmax);
   Strings res;
@@ -142,23 +287,7 @@ int egs_filters(uint64_t seed, uint32_t n, int dmin, int dmax, double wc_frac, d
   store.reserve(n);
   while (store.size() < n && attempts < (uint64_t)n * 50) {
     ++attempts;
-    f.clear();
-    int d = r.range(dmin, dmax);
-    bool wild = r.uni() < wc_frac, any = false;
-    for (int l = 0; l < d; ++l) {
-      if (l) f += '/';
-      if (wild && l == d - 1 && (r.uni() < p_hash || !any)) {
-        f += '#';
-        any = true;
-      } else if (wild && r.uni() < p_plus) {
-        f += '+';
-        any = true;
-      } else if (r.uni() < p_empty) {
-        // '' level
-      } else {
-        put_word(f, l, voc.sample(r, l));
-      }
-    }
+    gen_filter(r, voc, f, dmin, dmax, wc_frac, p_plus, p_hash, p_empty);
     store.push_back(f);
     if (!seen.insert(std::string_view(store.back())).second) {
       store.pop_back();
@@ -279,6 +408,31 @@ int egs_subscribers(uint64_t seed, uint32_t n, double lambda, double p_big, uint
   memcpy(*row_out, row.data(), row.size() * 8);
   memcpy(*ids_out, ids.data(), ids.size() * 4);
   *total_out = ids.size();
+  return 0;
+}
+
+// The strings idx[0..m) of a set, in that order (shard tables, samples).
+int egs_subset(const egs_strings* in, const uint32_t* idx, uint32_t m, egs_strings* out) {
+  if (!in || !out || (m && !idx)) return -1;
+  uint64_t total = 0;
+  for (uint32_t k = 0; k < m; ++k) {
+    if (idx[k] >= in->n) return -1;
+    total += in->off[idx[k] + 1] - in->off[idx[k]];
+  }
+  if (total > 0xFFFFFFF0ull) return -1;
+  out->n = m;
+  out->bytes = total;
+  out->blob = (uint8_t*)malloc(total + 16);
+  out->off = (uint32_t*)malloc(((size_t)m + 1) * 4);
+  if (!out->blob || !out->off) return -2;
+  uint64_t o = 0;
+  out->off[0] = 0;
+  for (uint32_t k = 0; k < m; ++k) {
+    const uint32_t a = in->off[idx[k]], len = in->off[idx[k] + 1] - a;
+    memcpy(out->blob + o, in->blob + a, len);
+    o += len;
+    out->off[k + 1] = (uint32_t)o;
+  }
   return 0;
 }
 

@@ -26,6 +26,8 @@ class IndexMap {
   template <class Eq>
   uint32_t find(uint64_t h, Eq eq) const;
   void insert(uint64_t h, uint32_t v);           // caller guarantees absence
+  // from n distinct keys at once (payload = key index), in parallel (egm_bulk.cpp)
+  void bulk_build(const std::vector<uint64_t>& h, unsigned threads);
   template <class Eq>
   bool erase(uint64_t h, Eq eq);
   size_t size() const { return n_; }
@@ -74,6 +76,10 @@ class HostTable {
 
   void relayout();          // BFS renumbering of nodes + edge table rebuild
   void clear();
+  // clear() + insert() of every filter + relayout(), in parallel (egm_bulk.cpp):
+  // ids must be valid and unique, none NONE (validated by the caller).
+  // threads 0 = build_threads().  0, or <0 when the table would be too large.
+  int bulk_build(const uint8_t* blob, const uint32_t* off, uint32_t n, const uint32_t* ids, unsigned threads);
 
   uint64_t n_filters() const { return n_filters_; }
   uint32_t n_nodes_live() const { return n_live_nodes_; }
@@ -131,5 +137,9 @@ class HostTable {
   void edge_rehash(size_t n_buckets);
   uint32_t find_local(const uint8_t* p, uint32_t len, uint64_t h) const;
 };
+
+// worker threads for host-side table work: EGM_BUILD_THREADS, else the usable
+// CPUs (affinity and cgroup quota), at most 64
+unsigned build_threads();
 
 }  // namespace egm

@@ -138,6 +138,57 @@ class ShardExchange:
         return self.merge(counts, parts, sum(self.last_totals), n)              # 5. merge
 
 
+class ShardFanout:
+    """The filter-sharded layout with subscriber fan-out (SURVEY §8e:
+    "Subscriber CSR rows live with their filter's shard").
+
+    One step:
+      1. broadcast the topic batch from rank 0                      [RCCL]
+      2. every rank matches it against its filter shard and expands the
+         matches through ITS subscriber rows (emqx_broker:dispatch/2,
+         apps/emqx/src/emqx_broker.erl:283-308): the deliveries of a topic are
+         the disjoint union over the ranks, and each rank keeps its part where
+         its subscribers' connections are
+      3. reduce the per-topic delivery totals to rank 0 (SUM)       [RCCL]
+         — the N of {ok, N} per topic (emqx_broker.erl:283-295)
+
+    ``local(blob, off, n) -> (delivery_row int64[n+1], overflow)`` is this
+    rank's match + fan-out.  No id or delivery list crosses xGMI: a C4 batch
+    has ~4.6 G deliveries (36 GB), gathering them would be the whole cost.
+    Returns (per-topic delivery totals int64[n]) on rank 0, None elsewhere;
+    ``last_overflow`` is set on every rank when any rank overflowed."""
+
+    def __init__(self, rank: int, world: int, device, local, group=None):
+        self.rank, self.world, self.device, self.local, self.group = rank, world, device, local, group
+        self.last_overflow = False
+        self._bufs = {}
+
+    def step(self, blob=None, off=None, sizes: Optional[Tuple[int, int]] = None):
+        import torch
+        import torch.distributed as dist
+        dev, g = self.device, self.group
+        n, nb = sizes
+        if self.rank != 0:
+            blob = self._bufs.get("blob")
+            if blob is None or blob.numel() < nb:
+                blob = self._bufs["blob"] = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+            off = self._bufs.get("off")
+            if off is None or off.numel() < n + 1:
+                off = self._bufs["off"] = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            blob, off = blob[:nb], off[: n + 1]
+        dist.broadcast(blob, 0, group=g)                                        # 1. topic batch
+        dist.broadcast(off, 0, group=g)
+        drow, ovf = self.local(blob, off, n)                                    # 2. match + own fan-out
+        flag = torch.tensor([1 if ovf else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(flag, group=g)
+        self.last_overflow = bool(flag.item())
+        if self.last_overflow:
+            return None
+        per = (drow[1 : n + 1] - drow[:n]).contiguous()
+        dist.reduce(per, 0, op=dist.ReduceOp.SUM, group=g)                       # 3. totals -> rank 0
+        return per if self.rank == 0 else None
+
+
 def gpu_merge(gm, stream: int, out_row, out_ids):
     """The merge of ShardExchange on rank 0: egm_shard_merge (HIP kernel) into
     caller-owned device buffers out_row int64[n+1] and out_ids int32[cap]."""

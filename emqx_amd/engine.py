@@ -321,6 +321,14 @@ class TableImage:
     def relayout(self):
         self.lib.egm_image_relayout(self.h)
 
+    def bulk_build(self, blob: np.ndarray, off: np.ndarray, ids: Optional[np.ndarray] = None, threads: int = 0):
+        """egm_image_build: the whole image at once (parallel, level by level)."""
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        ids = None if ids is None else np.ascontiguousarray(ids, dtype=np.uint32)
+        rc = self.lib.egm_image_build(self.h, _ptr(blob), _ptr(off), len(off) - 1, _ptr(ids), threads)
+        if rc != 0:
+            raise L.EgmError(rc, "egm_image_build")
+
     def arrays(self) -> dict:
         v = L.egm_image_view()
         assert self.lib.egm_image_get_view(self.h, C.byref(v)) == 0

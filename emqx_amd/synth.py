@@ -40,6 +40,8 @@ def _load():
         lib.egs_subscribers.argtypes = [C.c_uint64, C.c_uint32, C.c_double, C.c_double, C.c_uint32,
                                         C.c_double, C.c_uint32, C.POINTER(C.POINTER(C.c_uint64)),
                                         C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint64)]
+        lib.egs_subset.restype = C.c_int
+        lib.egs_subset.argtypes = [C.POINTER(egs_strings), C.c_void_p, C.c_uint32, C.POINTER(egs_strings)]
         lib.egs_free.argtypes = [C.POINTER(egs_strings)]
         lib.egs_free_ptr.argtypes = [C.c_void_p]
         _lib = lib
@@ -64,9 +66,13 @@ class StringSet:
         return [b[int(o[i]): int(o[i + 1])] for i in range(self.n)]
 
     def subset(self, idx) -> "StringSet":
-        from .engine import pack_strings
-        blob, off = pack_strings([self[int(i)] for i in idx])
-        return StringSet(blob, off)
+        """The strings at idx, in that order (native gather)."""
+        idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        s = egs_strings()
+        rc = _load().egs_subset(C.byref(self.as_struct()), C.c_void_p(idx.ctypes.data), len(idx), C.byref(s))
+        if rc != 0:
+            raise ValueError(f"egs_subset rc={rc}")
+        return _take(s)
 
     def as_struct(self) -> egs_strings:
         s = egs_strings()

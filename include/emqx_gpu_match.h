@@ -284,6 +284,13 @@ int egm_image_insert(egm_image* im, const uint8_t* filter, uint32_t len, uint32_
 /* 0 removed, 1 absent */
 int egm_image_remove(egm_image* im, const uint8_t* filter, uint32_t len);
 void egm_image_relayout(egm_image* im);
+/* The whole image from n filters at once (what egm_table_build does from
+   EGM_BULK_MIN = 65 536 filters on): the image of inserting them in order
+   (first occurrence of a repeat wins) + relayout, built level by level on
+   `threads` host threads (0 = the usable CPUs).  ids NULL = 0..n-1; no id may
+   be NONE. */
+int egm_image_build(egm_image* im, const uint8_t* blob, const uint32_t* offsets, uint32_t n, const uint32_t* ids,
+                    uint32_t threads);
 int egm_image_get_view(egm_image* im, egm_image_view* out);
 /* Records of the image changed since the previous call (sorted, unique
    indices; *_full = the array was rebuilt): what egm_table_commit patches.

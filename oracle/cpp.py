@@ -25,6 +25,8 @@ def _load():
         lib.ot_new.restype = P
         lib.ot_new.argtypes = [C.c_int, C.c_int]
         lib.ot_free.argtypes = [P]
+        lib.ot_set_mode.restype = C.c_int
+        lib.ot_set_mode.argtypes = [P, C.c_int]
         lib.ot_add.argtypes = [P, P, P, C.c_uint32, P]
         lib.ot_remove.argtypes = [P, P, P, C.c_uint32]
         lib.ot_match.restype = C.c_uint64
@@ -62,6 +64,11 @@ class OracleTrie:
         if getattr(self, "h", None):
             self.lib.ot_free(self.h)
             self.h = None
+
+    def set_mode(self, mode: int):
+        """Switch match mode (all-wildcard filter sets only: same trie in both)."""
+        if self.lib.ot_set_mode(self.h, mode) != 0:
+            raise ValueError("ot_set_mode: the filter set has exact filters; build one oracle per mode")
 
     def add(self, blob, off, ids=None):
         off = np.ascontiguousarray(off, dtype=np.uint32)

@@ -285,6 +285,20 @@ void* ot_new(int compact, int mode) {
 
 void ot_free(void* h) { delete (Oracle*)h; }
 
+// Switch the match mode of a built oracle.  Only valid when the trie holds the
+// same filters in both modes, i.e. every filter added is a wildcard filter
+// (mode 1 keeps exact filters out of the trie, emqx_router.erl:118-123);
+// returns -1 otherwise.  Saves building a large all-wildcard oracle twice.
+int ot_set_mode(void* h, int mode) {
+  Oracle* o = (Oracle*)h;
+  if (o->trie.tab.size() && o->mode != mode) {
+    for (const auto& kv : o->ids)
+      if (!wildcard(words(kv.first.data(), kv.first.size()))) return -1;
+  }
+  o->mode = mode;
+  return 0;
+}
+
 // Add filters (ids optional, default = running index).  In mode 1 only
 // wildcard filters enter the trie (emqx_router.erl:118-123); every filter is a
 // route-table key.

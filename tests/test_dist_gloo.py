@@ -86,3 +86,62 @@ def test_topic_slices_cover():
             s = [topic_slice(n, r, w) for r in range(w)]
             assert s[0][0] == 0 and s[-1][1] == n
             assert all(s[i][1] == s[i + 1][0] for i in range(w - 1))
+
+
+def _fanout_worker(rank, world, port, q):
+    """ShardFanout over gloo: each rank matches its filter shard (oracle
+    stand-in for the GPU matcher) and expands through the subscriber rows of
+    ITS filters; only the per-topic delivery totals reach rank 0."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from emqx_amd.dist import ShardFanout
+    f, t = synth.config("c0", n_filters=3000, n_topics=4000)
+    srow, subs = synth.subscribers(f.n, lam=1.0, p_big=0.01, n_big=50, p_share=0.1, seed=5)
+    sh = shard_of(f, world)
+    fl = f.to_list()
+    idx = np.nonzero(sh == rank)[0]
+    o = OracleTrie(True, 1)
+    blob, off = pack_strings([fl[i] for i in idx])
+    o.add(blob, off, idx.astype(np.uint32))
+    per_sub = np.diff(srow).astype(np.int64)
+
+    def local(tb, to, n):
+        row, ids = o.match(tb.numpy(), to.numpy().view(np.uint32), threads=1)
+        dcount = np.zeros(n, np.int64)
+        rid = np.repeat(np.arange(n), np.diff(row).astype(np.int64))
+        np.add.at(dcount, rid, per_sub[ids.astype(np.int64)])
+        drow = np.concatenate([[0], np.cumsum(dcount)])
+        return torch.from_numpy(drow.astype(np.int64)), False
+
+    ex = ShardFanout(rank, world, torch.device("cpu"), local)
+    sizes = (t.n, len(t.blob))
+    if rank == 0:
+        out = ex.step(torch.from_numpy(t.blob.copy()), torch.from_numpy(t.off.view(np.int32).copy()), sizes)
+        q.put(out.numpy())
+    else:
+        assert ex.step(sizes=sizes) is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_fanout_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fanout_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    per = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    f, t = synth.config("c0", n_filters=3000, n_topics=4000)
+    srow, subs = synth.subscribers(f.n, lam=1.0, p_big=0.01, n_big=50, p_share=0.1, seed=5)
+    o = OracleTrie(True, 1)
+    o.add(f.blob, f.off)
+    row, ids = o.match(t.blob, t.off)
+    want = np.zeros(t.n, np.int64)
+    np.add.at(want, np.repeat(np.arange(t.n), np.diff(row).astype(np.int64)),
+              np.diff(srow).astype(np.int64)[ids.astype(np.int64)])
+    assert np.array_equal(per, want) and want.sum() > t.n

@@ -5,14 +5,15 @@ benchmarked but never checked).
   workload: every topic's row total against the C++ oracle (in four parts, so
   no single test is silent for minutes), 200K sampled rows id-exact, and
   determinism of the whole batch through a per-row order-independent checksum.
-* C4-shaped fan-out at 10M filters (20% wildcard, 1+Poisson(1) subscribers,
-  0.1% of filters with 2 000, 10% $share groups): the match rows against the
-  oracle, the delivery row pointers complete, sampled delivery rows
-  element-for-element in emqx_broker:dispatch/2 order
-  (apps/emqx/src/emqx_broker.erl:283-308).
-* C3 at 1M depth-16 filters ('+' p=.35, '#' p=.7): the walk must run in its
-  depth-first regime (pops cut by the stack-room bound, counted by the
-  kernel), sampled rows id-exact in both match modes and all row totals.
+* C4 at its full size: 100M filters with the subscriber table, 1M topics,
+  match + fan-out; the oracle is built as 10 disjoint filter shards of 10M
+  (all row totals, sampled rows id-exact, every delivery row pointer,
+  sampled delivery rows element-for-element in emqx_broker:dispatch/2 order,
+  apps/emqx/src/emqx_broker.erl:283-308).
+* C3 at its full size: 10M depth-16 filters ('+' p=.35, '#' p=.7), both match
+  modes, in the walk's depth-first regime (pops cut by the stack-room bound,
+  counted by the kernel); all row totals, sampled rows id-exact, V_t.
+* C3's $share-group fan-out at 1M filters.
 
 The oracle is the pinned C++ restatement of emqx_trie compact mode
 (oracle/trie_oracle.cpp; apps/emqx/src/emqx_trie.erl:251-266).
@@ -54,7 +55,7 @@ def sampled_rows(res_row, res_ids, idx):
 
 
 # ------------------------------------------------------------------ C2 -------
-@pytest.fixture(scope="module")
+@pytest.fixture(scope="class")
 def c2():
     f, t = synth.config("c2")
     gm = GpuMatcher(0, max_batch=t.n)
@@ -67,38 +68,40 @@ def c2():
     gm.close()
 
 
-@pytest.mark.parametrize("part", range(4))
-def test_c2_full_row_totals(c2, part):
-    t, res, o = c2["t"], c2["res"], c2["o"]
-    lo, hi = t.n * part // 4, t.n * (part + 1) // 4
-    want = o.match_counts(t.blob, t.off[lo:hi + 1], threads=THREADS)   # absolute offsets into one blob
-    got = np.diff(res.row_ptr[lo:hi + 1]).astype(np.uint32)
-    bad = np.nonzero(got != want)[0]
-    assert len(bad) == 0, (len(bad), [(int(lo + i), int(got[i]), int(want[i])) for i in bad[:5]])
+class TestC2Full:
+    """C2 at full size; the class scope frees its 10M-filter table and oracle
+    before the C4/C3 tests build theirs."""
 
+    @pytest.mark.parametrize("part", range(4))
+    def test_c2_full_row_totals(self, c2, part):
+        t, res, o = c2["t"], c2["res"], c2["o"]
+        lo, hi = t.n * part // 4, t.n * (part + 1) // 4
+        want = o.match_counts(t.blob, t.off[lo:hi + 1], threads=THREADS)   # absolute offsets into one blob
+        got = np.diff(res.row_ptr[lo:hi + 1]).astype(np.uint32)
+        bad = np.nonzero(got != want)[0]
+        assert len(bad) == 0, (len(bad), [(int(lo + i), int(got[i]), int(want[i])) for i in bad[:5]])
 
-def test_c2_full_sampled_rows_exact(c2):
-    t, res, o = c2["t"], c2["res"], c2["o"]
-    idx = np.sort(np.random.default_rng(2).choice(t.n, 200_000, replace=False))
-    sub = t.subset(idx)
-    row, ids = o.match(sub.blob, sub.off, threads=THREADS)
-    grow, gids = sampled_rows(res.row_ptr, res.ids, idx)
-    assert np.array_equal(grow, row)
-    assert np.array_equal(canonical(grow, gids), canonical(row, ids))
-    assert int(res.row_ptr[-1]) > 40 * t.n   # ~50 matches per C2 topic
-    # the bench line's V_t (32 B per state of its 22.4 GB model): the sample's
-    # kernel count equals the oracle's independent count
-    vt, _ = o.visited_counts(sub.blob, sub.off, threads=THREADS)
-    assert c2["gm"].match(sub.blob, sub.off, L.EGM_MODE_ROUTES).visited == vt
+    def test_c2_full_sampled_rows_exact(self, c2):
+        t, res, o = c2["t"], c2["res"], c2["o"]
+        idx = np.sort(np.random.default_rng(2).choice(t.n, 200_000, replace=False))
+        sub = t.subset(idx)
+        row, ids = o.match(sub.blob, sub.off, threads=THREADS)
+        grow, gids = sampled_rows(res.row_ptr, res.ids, idx)
+        assert np.array_equal(grow, row)
+        assert np.array_equal(canonical(grow, gids), canonical(row, ids))
+        assert int(res.row_ptr[-1]) > 40 * t.n   # ~50 matches per C2 topic
+        # the bench line's V_t (32 B per state of its 22.4 GB model): the sample's
+        # kernel count equals the oracle's independent count
+        vt, _ = o.visited_counts(sub.blob, sub.off, threads=THREADS)
+        assert c2["gm"].match(sub.blob, sub.off, L.EGM_MODE_ROUTES).visited == vt
 
-
-def test_c2_full_determinism(c2):
-    t, res, gm = c2["t"], c2["res"], c2["gm"]
-    again = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
-    assert np.array_equal(again.row_ptr, res.row_ptr)
-    assert np.array_equal(row_checksums(again.row_ptr, again.ids), row_checksums(res.row_ptr, res.ids))
-    st = gm.walk_counters()
-    assert st["popped"] > 0
+    def test_c2_full_determinism(self, c2):
+        t, res, gm = c2["t"], c2["res"], c2["gm"]
+        again = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+        assert np.array_equal(again.row_ptr, res.row_ptr)
+        assert np.array_equal(row_checksums(again.row_ptr, again.ids), row_checksums(res.row_ptr, res.ids))
+        st = gm.walk_counters()
+        assert st["popped"] > 0
 
 
 # ------------------------------------------------------------------ C4 -------
@@ -111,15 +114,53 @@ def _expected_deliveries(mids, srow, subs):
     return fid.astype(np.uint32), sub.astype(np.uint32)
 
 
-def test_c4_fanout_10m_filters():
+def _oracle_shards(f, n_shards, mode, par=5):
+    """The oracle over f as n_shards disjoint filter ranges (global ids =
+    index), built `par` at a time: a string-keyed oracle of all 100M filters
+    would not fit, and the match set over F is the disjoint union of the sets
+    over its parts."""
+    import threading
+    bounds = [f.n * k // n_shards for k in range(n_shards + 1)]
+    shards = [None] * n_shards
+
+    def build(k):
+        o = OracleTrie(True, mode)
+        lo, hi = bounds[k], bounds[k + 1]
+        o.add(f.blob, f.off[lo:hi + 1], np.arange(lo, hi, dtype=np.uint32))
+        shards[k] = o
+
+    for k0 in range(0, n_shards, par):
+        th = [threading.Thread(target=build, args=(k,)) for k in range(k0, min(n_shards, k0 + par))]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    return shards
+
+
+def test_c4_full_size_match_and_fanout():
+    """BASELINE C4 at its full size: 100M filters (20 %
+    wildcard, depth 4-8) with the subscriber table (1+Poisson(1) subscribers,
+    0.1 % of filters with 2 000, 10 % $share groups), 1M topics, ROUTES mode
+    (emqx_router:match_routes/1) + fan-out (emqx_broker:dispatch/2,
+    apps/emqx/src/emqx_broker.erl:283-324).  Checked against the pinned C++
+    oracle (emqx_trie.erl:251-266) built as 10 disjoint filter shards of 10M:
+    every match row total, 20K rows id-exact, every delivery row pointer and
+    3K delivery rows element for element."""
+    import time
     import torch
-    f, t = synth.config("c4", n_filters=10_000_000, n_topics=1_000_000)
+    t0 = time.time()
+    f, t = synth.config("c4", n_topics=1_000_000)
+    assert f.n == 100_000_000
+    print(f"[c4] generated in {time.time() - t0:.0f}s", flush=True)
     srow, subs = synth.subscribers(f.n, lam=1.0, p_big=0.001, n_big=2000, p_share=0.1,
                                    seed=synth.SEED_BASE + synth.CONFIG_INDEX["c4"])
     gm = GpuMatcher(0, max_batch=t.n)
     try:
+        t0 = time.time()
         gm.build(f.blob, f.off)
         gm.subs_build(srow, subs)
+        print(f"[c4] table + subscribers built in {time.time() - t0:.0f}s: {gm.stats()}", flush=True)
         dev = torch.device("cuda:0")
         s = torch.cuda.current_stream().cuda_stream
         d_blob = torch.from_numpy(t.blob).to(dev)
@@ -134,19 +175,7 @@ def test_c4_fanout_10m_filters():
         assert st["overflow"] == 0 and st["errors"] == 0, st
         mrow = d_row.cpu().numpy().view(np.uint64)
         mids = d_ids[: int(mrow[-1])].cpu().numpy().view(np.uint32)
-        # match rows: all row totals and sampled id sets against the oracle
-        o = OracleTrie(True, L.EGM_MODE_ROUTES)
-        o.add(f.blob, f.off)
-        want_cnt = o.match_counts(t.blob, t.off, threads=THREADS)
-        assert np.array_equal(np.diff(mrow).astype(np.uint32), want_cnt)
-        idx = np.sort(np.random.default_rng(4).choice(n, 20_000, replace=False))
-        sub = t.subset(idx)
-        orow, oids = o.match(sub.blob, sub.off, threads=THREADS)
-        grow, gids = sampled_rows(mrow, mids, idx)
-        assert np.array_equal(grow, orow)
-        assert np.array_equal(canonical(grow, gids), canonical(orow, oids))
-        del o
-        # fan-out
+        # fan-out on the device, checked below
         cnt = (srow[mids.astype(np.int64) + 1] - srow[mids.astype(np.int64)]).astype(np.uint64)
         dpos = np.zeros(len(mids) + 1, np.uint64)
         np.cumsum(cnt, out=dpos[1:])
@@ -160,7 +189,8 @@ def test_c4_fanout_10m_filters():
         torch.cuda.synchronize()
         drow = d_drow.cpu().numpy().view(np.uint64)
         assert np.array_equal(drow, dpos[mrow.astype(np.int64)])   # every delivery row
-        for i in np.random.default_rng(5).choice(n, 3_000, replace=False):
+        rng = np.random.default_rng(5)
+        for i in rng.choice(n, 3_000, replace=False):
             a, b = int(mrow[i]), int(mrow[i + 1])
             wf, ws = _expected_deliveries(mids[a:b], srow, subs)
             lo, hi = int(drow[i]), int(drow[i + 1])
@@ -168,51 +198,102 @@ def test_c4_fanout_10m_filters():
             if hi > lo:
                 assert np.array_equal(d_fid[lo:hi].cpu().numpy().view(np.uint32), wf), i
                 assert np.array_equal(d_sub[lo:hi].cpu().numpy().view(np.uint32), ws), i
-        # shared groups appear as (filter, group) entries, never as members
         grp = d_sub[: min(tot, 50_000_000)].cpu().numpy().view(np.uint32)
-        assert np.count_nonzero(grp & np.uint32(L.GROUP_BIT)) > 0
-    finally:
+        assert np.count_nonzero(grp & np.uint32(L.GROUP_BIT)) > 0   # (filter, group) entries, never members
+        del d_fid, d_sub, d_ids, grp
+        torch.cuda.empty_cache()
         gm.close()
+        gm = None
+        del srow, subs
+        # the oracle, 10 disjoint shards of 10M filters
+        t0 = time.time()
+        shards = _oracle_shards(f, 10, L.EGM_MODE_ROUTES)
+        print(f"[c4] oracle shards built in {time.time() - t0:.0f}s", flush=True)
+        want = np.zeros(n, np.uint64)
+        idx = np.sort(np.random.default_rng(4).choice(n, 20_000, replace=False))
+        sub = t.subset(idx)
+        parts = []
+        for o in shards:
+            want += o.match_counts(t.blob, t.off, threads=THREADS)
+            parts.append(o.match(sub.blob, sub.off, threads=THREADS))
+        print(f"[c4] oracle matched in {time.time() - t0:.0f}s", flush=True)
+        got = np.diff(mrow)
+        bad = np.nonzero(got != want)[0]
+        assert len(bad) == 0, (len(bad), [(int(i), int(got[i]), int(want[i])) for i in bad[:5]])
+        from tests.shard_ref import merge_shard_results
+        orow, oids = merge_shard_results(parts)
+        grow, gids = sampled_rows(mrow, mids, idx)
+        assert np.array_equal(grow, orow)
+        assert np.array_equal(canonical(grow, gids), canonical(orow, oids))
+    finally:
+        if gm is not None:
+            gm.close()
 
 
 # ------------------------------------------------------------------ C3 -------
-@pytest.mark.parametrize("mode", [L.EGM_MODE_TRIE, L.EGM_MODE_ROUTES])
-def test_c3_dense_dfs_regime(mode):
+def test_c3_full_size_dfs_regime_both_modes():
+    """BASELINE C3 at its full size: 10M depth-16 filters
+    ('+' p=.35, '#' p=.7; 116.7M trie nodes), 100K topics, both match modes.
+    The walk must run in its depth-first regime (pops cut by the stack-room
+    bound, counted by the kernel); every row total and 10K rows id-exact
+    against the C++ oracle, and V_t against the oracle's count."""
+    import time
+    t0 = time.time()
+    f, t = synth.config("c3", n_topics=100_000)
+    assert f.n == 10_000_000
+    gm = GpuMatcher(0, max_batch=t.n)
+    try:
+        gm.build(f.blob, f.off)
+        print(f"[c3] generated + built in {time.time() - t0:.0f}s: {gm.stats()}", flush=True)
+        res = {m: gm.match(t.blob, t.off, m) for m in (L.EGM_MODE_TRIE, L.EGM_MODE_ROUTES)}
+        wc = gm.walk_counters()
+        assert wc["bounded"] > 0, wc   # the depth-first regime ran
+    finally:
+        gm.close()
+    t0 = time.time()
+    o = OracleTrie(True, L.EGM_MODE_TRIE)
+    o.add(f.blob, f.off)
+    print(f"[c3] oracle built in {time.time() - t0:.0f}s", flush=True)
+    idx = np.sort(np.random.default_rng(3).choice(t.n, 10_000, replace=False))
+    sub = t.subset(idx)
+    for mode in (L.EGM_MODE_TRIE, L.EGM_MODE_ROUTES):
+        o.set_mode(mode)   # every C3 filter is a wildcard filter: one trie serves both modes
+        r = res[mode]
+        assert r.n_error == 0
+        want = o.match_counts(t.blob, t.off, threads=THREADS)
+        assert np.array_equal(np.diff(r.row_ptr).astype(np.uint32), want), mode
+        row, ids = o.match(sub.blob, sub.off, threads=THREADS)
+        grow, gids = sampled_rows(r.row_ptr, r.ids, idx)
+        assert np.array_equal(grow, row)
+        assert np.array_equal(canonical(grow, gids), canonical(row, ids))
+    assert res[L.EGM_MODE_TRIE].visited == res[L.EGM_MODE_ROUTES].visited == \
+        o.visited_counts(t.blob, t.off, threads=THREADS)[0]
+
+
+def test_c3_share_group_fanout():
+    """bench --config c3's fan-out (1+Poisson(1) subscribers, 10 % of the
+    filters through $share groups g0..g63 of 2-16 members) at 1M filters:
+    every delivery row and 3K rows element for element
+    (apps/emqx/src/emqx_broker.erl:283-308, emqx_shared_sub.erl:120-135)."""
     f, t = synth.config("c3", n_filters=1_000_000, n_topics=200_000)
     gm = GpuMatcher(0, max_batch=t.n)
     try:
         gm.build(f.blob, f.off)
-        res = gm.match(t.blob, t.off, mode)
-        assert res.n_error == 0
-        wc = gm.walk_counters()
-        assert wc["bounded"] > 0, wc   # pops cut by the stack-room bound: the depth-first regime ran
-        o = OracleTrie(True, mode)
-        o.add(f.blob, f.off)
-        want = o.match_counts(t.blob, t.off, threads=THREADS)
-        assert np.array_equal(np.diff(res.row_ptr).astype(np.uint32), want)
-        idx = np.sort(np.random.default_rng(3).choice(t.n, 20_000, replace=False))
-        sub = t.subset(idx)
-        row, ids = o.match(sub.blob, sub.off, threads=THREADS)
-        grow, gids = sampled_rows(res.row_ptr, res.ids, idx)
-        assert np.array_equal(grow, row)
-        assert np.array_equal(canonical(grow, gids), canonical(row, ids))
-        if mode == L.EGM_MODE_ROUTES:
-            # bench --config c3's fan-out: 1+Poisson(1) subscribers, 10% of the
-            # filters through $share groups g0..g63 (2-16 members)
-            srow, subs = synth.subscribers(f.n, lam=1.0, p_big=0.001, n_big=2000, p_share=0.1, groups=64,
-                                           seed=synth.SEED_BASE + synth.CONFIG_INDEX["c3"])
-            gm.subs_build(srow, subs)
-            drow, dfid, dsub = gm.fanout(res)
-            mids = res.ids.astype(np.int64)
-            cnt = (srow[mids + 1] - srow[mids]).astype(np.uint64)
-            dpos = np.zeros(len(mids) + 1, np.uint64)
-            np.cumsum(cnt, out=dpos[1:])
-            assert np.array_equal(drow, dpos[res.row_ptr.astype(np.int64)])
-            for i in np.random.default_rng(6).choice(t.n, 3_000, replace=False):
-                a, b = int(res.row_ptr[i]), int(res.row_ptr[i + 1])
-                wf, ws = _expected_deliveries(res.ids[a:b], srow, subs)
-                lo, hi = int(drow[i]), int(drow[i + 1])
-                assert np.array_equal(dfid[lo:hi], wf) and np.array_equal(dsub[lo:hi], ws), i
-            assert np.count_nonzero(dsub & np.uint32(L.GROUP_BIT)) > 0
+        res = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+        srow, subs = synth.subscribers(f.n, lam=1.0, p_big=0.001, n_big=2000, p_share=0.1, groups=64,
+                                       seed=synth.SEED_BASE + synth.CONFIG_INDEX["c3"])
+        gm.subs_build(srow, subs)
+        drow, dfid, dsub = gm.fanout(res)
+        mids = res.ids.astype(np.int64)
+        cnt = (srow[mids + 1] - srow[mids]).astype(np.uint64)
+        dpos = np.zeros(len(mids) + 1, np.uint64)
+        np.cumsum(cnt, out=dpos[1:])
+        assert np.array_equal(drow, dpos[res.row_ptr.astype(np.int64)])
+        for i in np.random.default_rng(6).choice(t.n, 3_000, replace=False):
+            a, b = int(res.row_ptr[i]), int(res.row_ptr[i + 1])
+            wf, ws = _expected_deliveries(res.ids[a:b], srow, subs)
+            lo, hi = int(drow[i]), int(drow[i + 1])
+            assert np.array_equal(dfid[lo:hi], wf) and np.array_equal(dsub[lo:hi], ws), i
+        assert np.count_nonzero(dsub & np.uint32(L.GROUP_BIT)) > 0
     finally:
         gm.close()

@@ -17,6 +17,6 @@ obj = f"/tmp/egm_kernels_{tag}.o"
 B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-fPIC", "-std=c++17", *flags, "-c",
         os.path.join(B.CSRC, "egm_kernels.hip"), "-o", obj], True)
 B.build_lib()
-objs = [obj] + [os.path.join(B.BUILD, n) for n in ("egm_table.o", "egm_capi.o", "egm_retain.o")]
+objs = [obj] + [os.path.join(B.BUILD, n) for n in ("egm_table.o", "egm_bulk.o", "egm_capi.o", "egm_retain.o")]
 B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-pthread", "-o", out] + objs, True)
 print(out)

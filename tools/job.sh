@@ -58,6 +58,9 @@ for step in "$@"; do
     bench_c1|bench_c3|bench_c4)
       cfg=${step#bench_}
       run "$step" 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$cfg" -o run --output-format csv -- $B --config "$cfg" --steps 10 --warmup 2 --host-e2e off --pipelined off ;;
+    shardfan) run shardfan 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --config c4 --filters 2000000 --topics 1000000 --mode shard --steps 5 --warmup 1 --cpu-baseline off ;;
+    shardleg) run shardleg 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29535 bench.py --sharded-leg on --steps 5 --warmup 1 --cpu-baseline off --host-e2e off --pipelined off ;;
+    slowd) run slowd 1100 python -u -m pytest tests -m "gpu and slow" -x -v --timeout 900 --timeout-method thread --durations=0 ;;
     shard1) run shard1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --mode shard --steps 10 --warmup 2 --cpu-baseline off ;;
     pmc)
       run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off

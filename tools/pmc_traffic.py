@@ -6,12 +6,16 @@ per-launch HBM traffic of the walk kernel, for bench.py's roofline.traffic.
 
 Units and corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and
 WRITE_SIZE are in KiB and count the L2's memory-side requests.  The guide's
-x2 correction applies to wide coalesced streaming reads; the walk reads random
-16-B pieces of 64-B lines, and tools/membench.hip run under the same counter
-(gpurun_out/cal_fetch) shows FETCH_SIZE = 64 B per L2 miss for that shape
-(67.1M random 64-B reads of a 16 MB table at a 76 % miss rate -> 3.27 GB),
-so no factor is applied here.  Each counter is averaged over the k_walk
-dispatches of one run (every dispatch matches the same batch).
+x2 correction applies to reads of whole 128-B lines (a 128-B request is
+tallied at 64 B).  The walk reads 64-B halves of its 128-B edge buckets and
+16-B node records, and tools/granule.hip measured that shape on MI355X
+(profiles/r3_granule.json): a random read of 16, 32 or 64 B costs one 64-B
+fetch and FETCH_SIZE counts it at exactly 64 B (67.1M reads -> 4.26-4.29 GB
+for each width), the memory system serves ~50 G such requests/s whatever the
+width, and a whole 128-B line takes ~1.7x the time of a 64-B half but is
+counted at 64 B.  So the granule is 64 B and no factor applies to the walk.
+Each counter is the median over the k_walk dispatches of one run (every
+dispatch matches the same batch).
 """
 import argparse
 import csv
@@ -49,7 +53,9 @@ def main():
         "dispatches": [len(f), len(w)],
         "traffic_bytes_per_launch": statistics.median(f) + statistics.median(w),
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over bench.py "
-                  "(KiB x 1024; 64 B per L2 miss calibrated with tools/membench.hip)",
+                  "(KiB x 1024; no x2: random reads of <= 64 B are one 64-B fetch each, counted exactly, "
+                  "tools/granule.hip, profiles/r3_granule.json)",
+        "granule_bytes": 64,
     }
     with open(a.out, "w") as fh:
         json.dump(rec, fh, indent=1)
