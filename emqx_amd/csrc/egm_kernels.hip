@@ -249,7 +249,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
   __shared__ uint8_t wtop[TOK_WORDS];    // topic within the segment
   __shared__ uint32_t tg[TOK_BLOCK];     // wid index of the topic's word 0 (a word's level = wdst - tg)
   __shared__ uint32_t kw[TOK_BLOCK][KEY_LEVELS];   // the topic's first word ids (walk-order key)
-  __shared__ uint32_t tflag[TOK_BLOCK];
+  __shared__ uint32_t tflag[TOK_BLOCK];   // TF_* flags | levels << 8
   __shared__ uint32_t wsum[TOK_BLOCK / 64];
   const uint32_t blk0 = blockIdx.x * TOK_BLOCK;
   if (blk0 >= n) return;
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
       t0 = t1;
       continue;
     }
-    tflag[tid] = fl;
+    tflag[tid] = fl | (min(D, 0xFFFFFFu) << 8);
 
     // ---- pass 2: word boundaries ----
     if (t < t1) {
@@ -399,11 +399,15 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         const uint32_t i = i0 + u * TOK_BLOCK;
         if (spec[u]) atomicOr(&tflag[wtop[i]], (uint32_t)TF_WILDCARD);
         else res[u] = dict_resolve(tab, h[u], a[u], b[u], sw, st[u], wl[u]);
-        wid[wdst[i]] = res[u];
         if (wo.key) {
+          // sorted batch: a topic of <= FIX_WORDS levels is read only at the
+          // fixed stride (its record's fixed bit), so wid[] is not written
           const uint32_t tt = wtop[i], l = wdst[i] - tg[tt];
           if (l < KEY_LEVELS) kw[tt][l] = res[u];
-          if (l < FIX_WORDS) wo.wfix[(uint64_t)(t0 + tt) * FIX_WORDS + l] = res[u];
+          if ((tflag[tt] >> 8) <= FIX_WORDS) wo.wfix[(uint64_t)(t0 + tt) * FIX_WORDS + l] = res[u];
+          else wid[wdst[i]] = res[u];
+        } else {
+          wid[wdst[i]] = res[u];
         }
       }
     }
@@ -415,7 +419,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
 #pragma unroll
         for (uint32_t k = 0; k < KEY_LEVELS; ++k) w4[k] = kw[tid][k];
         wo.key[t] = walk_key(w4, D, wo.shape);
-        wo.val[t] = sort_val(t, D, tflag[tid], D <= FIX_WORDS);
+        wo.val[t] = sort_val(t, D, tflag[tid] & 0xFFu, D <= FIX_WORDS);
       }
     }
     __syncthreads();   // tflag, wpos and sw are rewritten by the next segment
@@ -467,6 +471,12 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #ifndef EGM_WALK_WORDS
 #define EGM_WALK_WORDS 448   // staged topic word ids per wave (a chunk's topics, [topic][level])
 #endif
+#ifndef EGM_WALK_TAILS
+#define EGM_WALK_TAILS 0     // 1: a topic's ids reach its fixed block in whole 16-id (64-B) units, the rest held in LDS
+#endif
+#ifndef EGM_WALK_ITEM12
+#define EGM_WALK_ITEM12 0    // 1: stack items of 12 B {node, meta, plus_child}; the word is read from the LDS stage at pop
+#endif
 #ifndef EGM_PROBE_SLOTS
 #define EGM_PROBE_SLOTS 2    // edge slots a literal probe reads up front (2 x 16-B loads each); the rest on a miss
 #endif
@@ -486,15 +496,26 @@ static_assert(WALK_STAGE <= 0xFFFF, "flush slots and spill starts are packed as 
 static_assert(LIGHT_DMAX >= 16, "stack too small");
 
 struct alignas(16) WaveLds {
+#if EGM_WALK_ITEM12
+  uint2 stk_nm[WALK_STACK];          // items: {node, meta}
+  uint32_t stk_plus[WALK_STACK];     //        plus_child
+#else
   uint4 stack[WALK_STACK];
+#endif
   uint32_t stage_fid[WALK_STAGE];
   uint16_t stage_rank[WALK_STAGE];
   uint8_t stage_t[WALK_STAGE];       // topic in chunk of the emit
   uint32_t words[WALK_WORDS];        // the sub-chunk's word ids, [topic][level]
   uint32_t tinfo[WALK_CHUNK];        // D | tflags << 24 | words at the fixed stride << 31
-  uint32_t gbase[WALK_CHUNK];        // the topic's word 0: wid[] index (off[t] + t), or its topic (fixed stride)
   uint32_t cnt[WALK_CHUNK];          // ids per topic, whole chunk
   uint32_t fcnt[WALK_CHUNK];         // ids per topic in the current stage / start inside the flush
+#if EGM_WALK_TAILS
+  uint32_t tail[WALK_CHUNK][16];     // per topic: its ids past the last whole 16-id unit written (fixed block)
+  uint32_t gsc[WALK_CHUNK];          // per topic in a flush: first unit-store slot | first position << 16
+#endif
+#ifdef EGM_AB_LDS_PAD   // measurement only: occupancy A/B (waves per CU) at the same code
+  uint32_t ab_pad[EGM_AB_LDS_PAD / 4];
+#endif
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
@@ -502,6 +523,30 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin
 // half would set the high word of a pointer whose bit 31 is set)
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | (uint64_t)uni((uint32_t)v);
+}
+
+// The LDS work stack.  With 12-B items the word of an item's level is not
+// stored: it is read back from the chunk's word stage at pop (one LDS read
+// beside the item's), which leaves room for more waves per CU.
+__device__ __forceinline__ void push_item(WaveLds& L, uint32_t i, uint4 it) {
+#if EGM_WALK_ITEM12
+  L.stk_nm[i] = make_uint2(it.x, it.y);
+  L.stk_plus[i] = it.z;
+#else
+  L.stack[i] = it;
+#endif
+}
+
+__device__ __forceinline__ uint4 pop_item(const WaveLds& L, uint32_t i, uint32_t S, uint32_t dmax) {
+#if EGM_WALK_ITEM12
+  const uint2 nm = L.stk_nm[i];
+  const uint32_t tt = (nm.y >> MT_SHIFT) & 0x7Fu, level = min(nm.y & LEVEL_MAX, dmax - 1);
+  return make_uint4(nm.x, nm.y, L.stk_plus[i], L.words[(tt & (S - 1)) * dmax + level]);
+#else
+  (void)S;
+  (void)dmax;
+  return L.stack[i];
+#endif
 }
 
 // An unused pieces-slab slot: count 0, skipped by k_compact.
@@ -533,6 +578,7 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
   return r;
 }
 
+#if !EGM_WALK_TAILS
 // Write the stage out.  Entries are ranked within their topic by a
 // conflict-free multi-split (lanes holding the same topic find each other
 // with 6 ballots; one LDS add per topic per 64 entries).  A topic's first
@@ -614,6 +660,111 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
   L.fcnt[lane] = 0;
   wave_sync();
 }
+#endif
+
+#if EGM_WALK_TAILS
+// flush_stage with whole-unit stores.  A topic's first fix_cap ids go to its
+// fixed block in 16-id units (64 B, the memory system's granule, tools/
+// granule.hip): a flush writes only the units it completes — with the ids an
+// earlier flush left in the topic's LDS tail — and keeps the rest in the
+// tail; the chunk's end writes the tails (flush_tails).  Positions [0, W)
+// of a topic with c ids are in HBM, W = min(c & ~15, fix_cap & ~15), and
+// [W, min(c, fix_cap)) in its tail.  Ids past fix_cap spill as pieces.
+__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t my_t, uint32_t lane,
+                                            const MatchWork& w, Slab& sid, Slab& spc) {
+#pragma unroll 1
+  for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {   // rank entries within their topic (as flush_stage)
+    const uint32_t i = i0 + lane;
+    const bool act = i < nstage;
+    const uint32_t tt = act ? L.stage_t[i] : 0u;
+    uint64_t m = __ballot(act);
+#pragma unroll
+    for (uint32_t b = 0; b < 6; ++b) {
+      const bool bit = (tt >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    const uint32_t leader = act ? (uint32_t)__builtin_ctzll(m) : lane;
+    uint32_t old = 0;
+    if (act && lane == leader) old = atomicAdd(&L.fcnt[tt], popc(m));
+    old = __shfl(old, (int)leader, 64);
+    if (act) L.stage_rank[i] = (uint16_t)(old + mbcnt(m));
+  }
+  wave_sync();
+  const uint32_t cap = w.fix_cap, cap16 = cap & ~15u;
+  const uint32_t fl = L.fcnt[lane];   // the chunk's topic `lane`: ids in this flush
+  const uint32_t c0 = L.cnt[lane];    // ... and before it
+  const uint32_t nfix = c0 >= cap ? 0u : min(fl, cap - c0);
+  const uint32_t over = fl - nfix;    // ids past the fixed block: spilled
+  const uint32_t W0 = min(c0 & ~15u, cap16), W1 = min((c0 + fl) & ~15u, cap16);
+  uint32_t tot, ptot, gtot, utot;
+  const uint32_t ex = wave_excl_scan(over, lane, &tot);
+  const uint32_t pex = wave_excl_scan(over ? 1u : 0u, lane, &ptot);
+  const uint32_t gx = wave_excl_scan(fl, lane, &gtot);
+  const uint32_t gs = wave_excl_scan(W1 - W0, lane, &utot);   // unit-store slots of this topic
+  unsigned long long base = 0;
+  bool ok = true;
+  if (tot) {   // wave-uniform
+    base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
+    const unsigned long long pbase =
+        slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
+    ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
+    if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
+    if (over && ok) w.pieces[pbase + pex] = make_uint4(my_t, over, (uint32_t)(base + ex), c0 + nfix);
+  }
+  L.fcnt[lane] = ex | (gx << 16);   // spill start | first slot of its entries in topic order
+  L.gsc[lane] = gs | (W0 << 16);
+  wave_sync();
+  constexpr uint32_t NQ = (WALK_STAGE + 63) / 64;
+  uint32_t qv[NQ];
+#pragma unroll
+  for (uint32_t r = 0; r < NQ; ++r) {
+    const uint32_t i = lane + 64 * r;
+    qv[r] = i < nstage ? (L.fcnt[L.stage_t[i]] >> 16) + L.stage_rank[i] : 0u;
+  }
+  wave_sync();
+#pragma unroll
+  for (uint32_t r = 0; r < NQ; ++r)
+    if (lane + 64 * r < nstage) L.stage_rank[qv[r]] = (uint16_t)(lane + 64 * r);   // now: slot -> entry
+  wave_sync();
+  // the units this flush completes: consecutive lanes store consecutive ids of a unit
+#pragma unroll 1
+  for (uint32_t q = lane; q < utot; q += 64) {
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t step = 32; step >= 1; step >>= 1)
+      if ((k + step) < WALK_CHUNK && (L.gsc[k + step] & 0xFFFFu) <= q) k += step;
+    const uint32_t g = L.gsc[k], pos = (g >> 16) + (q - (g & 0xFFFFu)), c = L.cnt[k];
+    const uint32_t v = pos < c ? L.tail[k][pos & 15u] : L.stage_fid[L.stage_rank[(L.fcnt[k] >> 16) + (pos - c)]];
+    w.ids_fix[(uint64_t)(t0 + k) * cap + pos] = v;
+  }
+  wave_sync();   // the old tail values are read before the new ones overwrite them
+#pragma unroll 1
+  for (uint32_t q = lane; q < nstage; q += 64) {
+    const uint32_t i = L.stage_rank[q], tt = L.stage_t[i], f = L.fcnt[tt], cb = L.cnt[tt];
+    const uint32_t k = cb + (q - (f >> 16));
+    const uint32_t g = L.gsc[tt];
+    const uint32_t nxt = tt + 1 < WALK_CHUNK ? (L.gsc[tt + 1] & 0xFFFFu) : utot;
+    const uint32_t wend = (g >> 16) + (nxt - (g & 0xFFFFu));   // W1 of the topic
+    if (k < wend) continue;                                     // stored in a unit above
+    if (k < cap) L.tail[tt][k & 15u] = L.stage_fid[i];
+    else if (ok) w.ids_tmp[base + (f & 0xFFFFu) + (k - max(cb, cap))] = L.stage_fid[i];
+  }
+  wave_sync();
+  L.cnt[lane] += fl;
+  L.fcnt[lane] = 0;
+  wave_sync();
+}
+
+// The chunk's end: every topic's tail (< 16 ids) to its fixed block.
+__device__ __forceinline__ void flush_tails(WaveLds& L, uint32_t t0, uint32_t lane, const MatchWork& w) {
+  const uint32_t cap = w.fix_cap, c = L.cnt[lane];
+  const uint32_t cf = min(c, cap), W = min(c & ~15u, cap & ~15u);
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k)
+    if (W + k < cf) w.ids_fix[(uint64_t)(t0 + lane) * cap + W + k] = L.tail[lane][k];
+}
+#endif
 
 // Slot search from slot k0 of bucket b on (rare: both first slots hold other keys).
 __device__ __forceinline__ bool edge_probe_from(const DevTable& tab, uint32_t b, int k0, uint32_t node, uint32_t w,
@@ -777,7 +928,12 @@ __device__ __forceinline__ const uint32_t* topic_words(const MatchWork& w, uint3
 // in sub-chunks of S topics with S * dmax <= WALK_WORDS), topics are admitted
 // 64 roots at a time while the stack is short, and the wave pops up to 64
 // items per iteration.
-__global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __restrict__ off, uint32_t n, int mode,
+#ifdef EGM_WALK_WPE   // A/B: ask the compiler for this many waves per SIMD (caps VGPRs)
+#define EGM_WALK_ATTR __attribute__((amdgpu_waves_per_eu(EGM_WALK_WPE)))
+#else
+#define EGM_WALK_ATTR
+#endif
+__global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const uint32_t* __restrict__ off, uint32_t n, int mode,
                                              MatchWork w) {
   __shared__ WaveLds L;
   const uint32_t lane = threadIdx.x;
@@ -815,7 +971,9 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
       D = w.lv[my_t];
       f = w.tfl[my_t];
     }
-    if (lane < nt) L.gbase[lane] = fixed ? my_t : off[my_t] + my_t;   // only words at a variable offset need off[]
+    // lane j's register: topic j's word 0, a wid[] index (off[t] + t) or its topic (fixed
+    // stride); only words at a variable offset need off[] (read by other lanes with a shuffle)
+    const uint32_t gb = lane < nt ? (fixed ? my_t : off[my_t] + my_t) : 0u;
     L.tinfo[lane] = D | (f << 24) | (fixed ? 0x80000000u : 0u);
     L.cnt[lane] = 0;
     L.fcnt[lane] = 0;
@@ -836,9 +994,10 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
     wave_sync();
     for (uint32_t sub = 0; sub < nt; sub += S) {
       const uint32_t end = min(sub + S, nt);
+      const uint32_t gsub = __shfl(gb, (int)min(sub + lane, (uint32_t)WALK_CHUNK - 1), 64);
       if (lane < end - sub) {   // stage the sub-chunk's words: topic j's word 0 at LDS (j % S) * dmax
         const uint32_t j = sub + lane, Dj = L.tinfo[j] & 0xFFFFFFu;
-        const uint32_t* src = topic_words(w, L.tinfo[j], L.gbase[j]);
+        const uint32_t* src = topic_words(w, L.tinfo[j], gsub);
         uint32_t* dst = L.words + lane * dmax;
         uint32_t i = 0;
         for (; i + 4 <= Dj; i += 4) {
@@ -871,10 +1030,11 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
           uint32_t fid = NONE;
           uint4 it = make_uint4(0, 0, 0, 0);
           const uint32_t j = next + lane;
+          const uint32_t gj = __shfl(gb, (int)min(j, (uint32_t)WALK_CHUNK - 1), 64);
           if (lane < k) {
             const uint32_t ti = L.tinfo[j], Dj = ti & 0xFFFFFFu, tf = (ti >> 24) & 0x7Fu;
             if (tf & TF_WILDCARD) {
-              if (mode == MODE_ROUTES) em = exact_walk(tab, topic_words(w, ti, L.gbase[j]), Dj, &fid);
+              if (mode == MODE_ROUTES) em = exact_walk(tab, topic_words(w, ti, gj), Dj, &fid);
             } else {
               const bool dollar = (tf & TF_DOLLAR) != 0;
               em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
@@ -887,7 +1047,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
             }
           }
           const uint64_t b = __ballot(has);
-          if (has) L.stack[sp + mbcnt(b)] = it;
+          if (has) push_item(L, sp + mbcnt(b), it);
           sp += popc(b);
           const uint64_t be = __ballot(em);
           if (em) {
@@ -918,7 +1078,7 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
         popped += take;
         Pend p;
         p.act = lane < take;
-        p.it = L.stack[min(bi + lane, WALK_STACK - 1)];   // unconditional: see issue()
+        p.it = pop_item(L, min(bi + lane, WALK_STACK - 1), S, dmax);   // unconditional: see issue()
         sp = bi;
         const uint32_t tt = (p.it.y >> MT_SHIFT) & 0x7Fu;
         const uint32_t ti = L.tinfo[tt];
@@ -938,8 +1098,8 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
           if (lane == 0) atomicOr(&w.stats->guard, GUARD_STACK);
           break;
         }
-        if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
-        if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;
+        if (o.p0) push_item(L, sp + mbcnt(c0b), o.c0);
+        if (o.p1) push_item(L, sp + m0 + mbcnt(c1b), o.c1);
         sp += nc;
         const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
         const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
@@ -974,6 +1134,9 @@ __global__ __launch_bounds__(64) void k_walk(DevTable tab, const uint32_t* __res
       }
     }
     if (nstage) flush_stage(L, nstage, t0, my_t, lane, w, sid, spc);
+#if EGM_WALK_TAILS
+    flush_tails(L, t0, lane, w);
+#endif
     if (lane < nt) {
       w.cnt[my_t] = L.cnt[lane];
       w.inv[my_t] = t0 + lane;   // its fixed block (k_compact_fix)
@@ -1036,12 +1199,16 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
     if (idx >= total) break;
     const uint32_t pos = w.deferred[idx / WALK_CHUNK] * WALK_CHUNK + idx % WALK_CHUNK;   // in walk order
     if (pos >= n) continue;
-    const uint32_t t = uni(w.order ? (uint32_t)w.order[pos] : pos);
+    const uint64_t rec = w.order ? w.order[pos] : (uint64_t)pos;
+    const uint32_t t = uni((uint32_t)rec);
     if (lane == 0) w.inv[t] = NONE;   // every id of a heavy topic is in its piece (no fixed block)
-    const uint32_t D = uni(w.lv[t]), tf = uni(w.tfl[t]), tb = uni(off[t] + t);
+    // a sorted batch keeps a short topic's words only at the fixed stride (k_tokenise)
+    const bool fixed = w.order && (rec >> 63);
+    const uint32_t* words = fixed ? w.wfix : w.wid;
+    const uint32_t D = uni(w.lv[t]), tf = uni(w.tfl[t]), tb = uni(fixed ? t * FIX_WORDS : off[t] + t);
     if (tf & TF_WILDCARD) {   // no trie walk: TRIE mode matches nothing, ROUTES mode one exact lookup
       uint32_t fid = NONE;
-      const bool em = mode == MODE_ROUTES && exact_walk(tab, w.wid + tb, D, &fid);
+      const bool em = mode == MODE_ROUTES && exact_walk(tab, words + tb, D, &fid);
       if (lane == 0) {
         if (em) {
           const unsigned long long base = atomicAdd(&w.stats->cursor, 1ull);
@@ -1067,7 +1234,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
       continue;
     }
     const bool dollar = (tf & TF_DOLLAR) != 0;
-    const uint32_t w0 = uni(w.wid[tb]);
+    const uint32_t w0 = uni(words[tb]);
     const uint32_t rfl = root_flags(root, dollar, w0);
     const bool rem = (root.w & F_HASH) && !dollar;
     unsigned long long base = 0;
@@ -1099,7 +1266,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
         p.it = ld16_l2(stk + (p.act ? bi + lane : 0u));
         p.D = D;
         p.d1 = D == 1 && (tf & TF_DOLLAR);
-        issue(tab, nullptr, w.wid, tb, p);
+        issue(tab, nullptr, words, tb, p);
         sp = bi;
         Out o;
         finish(tab, mode, p, o);
@@ -1411,7 +1578,8 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   }
   MatchWork w = w_in;
   const uint32_t kbits = min(walk_key_bits(w.key_shape), 32u);
-  const bool sorted = kbits && w.order && n >= SORT_MIN_TOPICS && !(w.debug & DEBUG_INPUT_ORDER);
+  // (fixed-stride word offsets t * FIX_WORDS stay 32-bit below 2^29 topics)
+  const bool sorted = kbits && w.order && n >= SORT_MIN_TOPICS && n < (1u << 29) && !(w.debug & DEBUG_INPUT_ORDER);
   size_t tb = 0;
   if (sorted) {
     tb = walk_sort_temp_bytes(n, w.key_shape);

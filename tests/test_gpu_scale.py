@@ -95,6 +95,53 @@ class TestC2Full:
         vt, _ = o.visited_counts(sub.blob, sub.off, threads=THREADS)
         assert c2["gm"].match(sub.blob, sub.off, L.EGM_MODE_ROUTES).visited == vt
 
+    def test_c2_full_eight_logical_shards_merged(self, c2):
+        """BASELINE C2's sharded layout on one GPU: the
+        10M filters split 8 ways by word_hash(filter) mod 8 with global ids,
+        the whole 10M-topic batch matched against each shard, the shard CSRs
+        merged on the GPU by egm_shard_merge — equal to the whole-table
+        result (every row pointer; every row as a set through a per-row
+        order-independent checksum)."""
+        import torch
+        from emqx_amd.dist import shard_of
+        f, t, res = c2["f"], c2["t"], c2["res"]
+        dev = torch.device("cuda:0")
+        s = torch.cuda.current_stream().cuda_stream
+        d_blob = torch.from_numpy(t.blob).to(dev)
+        d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+        n, G = t.n, 8
+        sh = shard_of(f, G)
+        m = GpuMatcher(0, max_batch=n)
+        cnts, idss = [], []
+        try:
+            for g in range(G):
+                idx = np.nonzero(sh == g)[0].astype(np.uint32)
+                part = f.subset(idx)
+                m.build(part.blob, part.off, idx)
+                row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+                ids = torch.zeros(12 * n, dtype=torch.int32, device=dev)
+                m.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES, s,
+                               row.data_ptr(), ids.data_ptr(), ids.numel())
+                torch.cuda.synchronize()
+                st = m.last_stats()
+                assert st["overflow"] == 0 and st["errors"] == 0, (g, st)
+                cnts.append((row[1:] - row[:-1]).to(torch.int32))
+                idss.append(ids[: int(row[-1].item())].clone())
+                del row, ids
+        finally:
+            m.close()
+        counts = torch.cat(cnts)
+        total = sum(int(x.numel()) for x in idss)
+        out_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        out_ids = torch.zeros(total + 16, dtype=torch.int32, device=dev)
+        c2["gm"].shard_merge(G, n, counts.data_ptr(), [x.data_ptr() for x in idss], total, s, out_row.data_ptr(),
+                             out_ids.data_ptr(), out_ids.numel())
+        torch.cuda.synchronize()
+        row = out_row.cpu().numpy().view(np.uint64)
+        assert np.array_equal(row, res.row_ptr)
+        ids = out_ids[:total].cpu().numpy().view(np.uint32)
+        assert np.array_equal(row_checksums(row, ids), row_checksums(res.row_ptr, res.ids))
+
     def test_c2_full_determinism(self, c2):
         t, res, gm = c2["t"], c2["res"], c2["gm"]
         again = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
