@@ -230,7 +230,7 @@ class ShardLeg:
             del lrow, lsubs
             self.fcap = max(8 * n // max(1, world), 1 << 20)
             self.drow = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-            self.dfid = torch.zeros(self.fcap, dtype=torch.int32, device=dev)
+            self.dpos = torch.zeros(self.cap + 1, dtype=torch.int64, device=dev)   # compact delivery form
             self.dsub = torch.zeros(self.fcap, dtype=torch.int32, device=dev)
             self.ex = ShardFanout(rank, world, dev, self._local_fanout)
         else:
@@ -257,8 +257,8 @@ class ShardLeg:
         self.last_ids = int(st["n_ids"])
         if st["overflow"]:
             return self.row, True
-        self.gm.fanout_device(self.row.data_ptr(), self.ids.data_ptr(), self.cap, nn, self.sp, self.drow.data_ptr(),
-                              self.dfid.data_ptr(), self.dsub.data_ptr(), self.fcap)
+        self.gm.fanout_device_compact(self.row.data_ptr(), self.ids.data_ptr(), self.cap, nn, self.sp,
+                                      self.drow.data_ptr(), self.dpos.data_ptr(), self.dsub.data_ptr(), self.fcap)
         fo = self.gm.last_fanout()
         self.last_deliveries = int(fo["deliveries"])
         return self.drow, bool(fo["overflow"])
@@ -278,18 +278,15 @@ class ShardLeg:
             if not self.ex.last_overflow:
                 return
             if self.fanout:
-                # grow both local buffers from this rank's own counts, in step on every rank
-                mine = torch.tensor([self.last_ids, getattr(self, "last_deliveries", 0)], dtype=torch.int64,
-                                    device=self.dev)
+                # grow both local buffers from this rank's own counts
                 if self.last_ids > self.cap:
                     self.cap = int(self.last_ids * 1.25) + 1024
                     self.ids = torch.zeros(self.cap, dtype=torch.int32, device=self.dev)
+                    self.dpos = torch.zeros(self.cap + 1, dtype=torch.int64, device=self.dev)
                 d = getattr(self, "last_deliveries", 0)
                 if d > self.fcap:
                     self.fcap = int(d * 1.1) + 1024
-                    self.dfid = torch.zeros(self.fcap, dtype=torch.int32, device=self.dev)
                     self.dsub = torch.zeros(self.fcap, dtype=torch.int32, device=self.dev)
-                del mine
                 continue
             tots = self.ex.last_totals
             if tots[self.rank] > self.cap:
@@ -362,6 +359,9 @@ def main():
                     help="also time the host-visible path (pinned staging, H2D, match, D2H) at N=1")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--fanout-form", default="compact", choices=["compact", "pairs"],
+                    help="delivery lists as subscriber ids + each match entry's first delivery "
+                         "(egm_fanout_device_compact), or as (filter, subscriber) pairs (egm_fanout_device)")
     ap.add_argument("--sharded-leg", default="auto", choices=["auto", "on", "off"],
                     help="replicate mode at N>1 (auto) or any N (on): also time the filter-sharded layout "
                          "(BASELINE C2 as worded: broadcast + RCCL gather + GPU merge; with fan-out, fan-out on "
@@ -450,9 +450,12 @@ def main():
     bufs["idss"] = [torch.zeros(bufs["cap"], dtype=torch.int32, device=dev) for _ in range(nbuf)]
     bufs["row"], bufs["ids"] = bufs["rows"][0], bufs["idss"][0]
 
+    compact = args.fanout_form == "compact"
     fcap = max(8 * n, 1 << 20) if fanout else 0
     d_drow = torch.zeros(n + 1, dtype=torch.int64, device=dev) if fanout else None
-    d_fid = torch.zeros(fcap, dtype=torch.int32, device=dev) if fanout else None
+    # compact: each match entry's first delivery (the filter of a delivery), else a filter id per delivery
+    d_fid = (torch.zeros(bufs["cap"] + 1, dtype=torch.int64, device=dev) if compact
+             else torch.zeros(fcap, dtype=torch.int32, device=dev)) if fanout else None
     d_sub = torch.zeros(fcap, dtype=torch.int32, device=dev) if fanout else None
     fan_on = False   # enabled once the id buffer holds a whole match batch
 
@@ -465,8 +468,9 @@ def main():
         gm.match_device(d_blob.data_ptr(), nbytes, d_off.data_ptr(), n, mode, s_i, row.data_ptr(), ids.data_ptr(),
                         bufs["cap"])
         if fan_on:
-            gm.fanout_device(row.data_ptr(), ids.data_ptr(), bufs["cap"], n, s_i, d_drow.data_ptr(),
-                             d_fid.data_ptr(), d_sub.data_ptr(), fcap)
+            fan = gm.fanout_device_compact if compact else gm.fanout_device
+            fan(row.data_ptr(), ids.data_ptr(), bufs["cap"], n, s_i, d_drow.data_ptr(), d_fid.data_ptr(),
+                d_sub.data_ptr(), fcap)
 
     def step():
         if leg is None:
@@ -490,6 +494,8 @@ def main():
             bufs["k"] = 0
             log(f"[rank {rank}] grew id buffers to {bufs['cap']}")
     if fanout and leg is None:
+        if compact:   # the entry offsets follow the (grown) id buffer
+            d_fid = torch.zeros(bufs["cap"] + 1, dtype=torch.int64, device=dev)
         fan_on = True
         bufs["k"] = 0
         step()
@@ -497,8 +503,10 @@ def main():
         need = int(d_drow[n].item())
         if need > fcap:   # k_fan_fill wrote nothing: size the delivery buffers and run again
             fcap = int(need * 1.1) + 1024
-            del d_fid, d_sub
-            d_fid = torch.zeros(fcap, dtype=torch.int32, device=dev)
+            del d_sub
+            if not compact:
+                del d_fid
+                d_fid = torch.zeros(fcap, dtype=torch.int32, device=dev)
             d_sub = torch.zeros(fcap, dtype=torch.int32, device=dev)
             log(f"[rank {rank}] grew delivery buffers to {fcap}")
     for _ in range(args.warmup):
@@ -639,7 +647,10 @@ def main():
             "fanout": ({"deliveries_per_step": deliveries, "subscriber_entries": sub_entries,
                         "fanout_ms": tim["fanout_ms"] / max(1, tim["fanout_launches"]),
                         "deliveries_per_s": deliveries * (1 if shard else world) * args.steps / elapsed,
-                        "bytes_per_launch": 12 * deliveries + 20 * n_ids + 8 * (n + 1)}
+                        "form": args.fanout_form,
+                        # compact: subscriber id read + written, entry offsets; pairs: + a filter id written
+                        "bytes_per_launch": ((8 * deliveries + 28 * n_ids if args.fanout_form == "compact"
+                                              else 12 * deliveries + 20 * n_ids) + 8 * (n + 1))}
                        if fanout else None),
             "pipelined": pipelined,
             "sharded": sharded,

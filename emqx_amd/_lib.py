@@ -107,6 +107,7 @@ SIGNATURES = {
     "egm_subs_build": (C.c_int, [_P, _P, C.c_uint32, _P]),
     "egm_fanout_batch": (C.c_int, [_P, C.POINTER(egm_result), C.POINTER(C.POINTER(egm_delivery))]),
     "egm_fanout_device": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P, _P, C.c_uint64]),
+    "egm_fanout_device_compact": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P, _P, C.c_uint64]),
     "egm_last_fanout": (C.c_int, [_P, _u64p, _u32p]),
     "egm_shard_merge": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, C.POINTER(_P), C.c_uint64, _P, _P, _P,
                                   C.c_uint64]),

@@ -1297,7 +1297,8 @@ int egm_subs_build(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint
 
 static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids, uint64_t mids_len, uint32_t n,
                       hipStream_t s,
-                      uint64_t* d_drow, uint32_t* d_fid, uint32_t* d_sub, uint64_t cap, uint64_t* total) {
+                      uint64_t* d_drow, uint32_t* d_fid, uint32_t* d_sub, uint64_t cap, uint64_t* total,
+                      uint64_t* d_entry_pos = nullptr) {
   uint64_t nids = 0;
   hipError_t e = hipMemcpyAsync(&nids, d_mrow + n, 8, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -1306,7 +1307,8 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   if (nids > mids_len) return c->fail(EGM_E_OVERFLOW, "match row total exceeds the id buffer (overflowed match batch)");
   if ((e = c->f_dc.ensure((nids + 1) * 4)) != hipSuccess) return c->hip_fail(e, "f_dc");
   if ((e = c->f_ds0.ensure((nids + 1) * 8)) != hipSuccess) return c->hip_fail(e, "f_ds0");
-  if ((e = c->f_dpos.ensure((nids + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_dpos");
+  if (!d_entry_pos && (e = c->f_dpos.ensure((nids + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_dpos");
+  uint64_t* dpos = d_entry_pos ? d_entry_pos : c->f_dpos.as<uint64_t>();   // the caller's, in the compact form
   if ((e = c->f_tiles.ensure((scan_tiles((uint32_t)nids) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_tiles");
   if ((e = c->f_ovf.ensure(16)) != hipSuccess) return c->hip_fail(e, "f_ovf");
   SubTable st{c->sub_row.as<uint64_t>(), c->sub_ids.as<uint32_t>(), c->n_fid_slots, c->sub_rp.as<uint4>()};
@@ -1317,7 +1319,7 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   }
   c->work_begin(s);
   e = launch_fanout(st, d_mrow, d_mids, n, nids, d_drow, d_fid, d_sub, cap, c->f_dc.as<uint32_t>(),
-                    c->f_ds0.as<uint64_t>(), c->f_dpos.as<uint64_t>(), c->f_tiles.as<uint64_t>(), c->f_ovf.as<unsigned int>(), s,
+                    c->f_ds0.as<uint64_t>(), dpos, c->f_tiles.as<uint64_t>(), c->f_ovf.as<unsigned int>(), s,
                     c->timing ? evp : nullptr);
   if (c->timing) {
     c->ev_fan.push_back(evp[0]);
@@ -1347,6 +1349,16 @@ int egm_fanout_device(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   if (set_device(c)) return EGM_E_DEVICE;
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
   return run_fanout(c, d_mrow, d_mids, mids_len, n, s, d_drow, d_fid, d_sub, cap, nullptr);
+}
+
+int egm_fanout_device_compact(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids, uint64_t mids_len,
+                              uint32_t n, void* hip_stream, uint64_t* d_drow, uint64_t* d_entry_pos, uint32_t* d_sub,
+                              uint64_t cap) {
+  if (!c || !d_mrow || !d_drow || !d_entry_pos) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  return run_fanout(c, d_mrow, d_mids, mids_len, n, s, d_drow, nullptr, d_sub, cap, nullptr, d_entry_pos);
 }
 
 int egm_fanout_batch(egm_ctx* c, const egm_result* m, egm_delivery** out) {

@@ -42,6 +42,10 @@ constexpr int TOK_LDS = EGM_TOK_LDS;
 #define EGM_TOK_WORDS 2048   // words per tokenise block (9 B of LDS each; 34 KB per block -> 4 blocks per CU)
 #endif
 constexpr int TOK_WORDS = EGM_TOK_WORDS;
+#ifndef EGM_TOK_U
+#define EGM_TOK_U 2          // words per lane whose dictionary probes are in flight together
+#endif
+constexpr int TOK_U = EGM_TOK_U;
 constexpr int SCAN_TILE = 2048;      // counts per scan tile (256 threads x 8)
 
 
@@ -364,12 +368,12 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
     __syncthreads();
 
     // ---- pass 3: hash + dictionary probe, lane per word ----
-    for (uint32_t i0 = tid; i0 < W; i0 += 2 * TOK_BLOCK) {
-      uint32_t st[2], wl[2], res[2];
-      uint64_t h[2];
-      bool act[2], spec[2];
+    for (uint32_t i0 = tid; i0 < W; i0 += TOK_U * TOK_BLOCK) {
+      uint32_t st[TOK_U], wl[TOK_U], res[TOK_U];
+      uint64_t h[TOK_U];
+      bool act[TOK_U], spec[TOK_U];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < TOK_U; ++u) {
         const uint32_t i = i0 + u * TOK_BLOCK;
         act[u] = i < W;
         const uint32_t pw = act[u] ? wpos[i] : 0u;
@@ -386,15 +390,15 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
           }
         }
       }
-      uint4 a[2], b[2];
+      uint4 a[TOK_U], b[TOK_U];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {   // both first-slot reads in flight (unconditional: see issue())
+      for (int u = 0; u < TOK_U; ++u) {   // every first-slot read in flight (unconditional: see issue())
         const uint8_t* sp = (const uint8_t*)(tab.dict + ((act[u] && !spec[u]) ? ((uint32_t)h[u] & tab.dict_mask) : 0u));
         a[u] = ld16(sp);
         b[u] = ld16(sp + 16);
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < TOK_U; ++u) {
         if (!act[u]) continue;
         const uint32_t i = i0 + u * TOK_BLOCK;
         if (spec[u]) atomicOr(&tflag[wtop[i]], (uint32_t)TF_WILDCARD);
@@ -512,6 +516,9 @@ struct alignas(16) WaveLds {
 #if EGM_WALK_TAILS
   uint32_t tail[WALK_CHUNK][16];     // per topic: its ids past the last whole 16-id unit written (fixed block)
   uint32_t gsc[WALK_CHUNK];          // per topic in a flush: first unit-store slot | first position << 16
+#endif
+#ifdef EGM_AB_APPEND
+  uint32_t ab_app;
 #endif
 #ifdef EGM_AB_LDS_PAD   // measurement only: occupancy A/B (waves per CU) at the same code
   uint32_t ab_pad[EGM_AB_LDS_PAD / 4];
@@ -652,10 +659,17 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
 #ifdef EGM_AB_NO_ID_STORES   // measurement only (tools/build_variant.py): the walk without its id stores
     if (L.stage_fid[i] != 0x7FFFFFF1u) continue;
 #endif
+#ifdef EGM_AB_APPEND   // measurement only: the same stores as one contiguous run per flush (rows wrong)
+    if (k < cap) w.ids_fix[(uint64_t)t0 * cap + ((L.ab_app + q) % (WALK_CHUNK * cap))] = L.stage_fid[i];
+#else
     if (k < cap) w.ids_fix[(uint64_t)(t0 + tt) * cap + k] = L.stage_fid[i];
+#endif
     else if (ok) w.ids_tmp[base + (f & 0xFFFFu) + (k - max(cb, cap))] = L.stage_fid[i];
   }
   wave_sync();
+#ifdef EGM_AB_APPEND
+  if (lane == 0) L.ab_app += nstage;
+#endif
   L.cnt[lane] += fl;
   L.fcnt[lane] = 0;
   wave_sync();
@@ -976,6 +990,9 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
     const uint32_t gb = lane < nt ? (fixed ? my_t : off[my_t] + my_t) : 0u;
     L.tinfo[lane] = D | (f << 24) | (fixed ? 0x80000000u : 0u);
     L.cnt[lane] = 0;
+#ifdef EGM_AB_APPEND
+    if (lane == 0) L.ab_app = 0;
+#endif
     L.fcnt[lane] = 0;
     uint32_t dmax = D;
 #pragma unroll
@@ -1715,7 +1732,7 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
         if (s_pre[wave][k + b] <= q) k += b;
       const uint32_t o = q - s_pre[wave][k];
       const uint64_t d = base + s_off[wave][k] + o;
-      dfid[d] = s_fid[wave][k];
+      if (dfid) dfid[d] = s_fid[wave][k];   // null: the compact form (the entry offsets give the filter)
       dsub[d] = st.subs[s_src[wave][k] + o];
     }
     // big entries (C4: 2 000-subscriber filters): the wave streams the row, 4 per lane in flight
@@ -1730,7 +1747,7 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (j0 + 64u * r < cnt) {
-            dfid[dst + j0 + 64u * r] = f;
+            if (dfid) dfid[dst + j0 + 64u * r] = f;
             dsub[dst + j0 + 64u * r] = v[r];
           }
       }

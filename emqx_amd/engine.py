@@ -284,6 +284,12 @@ class GpuMatcher:
         self._check(self.lib.egm_fanout_device(self.ctx, d_mrow, d_mids, mids_len, n, stream or None, d_drow,
                                                d_fid, d_sub, cap), "egm_fanout_device")
 
+    def fanout_device_compact(self, d_mrow: int, d_mids: int, mids_len: int, n: int, stream: int, d_drow: int,
+                              d_entry_pos: int, d_sub: int, cap: int):
+        """egm_fanout_device_compact: subscriber ids only + each match entry's first delivery."""
+        self._check(self.lib.egm_fanout_device_compact(self.ctx, d_mrow, d_mids, mids_len, n, stream or None, d_drow,
+                                                       d_entry_pos, d_sub, cap), "egm_fanout_device_compact")
+
     def last_fanout(self) -> dict:
         """Delivery total of the last fan-out and whether its buffers were too small."""
         tot, ovf = C.c_uint64(), C.c_uint32()

@@ -209,6 +209,16 @@ int egm_fanout_batch(egm_ctx* ctx, const egm_result* matched, egm_delivery** out
 int egm_fanout_device(egm_ctx* ctx, const uint64_t* d_match_row, const uint32_t* d_match_ids,
                       uint64_t match_ids_len, uint32_t n_topics, void* hip_stream, uint64_t* d_deliv_row, uint32_t* d_fid,
                       uint32_t* d_sub, uint64_t deliv_cap);
+/* The compact form of egm_fanout_device: only the subscriber ids are written
+   (4 B per delivery instead of 8), and d_entry_pos[match_ids + 1] receives
+   each match entry's first delivery — so delivery k of match entry i, i.e.
+   of filter d_match_ids[i], is d_sub[d_entry_pos[i] + k]; a topic's
+   deliveries are its match row's entries' in order (d_deliv_row as above).
+   The same delivery lists as the pair form, half the bytes written (C4 writes
+   ~4.6 G deliveries per 10M-topic batch). */
+int egm_fanout_device_compact(egm_ctx* ctx, const uint64_t* d_match_row, const uint32_t* d_match_ids,
+                              uint64_t match_ids_len, uint32_t n_topics, void* hip_stream, uint64_t* d_deliv_row,
+                              uint64_t* d_entry_pos, uint32_t* d_sub, uint64_t deliv_cap);
 /* Synchronises the last fan-out and reports its delivery total and whether
    deliv_cap was too small (overflow != 0: d_fid/d_sub were not written;
    rerun with deliv_cap >= n_deliveries). */

@@ -474,6 +474,17 @@ def test_fanout_device_exact_and_guarded(gm):
     assert np.array_equal(drow, want_row)
     assert np.array_equal(d_fid.cpu().numpy().view(np.uint32)[:tot], want_fid)
     assert np.array_equal(d_sub.cpu().numpy().view(np.uint32)[:tot], want_sub)
+    # the compact form: subscriber ids only + each match entry's first delivery
+    d_pos = torch.zeros(len(mids) + 1, dtype=torch.int64, device=dev)
+    d_sub2 = torch.zeros(tot + 8, dtype=torch.int32, device=dev)
+    d_drow2 = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    gm.fanout_device_compact(d_row.data_ptr(), d_ids.data_ptr(), cap, n, s, d_drow2.data_ptr(), d_pos.data_ptr(),
+                             d_sub2.data_ptr(), tot + 8)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_drow2.cpu().numpy().view(np.uint64), want_row)
+    assert np.array_equal(d_pos.cpu().numpy().view(np.uint64), np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint64))
+    assert np.array_equal(d_sub2.cpu().numpy().view(np.uint32)[:tot], want_sub)
+    assert gm.last_fanout() == {"deliveries": tot, "overflow": 0}
     # the host-buffer API gives the same rows
     hrow, hfid, hsub = gm.fanout(host)
     assert int(hrow[-1]) == tot
