@@ -136,6 +136,16 @@ def main():
                 # the non-'$' live topics are contiguous only if '$' words sort together; count it as one read
                 stack.append((plus, lvl + 1, int(pr[3]), int(pr[0]), nd[0], nd[-1] + 1))
     n = nch * 64
+    for cn in (0, 32, 64, 128, 256):
+        tot_it = tot_r = tot_l = tot_h = 0
+        for s0 in starts[:100]:
+            ch = [ti for ti in order[s0:s0 + 64] if b"+" not in topics[ti] and b"#" not in topics[ti]]
+            W = [wids[ti] for ti in ch]
+            dol = [topics[ti][:1] == b"$" for ti in ch]
+            i_, r_, l_, h_ = emulate_wave(nodes, edge, W, dol, cache_n=cn)
+            tot_it += i_; tot_r += r_; tot_l += l_; tot_h += h_
+        print(f"per-topic walk, cache {cn}: iterations/chunk {tot_it / 100:.1f}, reads/topic {tot_r / 6400:.1f}, "
+              f"lines after merging/topic {tot_l / 6400:.1f}, cache hits/topic {tot_h / 6400:.1f}", flush=True)
     print(f"prefix-group walk per topic: literal probes {grp['lit'] / n:.2f}, '+' reads {grp['plus'] / n:.2f}, "
           f"range emits {grp['emits'] / n:.2f} covering {grp['ids'] / n:.1f} ids")
     tot = dict(lit=0, lit_lines=0, plus=0, plus_lines=0, states=0, lit_fail=0, lit_keys=0, plus_keys=0)
@@ -185,6 +195,69 @@ def main():
     print("level: [literal probes, '+' reads, failed probes] per topic")
     for l in sorted(by_level):
         print(l, [round(x / n, 2) for x in by_level[l]])
+
+
+
+def emulate_wave(nodes, edge_fn, W, dollar, S=32, stack_cap=320, cache_n=0):
+    """The per-topic walk of k_walk (round 2) over one chunk, iteration by
+    iteration: sub-chunks of S topics admitted at once, up to 64 items popped
+    LIFO (bounded by room - dmax), literal children pushed before '+'
+    children.  Returns (iterations, lane reads, distinct lines per iteration
+    summed (what the CU's merging leaves), reads a direct-mapped per-wave cache
+    of cache_n entries would have served)."""
+    dmax = max(len(w) for w in W)
+    it = reads = lines = hits = 0
+    cache = {}
+    for s0 in range(0, len(W), S):
+        stack = []
+        for j in range(s0, min(s0 + S, len(W))):
+            r = nodes[0]
+            stack.append((0, 0, int(r[3]), int(r[0]), j))
+        while stack:
+            room = stack_cap - len(stack)
+            take = min(64, len(stack), room - dmax if room > dmax else 1)
+            pop = stack[len(stack) - take:]
+            del stack[len(stack) - take:]
+            it += 1
+            ln = set()
+            c0, c1 = [], []
+            for (node, lvl, fl, plus, j) in pop:
+                w = W[j]
+                if lvl == len(w):
+                    continue
+                rootd = lvl == 0 and dollar[j]
+                wd = w[lvl]
+                for kind, key in ((0, (node, wd)), (1, plus)):
+                    if kind == 0 and not ((fl & F_LIT) and wd < WID_MAX and (fl & sig_bit(wd))):
+                        continue
+                    if kind == 1 and not ((fl & F_PLUS) and not rootd):
+                        continue
+                    reads += 1
+                    line = ("b", key) if kind == 0 else ("p", key >> 2)
+                    if cache_n:
+                        slot = hash(line) % cache_n
+                        if cache.get(slot) == line and line not in ln:
+                            hits += 1
+                        cache[slot] = line
+                    ln.add(line)
+                    if kind == 0:
+                        c, cfl, cplus, _ = edge_fn(node, wd)
+                        if c != NONE and lvl + 1 < len(w) + 1:
+                            c0.append((c, lvl + 1, cfl, cplus, j))
+                    else:
+                        pr = nodes[key]
+                        c1.append((key, lvl + 1, int(pr[3]), int(pr[0]), j))
+            lines += len(ln)
+
+            def go(x):   # pushed only with a transition left to take (finish())
+                node, lvl, fl, plus, j = x
+                if lvl >= len(W[j]):
+                    return False
+                wd = W[j][lvl]
+                return bool((fl & F_PLUS) or ((fl & F_LIT) and wd < WID_MAX and (fl & sig_bit(wd))))
+            stack.extend(x for x in c0 if go(x))
+            stack.extend(x for x in c1 if go(x))
+    return it, reads, lines, hits
 
 
 if __name__ == "__main__":
