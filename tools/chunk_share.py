@@ -144,8 +144,13 @@ def main():
             dol = [topics[ti][:1] == b"$" for ti in ch]
             i_, r_, l_, h_ = emulate_wave(nodes, edge, W, dol, cache_n=cn)
             tot_it += i_; tot_r += r_; tot_l += l_; tot_h += h_
+            tot_x = globals().get("TOT_X", 0) + EXACT
+            globals()["TOT_X"] = tot_x
         print(f"per-topic walk, cache {cn}: iterations/chunk {tot_it / 100:.1f}, reads/topic {tot_r / 6400:.1f}, "
-              f"lines after merging/topic {tot_l / 6400:.1f}, cache hits/topic {tot_h / 6400:.1f}", flush=True)
+              f"lines after merging/topic {tot_l / 6400:.1f} (same address only {globals().get('TOT_X', 0) / 6400:.1f}), "
+              f"cache hits/topic {tot_h / 6400:.1f}", flush=True)
+        globals()["TOT_X"] = 0
+        break
     print(f"prefix-group walk per topic: literal probes {grp['lit'] / n:.2f}, '+' reads {grp['plus'] / n:.2f}, "
           f"range emits {grp['emits'] / n:.2f} covering {grp['ids'] / n:.1f} ids")
     tot = dict(lit=0, lit_lines=0, plus=0, plus_lines=0, states=0, lit_fail=0, lit_keys=0, plus_keys=0)
@@ -207,6 +212,8 @@ def emulate_wave(nodes, edge_fn, W, dollar, S=32, stack_cap=320, cache_n=0):
     of cache_n entries would have served)."""
     dmax = max(len(w) for w in W)
     it = reads = lines = hits = 0
+    global EXACT
+    EXACT = 0
     cache = {}
     for s0 in range(0, len(W), S):
         stack = []
@@ -220,6 +227,7 @@ def emulate_wave(nodes, edge_fn, W, dollar, S=32, stack_cap=320, cache_n=0):
             del stack[len(stack) - take:]
             it += 1
             ln = set()
+            ex = set()
             c0, c1 = [], []
             for (node, lvl, fl, plus, j) in pop:
                 w = W[j]
@@ -240,6 +248,7 @@ def emulate_wave(nodes, edge_fn, W, dollar, S=32, stack_cap=320, cache_n=0):
                             hits += 1
                         cache[slot] = line
                     ln.add(line)
+                    ex.add((kind, key))
                     if kind == 0:
                         c, cfl, cplus, _ = edge_fn(node, wd)
                         if c != NONE and lvl + 1 < len(w) + 1:
@@ -248,6 +257,7 @@ def emulate_wave(nodes, edge_fn, W, dollar, S=32, stack_cap=320, cache_n=0):
                         pr = nodes[key]
                         c1.append((key, lvl + 1, int(pr[3]), int(pr[0]), j))
             lines += len(ln)
+            EXACT += len(ex)
 
             def go(x):   # pushed only with a transition left to take (finish())
                 node, lvl, fl, plus, j = x

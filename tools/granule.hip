@@ -24,11 +24,12 @@ __device__ __forceinline__ uint64_t mix(uint64_t x) {
   return x;
 }
 
-template <int K, int W16, int S16, int G = 1>
+template <int K, int W16, int S16, int G = 1, bool STRIDED = false>
 __global__ __launch_bounds__(64) void k_granule(const uint4* __restrict__ t, uint64_t nslots, int iters,
                                                 uint32_t* out) {
-  // G lanes in a row read the same slot (G = 64: the whole wave one line per read)
-  const uint64_t gid = blockIdx.x * 64ull + threadIdx.x / G;
+  // G lanes read the same slot (G = 64: the whole wave one line per read):
+  // G lanes in a row, or (STRIDED) lanes 64/G apart
+  const uint64_t gid = blockIdx.x * 64ull + (STRIDED ? threadIdx.x % (64 / G) : threadIdx.x / G);
   uint32_t acc = 0;
   for (int i = 0; i < iters; ++i) {
     uint4 v[K][W16];
@@ -46,25 +47,25 @@ __global__ __launch_bounds__(64) void k_granule(const uint4* __restrict__ t, uin
   if (acc == 0x12345678u) out[0] = acc;
 }
 
-template <int K, int W16, int S16, int G = 1>
+template <int K, int W16, int S16, int G = 1, bool STRIDED = false>
 static void run(const uint4* t, uint64_t bytes, int blocks, int iters, uint32_t* out) {
   const uint64_t nslots = bytes / (16 * S16);
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  hipLaunchKernelGGL((k_granule<K, W16, S16, G>), dim3(blocks), dim3(64), 0, 0, t, nslots, 1, out);   // warm
+  hipLaunchKernelGGL((k_granule<K, W16, S16, G, STRIDED>), dim3(blocks), dim3(64), 0, 0, t, nslots, 1, out);   // warm
   hipEventRecord(a);
-  hipLaunchKernelGGL((k_granule<K, W16, S16, G>), dim3(blocks), dim3(64), 0, 0, t, nslots, iters, out);
+  hipLaunchKernelGGL((k_granule<K, W16, S16, G, STRIDED>), dim3(blocks), dim3(64), 0, 0, t, nslots, iters, out);
   hipEventRecord(b);
   hipEventSynchronize(b);
   float ms = 0;
   hipEventElapsedTime(&ms, a, b);
   const double reads = (double)blocks * 64 * iters * K;
   const double warm_reads = (double)blocks * 64 * 1 * K;
-  printf("{\"kernel\": \"k_granule<%d, %d, %d, %d>\", \"read_bytes\": %d, \"slot_bytes\": %d, \"K\": %d, "
-         "\"lanes_per_line\": %d, \"reads_timed\": %.0f, \"reads_per_dispatch\": [%.0f, %.0f], \"ms\": %.3f, "
+  printf("{\"kernel\": \"k_granule<%d, %d, %d, %d, %d>\", \"read_bytes\": %d, \"slot_bytes\": %d, \"K\": %d, "
+         "\"lanes_per_line\": %d, \"strided\": %d, \"reads_timed\": %.0f, \"reads_per_dispatch\": [%.0f, %.0f], \"ms\": %.3f, "
          "\"G_reads_per_s\": %.2f, \"GB_per_s_read\": %.1f}\n",
-         K, W16, S16, G, 16 * W16, 16 * S16, K, G, reads, warm_reads, reads, ms, reads / ms / 1e6,
+         K, W16, S16, G, (int)STRIDED, 16 * W16, 16 * S16, K, G, (int)STRIDED, reads, warm_reads, reads, ms, reads / ms / 1e6,
          reads * 16 * W16 / ms / 1e6);
   hipEventDestroy(a);
   hipEventDestroy(b);
@@ -93,6 +94,11 @@ int main() {
   run<4, 4, 4, 16>(t, big, blocks, iters, out);
   run<4, 4, 4, 64>(t, big, blocks, iters, out);
   run<4, 1, 4, 64>(t, big, blocks, iters, out);
+  // the same sharing with the sharing lanes spread over the wave (a walk's
+  // duplicates are not in adjacent lanes)
+  run<4, 4, 4, 4, true>(t, big, blocks, iters, out);
+  run<4, 4, 4, 16, true>(t, big, blocks, iters, out);
+  run<4, 1, 4, 4, true>(t, big, blocks, iters, out);
   hipDeviceSynchronize();
   return 0;
 }
