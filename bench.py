@@ -7,6 +7,10 @@ GPUs, with the HBM-roofline fraction of the dominant kernel.
 A *step* is one pass of the hot path — tokenise + NFA walk (+ heavy path) +
 CSR finalisation, i.e. emqx_router:match_routes/1's filter sets for a whole
 batch — over one batch of synthetic topics already resident in HBM.
+Consecutive steps alternate over two HIP streams with their own workspaces
+(one batch's sort, scan and compaction run beside the next one's walk), as a
+server keeps two batches in flight; the same steps one batch at a time on one
+stream are timed after them and reported as the line's `serial`.
 
 Layouts (emqx_amd/dist.py), named in the line's config.workload:
   replicate (default)  every GPU holds the 10M-filter table and matches its own
@@ -340,9 +344,10 @@ def main():
     ap.add_argument("--match", default="routes", choices=["routes", "trie"])
     ap.add_argument("--fanout", default="auto", choices=["auto", "on", "off"],
                     help="add emqx_broker:dispatch/2 subscriber fan-out to each step (auto: on for c3, c4)")
-    ap.add_argument("--streams", type=int, default=1,
+    ap.add_argument("--streams", type=int, default=0,
                     help="replicate mode: consecutive batches alternate over this many HIP streams (each with its "
-                         "own match workspace), so one batch's compaction overlaps the next one's walk")
+                         "own match workspace), so one batch's compaction overlaps the next one's walk "
+                         "(0 = auto: 2 without fan-out, else 1; the other setting is timed beside it)")
     ap.add_argument("--x-presort", type=int, default=-1,
                     help="experiment: sort the batch's topics on the host (untimed) by their first K levels "
                          "(0: whole topic) to measure how much trie-path locality between neighbouring topics "
@@ -353,8 +358,9 @@ def main():
                          "input order; EGM_FIX_CAP: ids per fixed block) and check "
                          "that every order gives the same rows (stderr)")
     ap.add_argument("--pipelined", default="on", choices=["on", "off"],
-                    help="after the timed steps, time them again with consecutive batches over two streams "
-                         "(replicate mode, no fan-out; reported as the line's `pipelined`)")
+                    help="after the timed steps, time them again in the other stream setting: one stream "
+                         "(`serial`) after two, two streams (`pipelined`) after --streams 1 (replicate mode, "
+                         "no fan-out)")
     ap.add_argument("--host-e2e", default="on", choices=["on", "off"],
                     help="also time the host-visible path (pinned staging, H2D, match, D2H) at N=1")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
@@ -413,8 +419,9 @@ def main():
 
     gm = GpuMatcher(local, max_batch=nt)
     t0 = time.time()
-    nstreams = 1 if shard else max(1, args.streams)
+    nstreams = 1 if (shard or fanout) else (args.streams if args.streams > 0 else 2)
     piped = args.pipelined == "on" and not shard and not fanout and nstreams == 1
+    serial_leg = args.pipelined == "on" and not shard and not fanout and nstreams > 1
     nbuf = 2 if piped else nstreams
     streams = [torch.cuda.Stream(dev) for _ in range(nbuf)]
     stream = streams[0]
@@ -555,7 +562,29 @@ def main():
         ti = gm.get_timing()
         iso_ms = ti["walk_ms"] / max(1, ti["walk_launches"])
         gm.set_timing(False)
-    pipelined = None
+    pipelined = serial = None
+    if serial_leg:
+        # the same steps one batch at a time on one stream (nothing overlaps):
+        # reported beside `value`
+        bufs["ns"], bufs["k"] = 1, 0
+        for _ in range(2):
+            run_local()
+        if have_pg:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run_local()
+        torch.cuda.synchronize(dev)
+        pe = time.perf_counter() - t0
+        if have_pg:
+            dist.barrier()
+            e = torch.tensor([pe], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            pe = float(e.item())
+        serial = {"streams": 1, "value": n * world * args.steps / pe, "ms_per_step": pe / args.steps * 1e3,
+                  "note": "same steps, one batch at a time on one HIP stream"}
+        bufs["ns"], bufs["k"] = nstreams, 0
     if piped:
         # the same steps with consecutive batches alternating over two streams,
         # so one batch's bandwidth-bound kernels (sort, scan, compaction) run
@@ -653,6 +682,7 @@ def main():
                                               else 12 * deliveries + 20 * n_ids) + 8 * (n + 1))}
                        if fanout else None),
             "pipelined": pipelined,
+            "serial": serial,
             "sharded": sharded,
             "xgmi_model": (shard_cost_model(n, nbytes, world, merged_ids) if shard else None),
             "host_e2e": host,
