@@ -7,10 +7,11 @@ GPUs, with the HBM-roofline fraction of the dominant kernel.
 A *step* is one pass of the hot path — tokenise + NFA walk (+ heavy path) +
 CSR finalisation, i.e. emqx_router:match_routes/1's filter sets for a whole
 batch — over one batch of synthetic topics already resident in HBM.
-Consecutive steps alternate over two HIP streams with their own workspaces
-(one batch's sort, scan and compaction run beside the next one's walk), as a
-server keeps two batches in flight; the same steps one batch at a time on one
-stream are timed after them and reported as the line's `serial`.
+The steps run one batch at a time on one HIP stream, so the walk's HIP-event
+time is its own (the roofline's kernel time); the same steps with two batches
+in flight (two streams with their own workspaces: one batch's sort, scan and
+compaction beside the next one's walk) are timed after them and reported as
+the line's `pipelined` (`--streams 2` makes that the timed mode instead).
 
 Layouts (emqx_amd/dist.py), named in the line's config.workload:
   replicate (default)  every GPU holds the 10M-filter table and matches its own
@@ -347,7 +348,7 @@ def main():
     ap.add_argument("--streams", type=int, default=0,
                     help="replicate mode: consecutive batches alternate over this many HIP streams (each with its "
                          "own match workspace), so one batch's compaction overlaps the next one's walk "
-                         "(0 = auto: 2 without fan-out, else 1; the other setting is timed beside it)")
+                         "(0 = 1; the other setting is timed beside it)")
     ap.add_argument("--x-presort", type=int, default=-1,
                     help="experiment: sort the batch's topics on the host (untimed) by their first K levels "
                          "(0: whole topic) to measure how much trie-path locality between neighbouring topics "
@@ -419,7 +420,7 @@ def main():
 
     gm = GpuMatcher(local, max_batch=nt)
     t0 = time.time()
-    nstreams = 1 if (shard or fanout) else (args.streams if args.streams > 0 else 2)
+    nstreams = 1 if (shard or fanout) else max(1, args.streams)
     piped = args.pipelined == "on" and not shard and not fanout and nstreams == 1
     serial_leg = args.pipelined == "on" and not shard and not fanout and nstreams > 1
     nbuf = 2 if piped else nstreams
