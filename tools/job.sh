@@ -83,6 +83,10 @@ for step in "$@"; do
     c4m_*)  # the same on variant V (tools/build_variant.py)
       v=${step#c4m_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 400 python $R/bench.py --config c4 --filters 10000000 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
+    c3_*)   # C3 on variant V (tools/build_variant.py)
+      v=${step#c3_}
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 python $R/bench.py --config c3 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
+    c3base) run c3base 600 python $R/bench.py --config c3 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
     tests_*)   # the fast GPU tests on variant V
       v=${step#tests_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 900 python -u -m pytest tests -m "gpu and not slow" -x -v --timeout 300 --timeout-method thread ;;
