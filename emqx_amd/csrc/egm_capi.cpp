@@ -589,7 +589,7 @@ static int ensure_work(egm_ctx* c, MatchWs& W, uint32_t n, uint64_t blob_bytes, 
   W.ids_tmp_cap = W.ids_tmp.cap / 4;
   if ((e = W.pieces.ensure(pieces_capacity(ids_cap, n) * 16)) != hipSuccess) return c->hip_fail(e, "pieces");
   W.pieces_cap = std::min<uint64_t>(W.pieces.cap / 16, 0xFFFFFFF0ull);
-  if ((e = W.deferred.ensure((n / WALK_CHUNK + 2) * 4)) != hipSuccess) return c->hip_fail(e, "deferred");
+  if ((e = W.deferred.ensure((n / WALK_CHUNK + 2) * 4 * 2)) != hipSuccess) return c->hip_fail(e, "deferred");
   const uint32_t hcap = heavy_stack_items(max_levels);
   if ((e = W.heavy_stack.ensure((uint64_t)c->heavy_waves * hcap * 16)) != hipSuccess)
     return c->hip_fail(e, "heavy stack");
@@ -625,6 +625,7 @@ static MatchWork work_view(egm_ctx* c, MatchWs& W) {
   w.pieces = W.pieces.as<uint4>();
   w.pieces_cap = W.pieces_cap;
   w.deferred = W.deferred.as<uint32_t>();
+  w.deep = w.deferred + W.deferred.cap / 8;   // the second half: the walk's deep-pass list
   w.heavy_stack = W.heavy_stack.as<uint4>();
   w.heavy_waves = c->heavy_waves;
   w.heavy_cap = W.heavy_cap;

@@ -36,6 +36,8 @@ struct MatchStats {               // device-side counters, zeroed per batch
   unsigned long long bounded;     // walk iterations whose pop was cut by the stack-room bound (DFS regime)
   unsigned long long lit_probes;  // walk pops that read an edge bucket (instrumentation)
   unsigned long long plus_reads;  // walk pops that read a '+' child's record (instrumentation)
+  unsigned int n_deep;            // chunks handed to the deep pass of the walk (more than DEEP_MIN levels)
+  unsigned int pad2_;
 };
 
 // A piece is one flush's run of a topic's spilled ids in ids_tmp:
@@ -60,6 +62,7 @@ struct MatchWork {                // per-batch device workspace
   uint4* pieces;                  // [pieces_cap]
   uint64_t pieces_cap;
   uint32_t* deferred;             // [n / CHUNK + 1] chunk ids for the heavy kernel
+  uint32_t* deep;                 // [n / CHUNK + 1] chunk ids for the walk's deep pass
   uint4* heavy_stack;             // [heavy_waves * heavy_cap] work stacks of the heavy waves
   uint32_t heavy_waves;
   uint32_t heavy_cap;             // items per heavy wave (>= deepest possible topic + 192)

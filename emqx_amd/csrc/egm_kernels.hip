@@ -467,7 +467,13 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #endif
 
 #ifndef EGM_WALK_STACK
-#define EGM_WALK_STACK 320   // items (16 B) per wave
+#define EGM_WALK_STACK 320   // items (16 B) per wave: chunks of up to DEEP_MIN levels
+#endif
+#ifndef EGM_WALK_STACK_DEEP
+#define EGM_WALK_STACK_DEEP 640   // items per wave of the deep pass (deeper chunks: C3's wide frontiers)
+#endif
+#ifndef EGM_WALK_DEEP_MIN
+#define EGM_WALK_DEEP_MIN 12   // a chunk with a deeper topic is walked by the deep pass
 #endif
 #ifndef EGM_WALK_STAGE
 #define EGM_WALK_STAGE 320   // staged emits per flush (7 B each; >= 4 emits x 64 lanes)
@@ -475,37 +481,27 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #ifndef EGM_WALK_WORDS
 #define EGM_WALK_WORDS 448   // staged topic word ids per wave (a chunk's topics, [topic][level])
 #endif
-#ifndef EGM_WALK_TAILS
-#define EGM_WALK_TAILS 0     // 1: a topic's ids reach its fixed block in whole 16-id (64-B) units, the rest held in LDS
-#endif
-#ifndef EGM_WALK_ITEM12
-#define EGM_WALK_ITEM12 0    // 1: stack items of 12 B {node, meta, plus_child}; the word is read from the LDS stage at pop
-#endif
-#ifndef EGM_PROBE_SLOTS
-#define EGM_PROBE_SLOTS 2    // edge slots a literal probe reads up front (2 x 16-B loads each); the rest on a miss
-#endif
 constexpr uint32_t WALK_STACK = EGM_WALK_STACK;
+constexpr uint32_t WALK_STACK_DEEP = EGM_WALK_STACK_DEEP;
+constexpr uint32_t DEEP_MIN = EGM_WALK_DEEP_MIN;
 constexpr uint32_t WALK_STAGE = EGM_WALK_STAGE;
 constexpr uint32_t WALK_WORDS = EGM_WALK_WORDS;
-constexpr int PROBE_SLOTS = EGM_PROBE_SLOTS;
-static_assert(PROBE_SLOTS == 1 || PROBE_SLOTS == 2, "probe width");
 // The pop bound (below) keeps room >= dmax after every iteration and a refill
 // fills the stack to at most 64 items, so the stack cannot overflow while
-// 64 + dmax <= WALK_STACK; the words of one topic must fit the word stage.
+// 64 + dmax <= the stack; the words of one topic must fit the word stage.
 // A chunk with a deeper topic goes to k_heavy before any of it is walked.
-constexpr uint32_t LIGHT_DMAX = (WALK_STACK - 64) < WALK_WORDS ? (WALK_STACK - 64) : WALK_WORDS;
+__host__ __device__ constexpr uint32_t light_dmax(uint32_t stack) {
+  return (stack - 64) < WALK_WORDS ? (stack - 64) : WALK_WORDS;
+}
 static_assert(WALK_CHUNK == 64, "one topic per lane in the chunk prologue");
 static_assert(WALK_STAGE >= 256, "a step stages up to 4 emits x 64 lanes");
 static_assert(WALK_STAGE <= 0xFFFF, "flush slots and spill starts are packed as 16-bit halves");
-static_assert(LIGHT_DMAX >= 16, "stack too small");
+static_assert(light_dmax(WALK_STACK) >= DEEP_MIN, "the first pass must take the chunks it does not hand on");
+static_assert(light_dmax(WALK_STACK_DEEP) >= 16, "stack too small");
 
+template <uint32_t STK>
 struct alignas(16) WaveLds {
-#if EGM_WALK_ITEM12
-  uint2 stk_nm[WALK_STACK];          // items: {node, meta}
-  uint32_t stk_plus[WALK_STACK];     //        plus_child
-#else
-  uint4 stack[WALK_STACK];
-#endif
+  uint4 stack[STK];
   uint32_t stage_fid[WALK_STAGE];
   uint16_t stage_rank[WALK_STAGE];
   uint8_t stage_t[WALK_STAGE];       // topic in chunk of the emit
@@ -513,16 +509,6 @@ struct alignas(16) WaveLds {
   uint32_t tinfo[WALK_CHUNK];        // D | tflags << 24 | words at the fixed stride << 31
   uint32_t cnt[WALK_CHUNK];          // ids per topic, whole chunk
   uint32_t fcnt[WALK_CHUNK];         // ids per topic in the current stage / start inside the flush
-#if EGM_WALK_TAILS
-  uint32_t tail[WALK_CHUNK][16];     // per topic: its ids past the last whole 16-id unit written (fixed block)
-  uint32_t gsc[WALK_CHUNK];          // per topic in a flush: first unit-store slot | first position << 16
-#endif
-#ifdef EGM_AB_APPEND
-  uint32_t ab_app;
-#endif
-#ifdef EGM_AB_LDS_PAD   // measurement only: occupancy A/B (waves per CU) at the same code
-  uint32_t ab_pad[EGM_AB_LDS_PAD / 4];
-#endif
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
@@ -530,30 +516,6 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin
 // half would set the high word of a pointer whose bit 31 is set)
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | (uint64_t)uni((uint32_t)v);
-}
-
-// The LDS work stack.  With 12-B items the word of an item's level is not
-// stored: it is read back from the chunk's word stage at pop (one LDS read
-// beside the item's), which leaves room for more waves per CU.
-__device__ __forceinline__ void push_item(WaveLds& L, uint32_t i, uint4 it) {
-#if EGM_WALK_ITEM12
-  L.stk_nm[i] = make_uint2(it.x, it.y);
-  L.stk_plus[i] = it.z;
-#else
-  L.stack[i] = it;
-#endif
-}
-
-__device__ __forceinline__ uint4 pop_item(const WaveLds& L, uint32_t i, uint32_t S, uint32_t dmax) {
-#if EGM_WALK_ITEM12
-  const uint2 nm = L.stk_nm[i];
-  const uint32_t tt = (nm.y >> MT_SHIFT) & 0x7Fu, level = min(nm.y & LEVEL_MAX, dmax - 1);
-  return make_uint4(nm.x, nm.y, L.stk_plus[i], L.words[(tt & (S - 1)) * dmax + level]);
-#else
-  (void)S;
-  (void)dmax;
-  return L.stack[i];
-#endif
 }
 
 // An unused pieces-slab slot: count 0, skipped by k_compact.
@@ -585,7 +547,6 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
   return r;
 }
 
-#if !EGM_WALK_TAILS
 // Write the stage out.  Entries are ranked within their topic by a
 // conflict-free multi-split (lanes holding the same topic find each other
 // with 6 ballots; one LDS add per topic per 64 entries).  A topic's first
@@ -594,7 +555,8 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
 // the wave's ids slab grouped by topic, one piece
 // {topic, count, ids_tmp offset, offset inside the topic's CSR row} per topic
 // that spills, so neither compaction needs atomics.
-__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t my_t, uint32_t lane,
+template <class LDS>
+__device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t t0, uint32_t my_t, uint32_t lane,
                                             const MatchWork& w, Slab& sid, Slab& spc) {
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {
@@ -659,109 +621,7 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
 #ifdef EGM_AB_NO_ID_STORES   // measurement only (tools/build_variant.py): the walk without its id stores
     if (L.stage_fid[i] != 0x7FFFFFF1u) continue;
 #endif
-#ifdef EGM_AB_APPEND   // measurement only: the same stores as one contiguous run per flush (rows wrong)
-    if (k < cap) w.ids_fix[(uint64_t)t0 * cap + ((L.ab_app + q) % (WALK_CHUNK * cap))] = L.stage_fid[i];
-#else
     if (k < cap) w.ids_fix[(uint64_t)(t0 + tt) * cap + k] = L.stage_fid[i];
-#endif
-    else if (ok) w.ids_tmp[base + (f & 0xFFFFu) + (k - max(cb, cap))] = L.stage_fid[i];
-  }
-  wave_sync();
-#ifdef EGM_AB_APPEND
-  if (lane == 0) L.ab_app += nstage;
-#endif
-  L.cnt[lane] += fl;
-  L.fcnt[lane] = 0;
-  wave_sync();
-}
-#endif
-
-#if EGM_WALK_TAILS
-// flush_stage with whole-unit stores.  A topic's first fix_cap ids go to its
-// fixed block in 16-id units (64 B, the memory system's granule, tools/
-// granule.hip): a flush writes only the units it completes — with the ids an
-// earlier flush left in the topic's LDS tail — and keeps the rest in the
-// tail; the chunk's end writes the tails (flush_tails).  Positions [0, W)
-// of a topic with c ids are in HBM, W = min(c & ~15, fix_cap & ~15), and
-// [W, min(c, fix_cap)) in its tail.  Ids past fix_cap spill as pieces.
-__device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_t t0, uint32_t my_t, uint32_t lane,
-                                            const MatchWork& w, Slab& sid, Slab& spc) {
-#pragma unroll 1
-  for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {   // rank entries within their topic (as flush_stage)
-    const uint32_t i = i0 + lane;
-    const bool act = i < nstage;
-    const uint32_t tt = act ? L.stage_t[i] : 0u;
-    uint64_t m = __ballot(act);
-#pragma unroll
-    for (uint32_t b = 0; b < 6; ++b) {
-      const bool bit = (tt >> b) & 1u;
-      const uint64_t bb = __ballot(bit);
-      m &= bit ? bb : ~bb;
-    }
-    const uint32_t leader = act ? (uint32_t)__builtin_ctzll(m) : lane;
-    uint32_t old = 0;
-    if (act && lane == leader) old = atomicAdd(&L.fcnt[tt], popc(m));
-    old = __shfl(old, (int)leader, 64);
-    if (act) L.stage_rank[i] = (uint16_t)(old + mbcnt(m));
-  }
-  wave_sync();
-  const uint32_t cap = w.fix_cap, cap16 = cap & ~15u;
-  const uint32_t fl = L.fcnt[lane];   // the chunk's topic `lane`: ids in this flush
-  const uint32_t c0 = L.cnt[lane];    // ... and before it
-  const uint32_t nfix = c0 >= cap ? 0u : min(fl, cap - c0);
-  const uint32_t over = fl - nfix;    // ids past the fixed block: spilled
-  const uint32_t W0 = min(c0 & ~15u, cap16), W1 = min((c0 + fl) & ~15u, cap16);
-  uint32_t tot, ptot, gtot, utot;
-  const uint32_t ex = wave_excl_scan(over, lane, &tot);
-  const uint32_t pex = wave_excl_scan(over ? 1u : 0u, lane, &ptot);
-  const uint32_t gx = wave_excl_scan(fl, lane, &gtot);
-  const uint32_t gs = wave_excl_scan(W1 - W0, lane, &utot);   // unit-store slots of this topic
-  unsigned long long base = 0;
-  bool ok = true;
-  if (tot) {   // wave-uniform
-    base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
-    const unsigned long long pbase =
-        slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
-    ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
-    if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
-    if (over && ok) w.pieces[pbase + pex] = make_uint4(my_t, over, (uint32_t)(base + ex), c0 + nfix);
-  }
-  L.fcnt[lane] = ex | (gx << 16);   // spill start | first slot of its entries in topic order
-  L.gsc[lane] = gs | (W0 << 16);
-  wave_sync();
-  constexpr uint32_t NQ = (WALK_STAGE + 63) / 64;
-  uint32_t qv[NQ];
-#pragma unroll
-  for (uint32_t r = 0; r < NQ; ++r) {
-    const uint32_t i = lane + 64 * r;
-    qv[r] = i < nstage ? (L.fcnt[L.stage_t[i]] >> 16) + L.stage_rank[i] : 0u;
-  }
-  wave_sync();
-#pragma unroll
-  for (uint32_t r = 0; r < NQ; ++r)
-    if (lane + 64 * r < nstage) L.stage_rank[qv[r]] = (uint16_t)(lane + 64 * r);   // now: slot -> entry
-  wave_sync();
-  // the units this flush completes: consecutive lanes store consecutive ids of a unit
-#pragma unroll 1
-  for (uint32_t q = lane; q < utot; q += 64) {
-    uint32_t k = 0;
-#pragma unroll
-    for (uint32_t step = 32; step >= 1; step >>= 1)
-      if ((k + step) < WALK_CHUNK && (L.gsc[k + step] & 0xFFFFu) <= q) k += step;
-    const uint32_t g = L.gsc[k], pos = (g >> 16) + (q - (g & 0xFFFFu)), c = L.cnt[k];
-    const uint32_t v = pos < c ? L.tail[k][pos & 15u] : L.stage_fid[L.stage_rank[(L.fcnt[k] >> 16) + (pos - c)]];
-    w.ids_fix[(uint64_t)(t0 + k) * cap + pos] = v;
-  }
-  wave_sync();   // the old tail values are read before the new ones overwrite them
-#pragma unroll 1
-  for (uint32_t q = lane; q < nstage; q += 64) {
-    const uint32_t i = L.stage_rank[q], tt = L.stage_t[i], f = L.fcnt[tt], cb = L.cnt[tt];
-    const uint32_t k = cb + (q - (f >> 16));
-    const uint32_t g = L.gsc[tt];
-    const uint32_t nxt = tt + 1 < WALK_CHUNK ? (L.gsc[tt + 1] & 0xFFFFu) : utot;
-    const uint32_t wend = (g >> 16) + (nxt - (g & 0xFFFFu));   // W1 of the topic
-    if (k < wend) continue;                                     // stored in a unit above
-    if (k < cap) L.tail[tt][k & 15u] = L.stage_fid[i];
     else if (ok) w.ids_tmp[base + (f & 0xFFFFu) + (k - max(cb, cap))] = L.stage_fid[i];
   }
   wave_sync();
@@ -769,16 +629,6 @@ __device__ __forceinline__ void flush_stage(WaveLds& L, uint32_t nstage, uint32_
   L.fcnt[lane] = 0;
   wave_sync();
 }
-
-// The chunk's end: every topic's tail (< 16 ids) to its fixed block.
-__device__ __forceinline__ void flush_tails(WaveLds& L, uint32_t t0, uint32_t lane, const MatchWork& w) {
-  const uint32_t cap = w.fix_cap, c = L.cnt[lane];
-  const uint32_t cf = min(c, cap), W = min(c & ~15u, cap & ~15u);
-#pragma unroll
-  for (uint32_t k = 0; k < 16; ++k)
-    if (W + k < cf) w.ids_fix[(uint64_t)(t0 + lane) * cap + W + k] = L.tail[lane][k];
-}
-#endif
 
 // Slot search from slot k0 of bucket b on (rare: both first slots hold other keys).
 __device__ __forceinline__ bool edge_probe_from(const DevTable& tab, uint32_t b, int k0, uint32_t node, uint32_t w,
@@ -823,15 +673,10 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* words
   const uint32_t bkt = edge_bucket(p.it.x, p.it.w, tab.edge_mask);
   p.prec = ld16(tab.nodes + (p.plus ? p.it.z : 0u));
   const uint8_t* bp = (const uint8_t*)(tab.edges + (size_t)(p.lit ? bkt : 0u) * EDGE_BUCKET);
-  p.l0 = ld16(bp);
+  p.l0 = ld16(bp);   // the bucket's first two slots: one 64-B line
   p.h0 = ld16(bp + 16);
-  if (PROBE_SLOTS == 2) {
-    p.l1 = ld16(bp + 32);
-    p.h1 = ld16(bp + 48);
-  } else {   // slot 1 unread: a key that is not in slot 0 goes to the slot search from slot 1
-    p.l1 = make_uint4(TOMB, WID_NONE, 0, 0);
-    p.h1 = make_uint4(0, 0, 0, 0);
-  }
+  p.l1 = ld16(bp + 32);
+  p.h1 = ld16(bp + 48);
   // the next level's word (clamped; used only if level + 1 < D)
   const uint32_t nl = min((meta & LEVEL_MAX) + 1, p.D - 1);
   p.nw = words ? words[nl] : wid[p.act ? gbase + nl : 0u];
@@ -875,7 +720,7 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend
   bool found = p.lit && (m0 || m1);
   if (p.lit && !m0 && !z0 && !m1 && !z1) {   // the slots read hold other keys: keep probing
     uint4 lo, hi;
-    found = edge_probe_from(tab, edge_bucket(node, p.it.w, tab.edge_mask), PROBE_SLOTS, node, p.it.w, &lo, &hi);
+    found = edge_probe_from(tab, edge_bucket(node, p.it.w, tab.edge_mask), 2, node, p.it.w, &lo, &hi);
     cz = lo.z;
     cw = lo.w;
     hx = hi.x;
@@ -942,16 +787,34 @@ __device__ __forceinline__ const uint32_t* topic_words(const MatchWork& w, uint3
 // in sub-chunks of S topics with S * dmax <= WALK_WORDS), topics are admitted
 // 64 roots at a time while the stack is short, and the wave pops up to 64
 // items per iteration.
+//
+// Two passes: the first (DEEP = false, a 320-item stack, 16 waves per CU)
+// walks the chunks of up to DEEP_MIN levels and hands deeper ones to the
+// second (DEEP = true: a 640-item stack, 10 waves per CU), whose wider stack
+// keeps the wave's pops full on deep, wide frontiers (C3: lane occupancy 0.39
+// -> 0.84) where the first pass's room bound would narrow it; a chunk deeper
+// than the deep pass takes goes to k_heavy.
 #ifdef EGM_WALK_WPE   // A/B: ask the compiler for this many waves per SIMD (caps VGPRs)
 #define EGM_WALK_ATTR __attribute__((amdgpu_waves_per_eu(EGM_WALK_WPE)))
 #else
 #define EGM_WALK_ATTR
 #endif
-__global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const uint32_t* __restrict__ off, uint32_t n, int mode,
-                                             MatchWork w) {
-  __shared__ WaveLds L;
+// Hand the first n (wave-uniform) of lane-held chunk ids to the deep pass.
+__device__ __forceinline__ void deep_flush(const MatchWork& w, uint32_t c, uint32_t n, uint32_t lane) {
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(&w.stats->n_deep, n);
+  base = uni(__shfl(base, 0, 64));
+  if (lane < n) w.deep[base + lane] = c;
+}
+
+template <bool DEEP>
+__global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const uint32_t* __restrict__ off, uint32_t n,
+                                                           int mode, MatchWork w) {
+  constexpr uint32_t STK = DEEP ? WALK_STACK_DEEP : WALK_STACK;
+  __shared__ WaveLds<STK> L;
   const uint32_t lane = threadIdx.x;
-  const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  // the first pass walks every chunk, the deep pass the chunks the first handed on
+  const uint32_t nchunks = DEEP ? uni(*(volatile unsigned int*)&w.stats->n_deep) : (n + WALK_CHUNK - 1) / WALK_CHUNK;
   uint4 root = ld16(tab.nodes);   // wave-uniform: keep it in SGPRs
   root.x = uni(root.x);
   root.y = uni(root.y);
@@ -964,16 +827,18 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
   // sorted batch: the record of the chunk's j-th topic in walk order, loaded
   // one chunk ahead (a grid stride: the wave's next chunk is c + gridDim.x)
   const uint64_t* ord = w.order;
-  uint64_t rec = ord ? ord[min(blockIdx.x * WALK_CHUNK + lane, n - 1)] : 0ull;
-  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+  uint64_t rec = (ord && !DEEP) ? ord[min(blockIdx.x * WALK_CHUNK + lane, n - 1)] : 0ull;
+  uint32_t deep_c = 0, n_pend = 0;   // chunks for the deep pass not yet handed on
+  for (uint32_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+    const uint32_t c = DEEP ? uni(w.deep[ci]) : ci;
     const uint32_t t0 = c * WALK_CHUNK;
     const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
     // ---- topic info (lane j: the chunk's j-th topic in walk order) ----
     uint32_t D = 0, f = 0, my_t = 0;
     bool fixed = false;
     if (ord) {
-      const uint64_t r = rec;
-      rec = ord[min((uint64_t)(c + gridDim.x) * WALK_CHUNK + lane, (uint64_t)n - 1)];   // the next chunk's, in flight now
+      const uint64_t r = DEEP ? ord[min(t0 + lane, n - 1)] : rec;
+      if (!DEEP) rec = ord[min((uint64_t)(c + gridDim.x) * WALK_CHUNK + lane, (uint64_t)n - 1)];   // the next chunk's, in flight now
       if (lane < nt) {
         my_t = (uint32_t)r;
         D = (uint32_t)(r >> 32) & 0xFFFFFFu;
@@ -985,26 +850,31 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
       D = w.lv[my_t];
       f = w.tfl[my_t];
     }
-    // lane j's register: topic j's word 0, a wid[] index (off[t] + t) or its topic (fixed
-    // stride); only words at a variable offset need off[] (read by other lanes with a shuffle)
-    const uint32_t gb = lane < nt ? (fixed ? my_t : off[my_t] + my_t) : 0u;
     L.tinfo[lane] = D | (f << 24) | (fixed ? 0x80000000u : 0u);
     L.cnt[lane] = 0;
-#ifdef EGM_AB_APPEND
-    if (lane == 0) L.ab_app = 0;
-#endif
     L.fcnt[lane] = 0;
     uint32_t dmax = D;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, d, 64));
     dmax = uni(dmax);
-    if (dmax > LIGHT_DMAX || (w.debug & DEBUG_FORCE_HEAVY)) {   // the whole chunk goes to k_heavy
+    if (dmax > light_dmax(WALK_STACK_DEEP) || (w.debug & DEBUG_FORCE_HEAVY)) {   // the whole chunk goes to k_heavy
       if (lane == 0) {
         const uint32_t d = atomicAdd(&w.stats->n_deferred, 1u);
         w.deferred[d] = c;
       }
       continue;
     }
+    if (!DEEP && dmax > DEEP_MIN) {   // to the deep pass: lane k holds the wave's k-th such chunk,
+      deep_c = lane == n_pend ? c : deep_c;   // handed on 64 at a time (one atomic per 64: a
+      if (++n_pend == 64) {                   // per-chunk atomic on one counter serialised a C3 batch)
+        deep_flush(w, deep_c, n_pend, lane);
+        n_pend = 0;
+      }
+      continue;
+    }
+    // lane j's register: a wid[] index (off[t] + t) or its topic (fixed stride);
+    // only words at a variable offset need off[] (read by other lanes with a shuffle)
+    const uint32_t gb = lane < nt ? (fixed ? my_t : off[my_t] + my_t) : 0u;
     uint32_t S = WALK_CHUNK;
     while (S > 1 && S * dmax > WALK_WORDS) S >>= 1;
     uint32_t nstage = 0;
@@ -1064,7 +934,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
             }
           }
           const uint64_t b = __ballot(has);
-          if (has) push_item(L, sp + mbcnt(b), it);
+          if (has) L.stack[sp + mbcnt(b)] = it;
           sp += popc(b);
           const uint64_t be = __ballot(em);
           if (em) {
@@ -1087,7 +957,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
         // one pending sibling per level below the top item.  So the stack
         // never overflows: a deep, wide frontier (C3: depth 16, '+' p=.35)
         // narrows the wave instead.
-        const uint32_t room = WALK_STACK - sp;
+        const uint32_t room = STK - sp;
         const uint32_t lim = room > dmax ? room - dmax : 1u;
         const uint32_t want = min(64u, sp), take = min(want, lim), bi = sp - take;
         bounded += take < want ? 1u : 0u;
@@ -1095,7 +965,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
         popped += take;
         Pend p;
         p.act = lane < take;
-        p.it = pop_item(L, min(bi + lane, WALK_STACK - 1), S, dmax);   // unconditional: see issue()
+        p.it = L.stack[min(bi + lane, STK - 1)];   // unconditional: see issue()
         sp = bi;
         const uint32_t tt = (p.it.y >> MT_SHIFT) & 0x7Fu;
         const uint32_t ti = L.tinfo[tt];
@@ -1111,12 +981,12 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
         created += o.created;
         const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
         const uint32_t m0 = popc(c0b), nc = m0 + popc(c1b);
-        if (sp + nc > WALK_STACK) {   // guard only: the pop bound keeps sp + pushes <= WALK_STACK
+        if (sp + nc > STK) {   // guard only: the pop bound keeps sp + pushes <= STK
           if (lane == 0) atomicOr(&w.stats->guard, GUARD_STACK);
           break;
         }
-        if (o.p0) push_item(L, sp + mbcnt(c0b), o.c0);
-        if (o.p1) push_item(L, sp + m0 + mbcnt(c1b), o.c1);
+        if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
+        if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;
         sp += nc;
         const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
         const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
@@ -1151,21 +1021,19 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
       }
     }
     if (nstage) flush_stage(L, nstage, t0, my_t, lane, w, sid, spc);
-#if EGM_WALK_TAILS
-    flush_tails(L, t0, lane, w);
-#endif
     if (lane < nt) {
       w.cnt[my_t] = L.cnt[lane];
       w.inv[my_t] = t0 + lane;   // its fixed block (k_compact_fix)
     }
     wave_sync();
   }
+  if (!DEEP && n_pend) deep_flush(w, deep_c, n_pend, lane);
   for (unsigned long long i = spc.cur + lane; i < spc.end && i < w.pieces_cap; i += 64)
     w.pieces[i] = empty_piece();   // unused tail of the last pieces slab
   unsigned long long v = created;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  if (lane == 0) {
+  if (lane == 0 && (iters || v)) {   // a wave that walked nothing adds nothing (same-address atomics serialise)
     if (v) atomicAdd(&w.stats->visited, v);
     atomicAdd(&w.stats->iters, iters);
     atomicAdd(&w.stats->popped, popped);
@@ -1176,7 +1044,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
 }
 
 // ----------------------------------------------------------------- heavy ----
-// Topics of deferred chunks (a topic deeper than LIGHT_DMAX, or every chunk
+// Topics of deferred chunks (a topic deeper than the walk's deep pass takes, or every chunk
 // under DEBUG_FORCE_HEAVY): one wave per topic, the same states and pop bound
 // as k_walk, but the stack lives in HBM — heavy_cap items per wave, sized by
 // the host to at least the batch's deepest possible topic + 192, so by the
@@ -1539,6 +1407,14 @@ int walk_grid_blocks(uint32_t n) {
   return blocks ? (int)blocks : 1;
 }
 
+// The deep pass: 10 waves per CU fit its LDS; a grid stride over the chunks handed to it.
+static int deep_grid_blocks(uint32_t n) {
+  const uint32_t chunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  uint32_t blocks = chunks < 256u * 10u ? chunks : 256u * 10u;
+  blocks = (blocks + 7) & ~7u;
+  return blocks ? (int)blocks : 1;
+}
+
 uint32_t heavy_stack_items(uint64_t max_levels) { return (uint32_t)(max_levels + 256); }
 
 size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
@@ -1616,9 +1492,13 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
     w.order = nullptr;
   }
   if (ev_walk) hipEventRecord(ev_walk[0], s);
-  hipLaunchKernelGGL(k_walk, dim3(walk_grid_blocks(n)), dim3(64), 0, s, tab, off, n, mode, w);
-  if (ev_walk) hipEventRecord(ev_walk[1], s);
+  hipLaunchKernelGGL(k_walk<false>, dim3(walk_grid_blocks(n)), dim3(64), 0, s, tab, off, n, mode, w);
   trace(s, "k_walk");
+  // the chunks of more than DEEP_MIN levels (their count is on the device: a
+  // small grid that exits at once when there are none)
+  hipLaunchKernelGGL(k_walk<true>, dim3(deep_grid_blocks(n)), dim3(64), 0, s, tab, off, n, mode, w);
+  if (ev_walk) hipEventRecord(ev_walk[1], s);
+  trace(s, "k_walk<deep>");
   hipLaunchKernelGGL(k_heavy, dim3(w.heavy_waves), dim3(64), 0, s, tab, off, n, mode, w);
   trace(s, "k_heavy");
   scan_counts(w.cnt, n, w.tile_sums, out.row_ptr, s);

@@ -6,12 +6,12 @@ import csv
 import statistics
 import sys
 
-KEYS = ("k_walk", "k_tokenise", "k_compact_fix", "k_compact(", "k_scan", "onesweep", "k_heavy", "k_fan")
+KEYS = ("k_walk<true>", "k_walk", "k_tokenise", "k_compact_fix", "k_compact(", "k_scan", "onesweep", "k_heavy", "k_fan")
 
 for d in sys.argv[1:]:
     rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    walks = [i for i, r in enumerate(rows) if "k_walk" in r["Kernel_Name"]]
+    walks = [i for i, r in enumerate(rows) if "k_walk" in r["Kernel_Name"] and "k_walk<true>" not in r["Kernel_Name"]]
     # the first 2/3 of the walk launches: sizing, warm-up and the timed steps, before the pipelined leg
     cut = rows[walks[int(len(walks) * 2 / 3)]]["Start_Timestamp"] if len(walks) > 6 else None
     per = collections.defaultdict(list)

@@ -24,12 +24,23 @@ import os
 import statistics
 
 
-def per_dispatch(run_dir, counter, kernel="k_walk"):
-    vals = []
-    for r in csv.DictReader(open(os.path.join(run_dir, "run_counter_collection.csv"))):
-        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            vals.append(float(r["Counter_Value"]) * 1024.0)
-    return vals
+def per_dispatch(run_dir, counter):
+    """Per walk launch: the first pass (k_walk<false>) plus the deep pass that
+    follows it on the stream (k_walk<true>, the chunks of more than DEEP_MIN
+    levels; empty at C2), paired in dispatch order."""
+    first, deep = [], []
+    rows = list(csv.DictReader(open(os.path.join(run_dir, "run_counter_collection.csv"))))
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    acc = {}
+    for r in rows:
+        if "k_walk" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            k = (int(r["Dispatch_Id"]), "k_walk<true>" in r["Kernel_Name"])
+            acc[k] = acc.get(k, 0.0) + float(r["Counter_Value"]) * 1024.0
+    for (d, is_deep), v in sorted(acc.items()):
+        (deep if is_deep else first).append(v)
+    if deep and len(deep) == len(first):
+        return [a + b for a, b in zip(first, deep)]
+    return first
 
 
 def main():
