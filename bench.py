@@ -369,6 +369,8 @@ def main():
     ap.add_argument("--fanout-form", default="compact", choices=["compact", "pairs"],
                     help="delivery lists as subscriber ids + each match entry's first delivery "
                          "(egm_fanout_device_compact), or as (filter, subscriber) pairs (egm_fanout_device)")
+    ap.add_argument("--sharded-timeout", type=float, default=300.0,
+                    help="seconds the sharded leg may take before the line is printed without it")
     ap.add_argument("--sharded-leg", default="auto", choices=["auto", "on", "off"],
                     help="replicate mode at N>1 (auto) or any N (on): also time the filter-sharded layout "
                          "(BASELINE C2 as worded: broadcast + RCCL gather + GPU merge; with fan-out, fan-out on "
@@ -615,9 +617,7 @@ def main():
     merged_ids = leg.merged_ids() if leg is not None else None
     if args.x_orders and leg is None:
         order_experiment(args, gm, run_local, bufs, dev, n)
-    sharded = None
-    if leg is None and (args.sharded_leg == "on" or (args.sharded_leg == "auto" and world > 1)):
-        sharded = sharded_leg(args, f, t, rank, world, dev, mode, fanout, seed, have_pg)
+    run_sharded = leg is None and (args.sharded_leg == "on" or (args.sharded_leg == "auto" and world > 1))
 
     units_per_step = n if shard else n * world
     value = units_per_step * args.steps / elapsed
@@ -684,11 +684,37 @@ def main():
                        if fanout else None),
             "pipelined": pipelined,
             "serial": serial,
-            "sharded": sharded,
+            "sharded": None,
             "xgmi_model": (shard_cost_model(n, nbytes, world, merged_ids) if shard else None),
             "host_e2e": host,
             "cpu_baseline": cpu,
         }
+    if run_sharded:
+        # the filter-sharded layout beside the value, after it is measured: a
+        # leg that fails or hangs (a collective that never completes) must not
+        # cost the line, so each rank runs it under a watchdog that prints the
+        # line without it and ends the process
+        import threading
+
+        def give_up(why):
+            if rank == 0:
+                line["sharded"] = {"error": why}
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+
+        wd = threading.Timer(args.sharded_timeout, give_up,
+                             args=(f"sharded leg did not finish within {args.sharded_timeout:.0f} s",))
+        wd.daemon = True
+        wd.start()
+        try:
+            sharded = sharded_leg(args, f, t, rank, world, dev, mode, fanout, seed, have_pg)
+        except Exception as e:   # noqa: BLE001 - reported in the line, the value stands
+            wd.cancel()
+            give_up(f"sharded leg failed: {e!r}"[:300])
+        wd.cancel()
+        if rank == 0:
+            line["sharded"] = sharded
+    if rank == 0:
         print(json.dumps(line), flush=True)
     gm.close()
     if have_pg:
