@@ -65,6 +65,9 @@ for step in "$@"; do
     pmc)
       run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
       run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc_write" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
+    pmc_c4)   # FETCH_SIZE / WRITE_SIZE passes over the C4 bench (100M filters, match + fan-out)
+      run pmc_c4_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_c4_fetch" -o run --output-format csv -- $B --config c4 --steps 2 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
+      run pmc_c4_write 600 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc_c4_write" -o run --output-format csv -- $B --config c4 --steps 2 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
     sq)
       run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU -d "$R/gpurun_out/${TAG}_pmc_sq" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off
       run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off ;;
