@@ -160,6 +160,7 @@ def test_no_overflow_2_14_wide_frontier(gm):
         [b"k0/zz"] * 100
     res = gm.match_strings(topics, L.EGM_MODE_TRIE)
     assert res.n_error == 0
+    assert gm.walk_counters()["bounded"] > 0   # the frontier outgrew the LDS stack: depth-first pops
     got = sets(res)
     assert len(got[0]) == (1 << D) - 1 + 1   # all but the all-literal filter, + '#'
     assert len(got[1]) == (1 << (D - 1)) + 1  # last level must be '+', + '#'
