@@ -694,24 +694,14 @@ def main():
         # leg that fails or hangs (a collective that never completes) must not
         # cost the line, so each rank runs it under a watchdog that prints the
         # line without it and ends the process
-        import threading
-
         def give_up(why):
             if rank == 0:
                 line["sharded"] = {"error": why}
                 print(json.dumps(line), flush=True)
             os._exit(0)
 
-        wd = threading.Timer(args.sharded_timeout, give_up,
-                             args=(f"sharded leg did not finish within {args.sharded_timeout:.0f} s",))
-        wd.daemon = True
-        wd.start()
-        try:
-            sharded = sharded_leg(args, f, t, rank, world, dev, mode, fanout, seed, have_pg)
-        except Exception as e:   # noqa: BLE001 - reported in the line, the value stands
-            wd.cancel()
-            give_up(f"sharded leg failed: {e!r}"[:300])
-        wd.cancel()
+        sharded = guarded(lambda: sharded_leg(args, f, t, rank, world, dev, mode, fanout, seed, have_pg),
+                          args.sharded_timeout, give_up, "sharded leg")
         if rank == 0:
             line["sharded"] = sharded
     if rank == 0:
@@ -719,6 +709,23 @@ def main():
     gm.close()
     if have_pg:
         dist.destroy_process_group()
+
+
+def guarded(fn, seconds, give_up, what):
+    """fn() under a watchdog: if it raises, or has not returned after `seconds`
+    (a collective that never completes), give_up(reason) is called — from a
+    timer thread in the second case, so it must end the process itself."""
+    import threading
+    wd = threading.Timer(seconds, give_up, args=(f"{what} did not finish within {seconds:.0f} s",))
+    wd.daemon = True
+    wd.start()
+    try:
+        out = fn()
+    except Exception as e:   # noqa: BLE001 - reported, the caller's result stands
+        wd.cancel()
+        return give_up(f"{what} failed: {e!r}"[:300])
+    wd.cancel()
+    return out
 
 
 def sharded_leg(args, f, t, rank, world, dev, mode, fanout, seed, have_pg):
