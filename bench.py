@@ -693,12 +693,15 @@ def main():
         # the filter-sharded layout beside the value, after it is measured: a
         # leg that fails or hangs (a collective that never completes) must not
         # cost the line, so each rank runs it under a watchdog that prints the
-        # line without it and ends the process
+        # line without it and ends the process — with a non-zero status, so the
+        # failure still shows in the return code
         def give_up(why):
             if rank == 0:
                 line["sharded"] = {"error": why}
                 print(json.dumps(line), flush=True)
-            os._exit(0)
+            sys.stderr.write(f"[rank {rank}] {why}\n")
+            sys.stderr.flush()
+            os._exit(SHARDED_LEG_FAILED)
 
         sharded = guarded(lambda: sharded_leg(args, f, t, rank, world, dev, mode, fanout, seed, have_pg),
                           args.sharded_timeout, give_up, "sharded leg")
@@ -711,20 +714,39 @@ def main():
         dist.destroy_process_group()
 
 
+SHARDED_LEG_FAILED = 3   # exit status after a line printed without its failed sharded leg
+
+
 def guarded(fn, seconds, give_up, what):
     """fn() under a watchdog: if it raises, or has not returned after `seconds`
     (a collective that never completes), give_up(reason) is called — from a
-    timer thread in the second case, so it must end the process itself."""
+    timer thread in the second case, so it must end the process itself.
+    Exactly one of {fn's result, the timer's give_up, the error's give_up}
+    wins (a timer firing as fn returns must not print a second
+    line): the first to take `decided` does; a loser that is the main thread
+    waits for the timer thread to end the process."""
     import threading
-    wd = threading.Timer(seconds, give_up, args=(f"{what} did not finish within {seconds:.0f} s",))
+    decided = threading.Lock()
+
+    def fire():
+        if decided.acquire(blocking=False):
+            give_up(f"{what} did not finish within {seconds:.0f} s")
+
+    wd = threading.Timer(seconds, fire)
     wd.daemon = True
     wd.start()
     try:
         out = fn()
     except Exception as e:   # noqa: BLE001 - reported, the caller's result stands
-        wd.cancel()
-        return give_up(f"{what} failed: {e!r}"[:300])
+        out, err = None, e
+    else:
+        err = None
+    if not decided.acquire(blocking=False):
+        while True:          # the timer fired first: it prints the line and exits
+            time.sleep(3600)
     wd.cancel()
+    if err is not None:
+        return give_up(f"{what} failed: {err!r}"[:300])
     return out
 
 

@@ -283,7 +283,10 @@ static ERL_NIF_TERM nif_wait(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   return enif_make_tuple2(env, ATOM_OK, rows);
 }
 
-/* cancel(Ctx, Ticket) -> ok | {error, _}: give the batch up without its rows */
+/* cancel(Ctx, Ticket) -> ok | {error, _}: give the batch up without its rows.
+   A normal (not dirty) NIF: egm_match_cancel never blocks — while a build or
+   commit holds the context it queues the cancel — so this call and the ticket
+   destructor (run on whatever scheduler collects the ticket) return at once. */
 static ERL_NIF_TERM nif_cancel(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   egm_res_t* r;
   egm_ticket_t* t;

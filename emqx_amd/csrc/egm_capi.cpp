@@ -107,7 +107,8 @@ struct PipeSlot {
   }
 };
 constexpr size_t PIPE_MAX_SLOTS = 8;     // tickets of egm_match_submit busy or held at once
-constexpr size_t PIPE_HARD_SLOTS = 64;   // all slots, egm_match_batch's included (then it waits)
+constexpr size_t PIPE_HARD_SLOTS = 16;   // all slots, egm_match_batch's included (then it waits); each
+                                         // keeps buffers for the largest batch it saw (~ dirty schedulers)
 constexpr int PIPE_BATCH_WAIT_MS = 30000;   // egm_match_batch's longest wait for a slot
 
 // ticket = generation << 16 | (slot index + 1)
@@ -221,6 +222,8 @@ struct egm_ctx {
   // host pipeline (egm_match_submit / egm_match_wait)
   std::vector<std::unique_ptr<PipeSlot>> pipe;
   std::condition_variable_any pipe_cv;   // a slot was freed (wait done, result freed, ticket cancelled)
+  std::mutex cancel_mu;                  // guards cancel_q only (never held across another lock)
+  std::vector<uint64_t> cancel_q;        // cancels that found the context busy (egm_match_cancel)
   hipStream_t copy_stream = nullptr;   // pipeline host->device copies
   hipStream_t d2h_stream = nullptr;    // pipeline device->host copies (PCIe is full duplex)
   // last fan-out (egm_last_fanout)
@@ -841,6 +844,13 @@ int egm_table_commit(egm_ctx* c, uint64_t* epoch) {
   return commit_locked(c, epoch);
 }
 
+int egm_table_epoch(egm_ctx* c, uint64_t* epoch) {
+  if (!c || !epoch) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  *epoch = c->cur ? c->cur->id : 0;
+  return EGM_OK;
+}
+
 int egm_table_empty(egm_ctx* c) {
   if (!c) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
@@ -1034,7 +1044,22 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
 
 // A free pipeline slot for a batch (index into c->pipe), or -1.  Slots whose
 // ticket was cancelled are reclaimed here once their batch has finished.
+static PipeSlot* ticket_slot_of(egm_ctx* c, uint64_t ticket);
+
+// Apply the cancels queued while the context was busy (context lock held).
+static void drain_cancels(egm_ctx* c) {
+  std::vector<uint64_t> q;
+  {
+    std::lock_guard<std::mutex> g(c->cancel_mu);
+    q.swap(c->cancel_q);
+  }
+  for (uint64_t t : q)
+    if (PipeSlot* sp = ticket_slot_of(c, t)) sp->abandoned = true;   // a stale ticket: dropped
+  if (!q.empty()) c->pipe_cv.notify_all();
+}
+
 static long pipe_free_slot(egm_ctx* c) {
+  drain_cancels(c);
   for (size_t k = 0; k < c->pipe.size(); ++k) {
     PipeSlot& S = *c->pipe[k];
     if (S.busy && S.abandoned && !S.waiting && hipEventQuery(S.ev_done) == hipSuccess) {
@@ -1151,6 +1176,7 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   if (!c || !out || ticket == 0) return EGM_E_INVAL;
   *out = nullptr;
   std::unique_lock<std::recursive_mutex> g(c->mu);
+  drain_cancels(c);
   PipeSlot* sp = ticket_slot_of(c, ticket);
   if (!sp) return c->fail(EGM_E_STATE, "unknown, stale or already waited ticket");
   if (set_device(c)) return EGM_E_DEVICE;
@@ -1238,7 +1264,13 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
 // egm_match_wait (e.g. the NIF ticket resource collected unwaited).
 int egm_match_cancel(egm_ctx* c, uint64_t ticket) {
   if (!c || ticket == 0) return EGM_E_INVAL;
-  std::lock_guard<std::recursive_mutex> g(c->mu);
+  std::unique_lock<std::recursive_mutex> g(c->mu, std::try_to_lock);
+  if (!g.owns_lock()) {   // busy (a build or commit can hold the context for seconds): queue it
+    std::lock_guard<std::mutex> q(c->cancel_mu);
+    c->cancel_q.push_back(ticket);
+    return EGM_OK;
+  }
+  drain_cancels(c);
   PipeSlot* sp = ticket_slot_of(c, ticket);
   if (!sp) return c->fail(EGM_E_STATE, "unknown, stale or already waited ticket");
   sp->abandoned = true;

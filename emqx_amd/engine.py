@@ -130,6 +130,12 @@ class GpuMatcher:
     def empty(self) -> bool:
         return self.lib.egm_table_empty(self.ctx) == 1
 
+    def epoch(self) -> int:
+        """The current (last published) table epoch (egm_table_epoch)."""
+        ep = C.c_uint64()
+        self._check(self.lib.egm_table_epoch(self.ctx, C.byref(ep)), "egm_table_epoch")
+        return ep.value
+
     def stats(self) -> dict:
         v = [C.c_uint64() for _ in range(5)]
         self._check(self.lib.egm_table_stats(self.ctx, *[C.byref(x) for x in v]), "egm_table_stats")

@@ -6,7 +6,15 @@ call for call on the Python host and tested (tests/test_gpu_batch_mirror.py):
 * ``RouteTable``  — ``emqx_route``: a bag of (topic, dest) with the add/delete
   rules of ``emqx_router:do_add_route/2`` / ``do_delete_route/2``
   (apps/emqx/src/emqx_router.erl:114-125,164-170) and the post-commit table
-  events mnesia delivers to subscribers.
+  events mnesia delivers to a ``{table, emqx_route, simple}`` subscriber:
+  ``{write, {emqx_route, Topic, Dest}, _}`` / ``{delete_object, ...}`` — the
+  record tagged with the TABLE name, not ``route``.  Its wildcard
+  add runs inside ``emqx_gpu_routes:with_pending/2``, the one-line hook the
+  integration adds to ``do_add_route/2``.
+* ``Overlay``     — ``emqx_gpu_pending``, the ETS set of ``emqx_gpu_routes``
+  that gives the GPU path the reference's subscribe -> publish ordering
+  (VERDICT r3 item 1): {Topic, Ref, pending | done} for the wildcard filters
+  whose route add started but that no published epoch holds yet.
 * ``GpuFilters``  — ``emqx_gpu_match``'s id map + ``build/1`` / ``sync/2`` /
   ``filters_of/1`` over a NIF-shaped matcher (``GpuMatcher``: apply / commit /
   submit / wait / cancel).
@@ -16,49 +24,135 @@ call for call on the Python host and tested (tests/test_gpu_batch_mirror.py):
   route transaction.
 * ``BatchServer`` — ``emqx_gpu_batch``: per-message ``match_routes/1`` calls
   batched (size + linger), matched in TRIE mode (``emqx_trie:match/1``) and
-  expanded as ``lookup_routes/1`` of ``[Topic | Matched]``, which is
-  ``emqx_router:match_routes/1`` exactly (emqx_router.erl:129-134); every
-  failure falls back to the reference ``match_routes``.
+  expanded as ``lookup_routes/1`` of ``[Topic | Matched ++ Overlay hits]``,
+  which is ``emqx_router:match_routes/1`` exactly (emqx_router.erl:129-134);
+  every failure falls back to the reference ``match_routes``.
+
+The ordering guarantee.  In the reference a PUBLISH issued after
+``emqx_broker:subscribe/3`` returns sees the new route: ``do_subscribe`` calls
+the broker pool synchronously (emqx_broker.erl:153) and that call runs
+``emqx_router:do_add_route/1`` (:438-440), whose transaction puts the filter in
+``emqx_trie`` (emqx_router.erl:114-125,230-235).  The GPU table learns of the
+route only at the next linger + commit, so (erl/emqx_gpu_routes.erl):
+
+1. ``with_pending/2`` inserts {F, Ref, pending} BEFORE the route transaction
+   (so before ``subscribe`` returns), marks it ``done`` after a commit and
+   deletes it after an abort;
+2. the batcher reads every pending filter BEFORE it submits a batch, and the
+   waiter adds to each topic's matches those F with
+   ``emqx_topic:match(Topic, F)`` (deduplicated); ``lookup_routes/1`` drops a
+   filter whose route is not (or no longer) there;
+3. a flush deletes a pending object (compare-and-delete of the object it read
+   before ``has_routes/1``) only AFTER the epoch holding the filter is
+   published; a ``pending`` entry whose route is not committed yet is kept, a
+   ``done`` entry without routes (deleted since) is dropped.
+
+So a filter whose add started before a publish call is, at that batch's
+submit, either still pending (step 2 adds it) or in an epoch published before
+the submit, which the batch is matched against or a newer one.
 """
 from __future__ import annotations
 
+import itertools
 import threading
 import time
 from collections import namedtuple
-from typing import Callable, Dict, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from . import _lib as L
 from .batcher import Batcher
 from .engine import pack_strings
+from .topic import match as topic_match
 from .topic import wildcard
 
 Route = namedtuple("Route", "topic dest")
+ROUTE_TAB = "emqx_route"
+
+
+class Overlay:
+    """``emqx_gpu_pending``.  Every method is one ETS operation (atomic on its
+    own), as in erl/emqx_gpu_routes.erl; nothing holds a lock across two."""
+
+    def __init__(self):
+        self._mu = threading.Lock()
+        self._pending: Dict[bytes, Tuple[int, str]] = {}
+        self._refs = itertools.count(1)
+
+    def insert_pending(self, topic: bytes) -> int:          # ets:insert/2
+        with self._mu:
+            ref = next(self._refs)
+            self._pending[topic] = (ref, "pending")
+            return ref
+
+    def mark_done(self, topic: bytes, ref: int):             # ets:select_replace/2 (compare-and-set)
+        with self._mu:
+            if self._pending.get(topic) == (ref, "pending"):
+                self._pending[topic] = (ref, "done")
+
+    def delete_pending(self, topic: bytes, obj) -> None:    # ets:delete_object/2 (compare-and-delete)
+        with self._mu:
+            if obj is not None and self._pending.get(topic) == obj:
+                del self._pending[topic]
+
+    def lookup_pending(self, topic: bytes):                 # ets:lookup/2
+        with self._mu:
+            return self._pending.get(topic)
+
+    def filters(self) -> List[bytes]:                       # overlay/0: ets:select/2
+        with self._mu:
+            return list(self._pending)
+
+    def size(self) -> int:
+        with self._mu:
+            return len(self._pending)
 
 
 class RouteTable:
-    """emqx_route (a bag) with post-commit events: ('write', topic) and
-    ('delete_object', topic), as mnesia:subscribe({table, emqx_route, simple})
-    delivers them."""
+    """emqx_route (a bag) with post-commit events as mnesia:subscribe({table,
+    emqx_route, simple}) delivers them: ('write', ('emqx_route', Topic, Dest))
+    and ('delete_object', ('emqx_route', Topic, Dest)).  ``pending_hook`` is
+    emqx_gpu_routes:with_pending/2 around the wildcard branch of
+    do_add_route/2 (None: the hook's module is not running)."""
 
     def __init__(self):
         self._routes: Dict[bytes, List[object]] = {}
-        self._subs: List[Callable[[str, bytes], None]] = []
+        self._subs: List[Callable[[str, tuple], None]] = []
         self._mu = threading.Lock()
+        self.pending_hook: Optional[Callable[[bytes, Callable[[], str]], str]] = None
+        self.fail_next_trans = False   # test hook: the next wildcard transaction aborts
 
-    def subscribe(self, fn: Callable[[str, bytes], None]):
+    def subscribe(self, fn: Callable[[str, tuple], None]):
         self._subs.append(fn)
 
-    def _event(self, kind: str, topic: bytes):
+    def _event(self, kind: str, topic: bytes, dest):
         for fn in self._subs:
-            fn(kind, topic)
+            fn(kind, (ROUTE_TAB, topic, dest))
+
+    def _trans_add(self, topic: bytes, dest) -> str:     # maybe_trans(insert_trie_route/1) :230-235
+        with self._mu:
+            if self.fail_next_trans:
+                self.fail_next_trans = False
+                return "aborted"                          # {error, _}: no write, no event
+            cur = self._routes.setdefault(topic, [])
+            if dest not in cur:
+                cur.append(dest)
+        self._event("write", topic, dest)                 # after the commit
+        return "ok"
 
     def add_route(self, topic: bytes, dest="local"):     # do_add_route/2 :114-125
         with self._mu:
-            cur = self._routes.setdefault(topic, [])
-            if dest in cur:
+            if dest in self._routes.get(topic, []):
                 return "ok"
-            cur.append(dest)
-        self._event("write", topic)                      # after the commit
+        if wildcard(topic):
+            hook = self.pending_hook
+            if hook is not None:
+                return hook(topic, lambda: self._trans_add(topic, dest))
+            return self._trans_add(topic, dest)
+        with self._mu:                                    # insert_direct_route/1 (dirty write)
+            cur = self._routes.setdefault(topic, [])
+            if dest not in cur:
+                cur.append(dest)
+        self._event("write", topic, dest)
         return "ok"
 
     def delete_route(self, topic: bytes, dest="local"):  # do_delete_route/2 :164-170
@@ -69,7 +163,7 @@ class RouteTable:
             cur.remove(dest)
             if not cur:
                 del self._routes[topic]
-        self._event("delete_object", topic)
+        self._event("delete_object", topic, dest)
         return "ok"
 
     def lookup_routes(self, topic: bytes) -> List[Route]:   # :144-145
@@ -128,19 +222,43 @@ class GpuFilters:
 
 
 class RouteSync:
-    """emqx_gpu_routes: post-commit route events -> one GPU epoch per linger."""
+    """emqx_gpu_routes: post-commit route events -> one GPU epoch per linger,
+    plus the read-your-writes overlay (module docstring, steps 1 and 3)."""
 
-    def __init__(self, routes: RouteTable, filters: GpuFilters, batch_size: int = 65536, linger_ms: float = 5.0):
+    def __init__(self, routes: RouteTable, filters: GpuFilters, batch_size: int = 65536, linger_ms: float = 5.0,
+                 overlay: Optional[Overlay] = None):
         self.routes, self.filters = routes, filters
+        self.overlay = overlay if overlay is not None else Overlay()
         self.size, self.linger = batch_size, linger_ms / 1000.0
         self._touched: Dict[bytes, bool] = {}
         self._first = 0.0
         self._mu = threading.Lock()
+        self._flush = threading.Lock()   # the gen_server runs one flush at a time
         self.epochs = 0
         filters.build([t for t in routes.topics() if wildcard(t)])
         routes.subscribe(self.on_event)
+        routes.pending_hook = self.with_pending
 
-    def on_event(self, kind: str, topic: bytes):
+    def with_pending(self, topic: bytes, trans: Callable[[], str]) -> str:
+        """emqx_gpu_routes:with_pending/2 — runs in the caller of
+        do_add_route/2, before its route transaction (step 1)."""
+        ref = self.overlay.insert_pending(topic)
+        try:
+            r = trans()
+        except BaseException:
+            self.overlay.delete_pending(topic, (ref, "pending"))
+            raise
+        if r == "ok":
+            self.overlay.mark_done(topic, ref)
+        else:
+            self.overlay.delete_pending(topic, (ref, "pending"))
+        return r
+
+    def on_event(self, kind: str, rec: tuple):
+        # {write | delete_object, {emqx_route, Topic, Dest}, _}: the table name tags the record
+        if kind not in ("write", "delete_object") or len(rec) != 3 or rec[0] != ROUTE_TAB:
+            return
+        topic = rec[1]
         if not wildcard(topic):     # exact filters never enter the trie (emqx_router.erl:120-124)
             return
         with self._mu:
@@ -158,34 +276,51 @@ class RouteSync:
             return bool(self._touched) and time.monotonic() - self._first >= self.linger
 
     def publish(self):
-        with self._mu:
-            touched, self._touched = list(self._touched), {}
-        if not touched:
-            return
-        ins = [t for t in touched if self.routes.has_routes(t)]
-        dels = [t for t in touched if t not in set(ins)]
-        self.filters.sync(ins, dels)
-        self.epochs += 1
+        with self._flush:
+            with self._mu:
+                touched, self._touched = list(self._touched), {}
+            if not touched:
+                return
+            ov = self.overlay
+            snap = {t: ov.lookup_pending(t) for t in touched}   # before has_routes/1
+            ins = [t for t in touched if self.routes.has_routes(t)]
+            sins = set(ins)
+            dels = [t for t in touched if t not in sins]
+            self.filters.sync(ins, dels)    # returns after the epoch holding `ins` is published
+            for t in ins:                   # step 3
+                ov.delete_pending(t, snap[t])
+            for t in dels:                  # deleted since its add committed; a pending add is kept
+                if snap[t] is not None and snap[t][1] == "done":
+                    ov.delete_pending(t, snap[t])
+            self.epochs += 1
 
 
 class BatchServer:
     """emqx_gpu_batch: batched match_routes/1 with the reference as fallback."""
 
     def __init__(self, routes: RouteTable, filters: GpuFilters, fallback: Callable[[bytes], List[Route]],
-                 batch_size: int = 4096, linger_ms: float = 1.0):
+                 batch_size: int = 4096, linger_ms: float = 1.0, overlay: Optional[Overlay] = None):
         self.routes, self.filters, self.fallback = routes, filters, fallback
+        self.overlay = overlay
         self._b: Optional[Batcher] = Batcher(self._commit, batch_size=batch_size, linger_ms=linger_ms)
         self.fallbacks = 0
+        self.overlay_hits = 0
 
     def _commit(self, topics: Sequence[bytes]):
-        """One committed batch: submit (TRIE mode) + wait -> id rows, or the
-        error for every caller (handle_info/submit/answer of the Erlang side)."""
+        """One committed batch: overlay read, submit (TRIE mode), wait -> id
+        rows and each topic's overlay hits, or the error for every caller
+        (handle_info/submit/answer of the Erlang side)."""
         nif = self.filters.nif
         try:
+            extra = self.overlay.filters() if self.overlay is not None else []   # before the submit (step 2)
             blob, off = pack_strings(list(topics))
             t = nif.submit(blob, off, L.EGM_MODE_TRIE)
             res = nif.wait(t)
-            return [("ok", res.row(k).tolist()) for k in range(len(topics))]
+            out = []
+            for k, tp in enumerate(topics):
+                ex = [f for f in extra if topic_match(tp, f)] if (extra and not wildcard(tp)) else []
+                out.append(("ok", (res.row(k).tolist(), ex)))
+            return out
         except Exception as e:  # noqa: BLE001 - an error is an answer: the caller falls back
             return [("error", repr(e))] * len(topics)
 
@@ -202,7 +337,13 @@ class BatchServer:
         if tag != "ok":
             self.fallbacks += 1
             return self.fallback(topic)
-        matched = self.filters.filters_of(val)
+        ids, extra = val
+        matched = self.filters.filters_of(ids)
+        if extra:
+            seen = set(matched)
+            add = [f for f in extra if f not in seen]
+            self.overlay_hits += len(add)
+            matched = matched + add
         out: List[Route] = []
         for to in [topic] + matched:
             out.extend(self.routes.lookup_routes(to))

@@ -22,6 +22,14 @@
 %% [Topic | Matched] with lookup_routes/1, so the topic's own exact routes are
 %% included just as the reference includes them.
 %%
+%% Subscribe -> publish ordering: a wildcard route whose add started before
+%% a caller's match_routes/1 call may not be in the table epoch yet.  Before
+%% each submit the batch takes emqx_gpu_routes:overlay/0 (the filters whose
+%% add started — emqx_gpu_routes:with_pending/2, run before the route
+%% transaction — and that no published epoch holds yet); the waiter gives each
+%% caller those F with emqx_topic:match(Topic, F), merged into Matched without
+%% duplicates (the protocol: erl/emqx_gpu_routes.erl, steps 1-3).
+%%
 %% Semantics never change on failure: a NIF error, a dead or absent server, a
 %% killed waiter or a timeout all end in emqx_router:match_routes/1.  Late
 %% replies are dropped (gen_server:call uses a process alias, OTP >= 24).
@@ -60,8 +68,9 @@ match_routes(Topic, Timeout) when is_binary(Topic) ->
           catch exit:_ -> {error, unavailable}   %% noproc, timeout, server down
           end,
     case Res of
-        {ok, Ids} ->
-            Matched = emqx_gpu_match:filters_of(Ids),
+        {ok, Ids, Extra} ->
+            Matched0 = emqx_gpu_match:filters_of(Ids),
+            Matched = Matched0 ++ [F || F <- Extra, not lists:member(F, Matched0)],
             lists:append([emqx_router:lookup_routes(To) || To <- [Topic | Matched]]);
         {error, _} ->
             emqx_router:match_routes(Topic)
@@ -98,7 +107,7 @@ handle_info({'DOWN', Ref, process, _Pid, Reason}, St = #st{waiters = W}) ->
         {Items, W1} ->
             %% a waiter answers before it exits normally; any other exit leaves
             %% its callers unanswered: they fall back to the reference
-            Reason =:= normal orelse answer(Items, {error, {waiter_down, Reason}}),
+            Reason =:= normal orelse answer(Items, [], {error, {waiter_down, Reason}}),
             {noreply, next(St#st{waiters = W1})};
         error ->
             {noreply, St}
@@ -121,19 +130,34 @@ next(St = #st{waiters = W, depth = D, queue = Q}) ->
         _ -> St
     end.
 
-%% Submit one committed batch and start its (monitored) waiter.
+%% Submit one committed batch and start its (monitored) waiter.  The overlay
+%% is read before the submit (emqx_gpu_routes, step 2).
 submit(Items, St = #st{ctx = Ctx, waiters = W}) ->
     Topics = [T || {_From, T} <- Items],
-    case emqx_gpu_match:submit(Ctx, Topics, ?MODE_TRIE) of
-        {ok, Ticket} ->
-            {_Pid, Ref} = spawn_monitor(fun() -> answer(Items, emqx_gpu_match:wait(Ctx, Ticket)) end),
-            St#st{waiters = W#{Ref => Items}};
-        {error, _} = Err ->
-            answer(Items, Err),
+    case emqx_gpu_routes:overlay() of
+        {ok, Ov} -> submit(Items, Topics, Ov, St);
+        unavailable ->   %% no route sync: the GPU table is not kept in step
+            answer(Items, [], {error, no_route_sync}),
             St
     end.
 
-answer(Items, {ok, Rows}) ->
-    lists:foreach(fun({{From, _}, Ids}) -> gen_server:reply(From, {ok, Ids}) end, lists:zip(Items, Rows));
-answer(Items, Err) ->
+submit(Items, Topics, Ov, St = #st{ctx = Ctx, waiters = W}) ->
+    case emqx_gpu_match:submit(Ctx, Topics, ?MODE_TRIE) of
+        {ok, Ticket} ->
+            {_Pid, Ref} = spawn_monitor(fun() -> answer(Items, Ov, emqx_gpu_match:wait(Ctx, Ticket)) end),
+            St#st{waiters = W#{Ref => Items}};
+        {error, _} = Err ->
+            answer(Items, [], Err),
+            St
+    end.
+
+answer(Items, Ov, {ok, Rows}) ->
+    lists:foreach(fun({{From, Topic}, Ids}) ->
+                          Extra = case Ov =/= [] andalso not emqx_topic:wildcard(Topic) of
+                                      true -> [F || F <- Ov, emqx_topic:match(Topic, F)];
+                                      false -> []
+                                  end,
+                          gen_server:reply(From, {ok, Ids, Extra})
+                  end, lists:zip(Items, Rows));
+answer(Items, _Ov, Err) ->
     lists:foreach(fun({From, _}) -> gen_server:reply(From, Err) end, Items).

@@ -92,18 +92,39 @@ sync(Inserts, Deletes) ->
             ok
     end.
 
-%% emqx_trie:match/1 — one topic; production callers go through the batcher
+%% emqx_trie:match/1 — one topic; production callers go through the batcher.
+%% The overlay of filters not yet in a published epoch is read before the
+%% match (erl/emqx_gpu_routes.erl, steps 1-3).
 match(Topic) when is_binary(Topic) ->
-    case match_batch(ctx(), [Topic], ?MODE_TRIE) of
-        {ok, [Ids]} -> filters_of(Ids);
+    case with_overlay(fun() -> match_batch(ctx(), [Topic], ?MODE_TRIE) end) of
+        {ok, [Ids], Ov} ->   %% a pending filter is in emqx_trie once its route committed
+            merge_overlay(Topic, filters_of(Ids), [F || F <- Ov, emqx_router:has_routes(F)]);
         {error, _} -> emqx_trie:match(Topic)
     end.
 
 %% emqx_router:match_routes/1 (emqx_router.erl:129-134) for one topic: the
 %% topic's own routes, then the routes of every trie match.
 match_routes(Topic) when is_binary(Topic) ->
-    case match_batch(ctx(), [Topic], ?MODE_TRIE) of
-        {ok, [Ids]} ->
-            lists:append([emqx_router:lookup_routes(To) || To <- [Topic | filters_of(Ids)]]);
+    case with_overlay(fun() -> match_batch(ctx(), [Topic], ?MODE_TRIE) end) of
+        {ok, [Ids], Ov} ->
+            Matched = merge_overlay(Topic, filters_of(Ids), Ov),
+            lists:append([emqx_router:lookup_routes(To) || To <- [Topic | Matched]]);
         {error, _} -> emqx_router:match_routes(Topic)
+    end.
+
+%% The overlay is read before the match (emqx_gpu_routes, step 2).
+with_overlay(Match) ->
+    case emqx_gpu_routes:overlay() of
+        {ok, Ov} ->
+            case Match() of
+                {ok, Rows} -> {ok, Rows, Ov};
+                {error, _} = E -> E
+            end;
+        unavailable -> {error, no_route_sync}
+    end.
+
+merge_overlay(Topic, Matched, Ov) ->
+    case emqx_topic:wildcard(Topic) of
+        true -> Matched;   %% match_trie/1 of a wildcard topic is [] (emqx_trie.erl:102-111)
+        false -> Matched ++ [F || F <- Ov, emqx_topic:match(Topic, F), not lists:member(F, Matched)]
     end.

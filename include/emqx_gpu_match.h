@@ -122,6 +122,11 @@ int egm_table_commit(egm_ctx* ctx, uint64_t* epoch);
    records patched, host wall time (ms). */
 int egm_last_commit_stats(egm_ctx* ctx, uint64_t* h2d_bytes, uint64_t* d2d_bytes, uint64_t* patched,
                           double* ms);
+/* The current (last published) epoch.  A batch submitted after this call is
+   matched against this epoch or a later one, so a caller that keeps filters
+   published after it in an overlay (erl/emqx_gpu_routes.erl) never misses one.
+   No reference counterpart: emqx_trie reads the committed mnesia table. */
+int egm_table_epoch(egm_ctx* ctx, uint64_t* epoch);
 /* 1 if the committed table holds no filter, 0 otherwise. */
 int egm_table_empty(egm_ctx* ctx);
 /* Counts of the committed table: filters, trie nodes, literal edges, words. */
@@ -149,9 +154,13 @@ int egm_match_batch(egm_ctx* ctx, const uint8_t* topics_blob, const uint32_t* to
    A ticket carries a generation: a stale, repeated or cancelled ticket is
    refused with EGM_E_STATE (never answered with another batch's result).
    egm_match_cancel gives a ticket up without waiting: its slot is reclaimed
-   once its batch has finished (for a waiter that will never call wait).
+   once its batch has finished (for a waiter that will never call wait).  It
+   never blocks: while another call holds the context (a bulk build or a
+   commit can for seconds) the cancel is queued and applied by the next
+   pipeline call, so it may run on a normal Erlang scheduler or in a resource
+   destructor; a queued cancel of a stale ticket is dropped.
    egm_match_batch is submit + wait on a slot of its own: concurrent callers
-   never see "pipeline full" (extra slots up to 64, then they queue for one).
+   never see "pipeline full" (extra slots up to 16, then they queue for one).
    A walk guard trip (a kernel invariant failed, egm_last_guard) makes wait
    return EGM_E_DEVICE; only a capacity overflow is retried. */
 int egm_match_submit(egm_ctx* ctx, const uint8_t* topics_blob, const uint32_t* topic_offsets, uint32_t n_topics,

@@ -27,8 +27,9 @@ class OracleNif:
     TRIE-mode match is the oracle's emqx_trie:match/1 — CPU tests only."""
 
     class _Res:
-        def __init__(self, rows):
+        def __init__(self, rows, epoch):
             self.rows = rows
+            self.epoch = epoch
 
         def row(self, k):
             return np.asarray(self.rows[k], dtype=np.uint32)
@@ -38,11 +39,18 @@ class OracleNif:
         self.committed = {}
         self.tickets = {}
         self.fail = False
+        self.ep = 0
+        self.before_wait = None   # test hook: runs between a batch's match and its answer
+        self.before_submit = None  # test hook: runs between the overlay read and the match
+
+    def epoch(self):
+        return self.ep
 
     def build(self, blob, off):
         b = blob.tobytes()
         self.staged = {b[int(off[i]):int(off[i + 1])]: i for i in range(len(off) - 1)}
         self.committed = dict(self.staged)
+        self.ep += 1
 
     def apply(self, inserts=None, deletes=None, insert_ids=None):
         for f, i in zip(inserts or [], insert_ids or []):
@@ -52,8 +60,12 @@ class OracleNif:
 
     def commit(self):
         self.committed = dict(self.staged)
+        self.ep += 1
+        return self.ep
 
     def submit(self, blob, off, mode):
+        if self.before_submit is not None:
+            self.before_submit()
         if self.fail:
             raise RuntimeError("device failure (injected)")
         trie = R.Trie()
@@ -63,11 +75,14 @@ class OracleNif:
         rows = [[self.committed[f] for f in trie.match(b[int(off[i]):int(off[i + 1])])]
                 for i in range(len(off) - 1)]
         t = len(self.tickets) + 1
-        self.tickets[t] = rows
+        self.tickets[t] = (rows, self.ep)
         return t
 
     def wait(self, t):
-        return self._Res(self.tickets.pop(t))
+        if self.before_wait is not None:
+            self.before_wait()
+        rows, ep = self.tickets.pop(t)
+        return self._Res(rows, ep)
 
 
 def _reference(routes):
@@ -87,7 +102,7 @@ def _stack(nif, fallback=None, linger_ms=1.0):
         ref = _reference({t: [r.dest for r in routes.lookup_routes(t)] for t in routes.topics()})
         return [Route(t, d) for t, d in ref.match_routes(topic)]
 
-    srv = BatchServer(routes, filters, fallback or fb, batch_size=64, linger_ms=linger_ms)
+    srv = BatchServer(routes, filters, fallback or fb, batch_size=64, linger_ms=linger_ms, overlay=sync.overlay)
     return routes, filters, sync, srv
 
 
@@ -228,6 +243,127 @@ def test_random_routes_vs_reference_router():
     _random_vs_reference(OracleNif(), 7)
 
 
+def _subscribe_then_publish(nif):
+    """a match issued right after add_route returns sees the
+    route, with no flush of the route sync in between (the reference adds the
+    route inside the synchronous subscribe call, emqx_broker.erl:153,438-440)."""
+    routes, filters, sync, srv = _stack(nif)
+    try:
+        routes.add_route(b"a/b", "n")
+        assert sorted(srv.match_routes(b"a/b")) == [Route(b"a/b", "n")]
+        routes.add_route(b"a/+", "n")            # no sync.publish()
+        assert sorted(srv.match_routes(b"a/b")) == [Route(b"a/+", "n"), Route(b"a/b", "n")]
+        assert srv.overlay_hits >= 1
+        routes.add_route(b"#", "m")
+        routes.add_route(b"a/+", "m")            # second dest of a filter already pending
+        got = sorted(srv.match_routes(b"a/b"))
+        assert got == [Route(b"#", "m"), Route(b"a/+", "m"), Route(b"a/+", "n"), Route(b"a/b", "n")]
+        assert srv.match_routes(b"$SYS/x") == []  # '#' never matches a '$' topic (emqx_topic.erl:71-74)
+        sync.publish()                           # now in the GPU table: overlay drained
+        assert sync.overlay.size() == 0
+        assert sorted(srv.match_routes(b"a/b")) == got
+        routes.delete_route(b"a/+", "n")         # a stale id expands to nothing
+        routes.delete_route(b"a/+", "m")
+        assert sorted(srv.match_routes(b"a/b")) == [Route(b"#", "m"), Route(b"a/b", "n")]
+        assert srv.fallbacks == 0
+    finally:
+        srv.stop()
+
+
+def test_subscribe_then_publish_without_flush():
+    _subscribe_then_publish(OracleNif())
+
+
+def test_overlay_races():
+    nif = OracleNif()
+    routes, filters, sync, srv = _stack(nif)
+    try:
+        # the flush runs between the batch's match (old epoch) and its answer
+        nif.before_wait = sync.publish
+        routes.add_route(b"r/+", "n")
+        assert srv.match_routes(b"r/1") == [Route(b"r/+", "n")]
+        nif.before_wait = None
+        # the flush runs between the overlay read and the submit: the epoch it publishes is matched
+        nif.before_submit = sync.publish
+        routes.add_route(b"q/+", "n")
+        assert srv.match_routes(b"q/1") == [Route(b"q/+", "n")]
+        nif.before_submit = None
+        # the linger fires inside the route transaction (not yet committed): the
+        # pending entry survives that flush and the route is still seen after
+        def slow_trans():
+            sync.on_event("write", ("emqx_route", b"s/+", "n"))   # a stray early event
+            sync.publish()                                          # has_routes/1 still false
+            return routes._trans_add(b"s/+", "n")
+        ref_hook = routes.pending_hook
+        assert ref_hook(b"s/+", slow_trans) == "ok"
+        assert srv.match_routes(b"s/1") == [Route(b"s/+", "n")]
+        sync.publish()
+        assert srv.match_routes(b"s/1") == [Route(b"s/+", "n")]
+        # an aborted transaction leaves nothing behind
+        routes.fail_next_trans = True
+        assert routes.add_route(b"t/+", "n") == "aborted"
+        assert sync.overlay.lookup_pending(b"t/+") is None
+        assert srv.match_routes(b"t/1") == []
+        # records tagged `route` instead of the table name are not this table's events
+        sync.on_event("write", ("route", b"u/+", "n"))
+        assert not sync.due() and b"u/+" not in sync._touched
+        sync.publish()
+        assert sync.overlay.size() == 0
+        assert srv.fallbacks == 0
+    finally:
+        srv.stop()
+
+
+def _threaded_churn(nif, n_threads=4, per_thread=40):
+    """Every match issued after an add_route returned contains its route, while
+    a syncer flushes at random moments and other routes are deleted."""
+    import threading
+
+    routes, filters, sync, srv = _stack(nif, linger_ms=0.2)
+    stop = threading.Event()
+    errors = []
+
+    def syncer():
+        rng = random.Random(5)
+        while not stop.is_set():
+            sync.publish()
+            stop.wait(rng.random() * 0.004)
+
+    def worker(k):
+        rng = random.Random(100 + k)
+        try:
+            for i in range(per_thread):
+                f = b"c/%d/%d/+" % (k, i)
+                routes.add_route(f, "n%d" % k)
+                got = srv.match_routes(b"c/%d/%d/x" % (k, i))
+                if Route(f, "n%d" % k) not in got:
+                    errors.append((f, got))
+                if i and rng.random() < 0.3:
+                    routes.delete_route(b"c/%d/%d/+" % (k, i - 1), "n%d" % k)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=syncer)] + [threading.Thread(target=worker, args=(k,)) for k in range(n_threads)]
+    try:
+        for t in ts:
+            t.start()
+        for t in ts[1:]:
+            t.join()
+        stop.set()
+        ts[0].join()
+        assert not errors, errors[:3]
+        assert srv.fallbacks == 0
+        sync.publish()
+        assert sync.overlay.size() == 0
+    finally:
+        stop.set()
+        srv.stop()
+
+
+def test_threaded_churn_subscribe_then_publish():
+    _threaded_churn(OracleNif())
+
+
 # ---- the same sequences with the real library as the NIF -----------------
 @pytest.mark.gpu
 def test_t_match_routes_through_mirror_gpu():
@@ -245,5 +381,25 @@ def test_random_routes_vs_reference_router_gpu():
     gm = GpuMatcher(0)
     try:
         _random_vs_reference(gm, 11)
+    finally:
+        gm.close()
+
+
+@pytest.mark.gpu
+def test_subscribe_then_publish_without_flush_gpu():
+    from emqx_amd.engine import GpuMatcher
+    gm = GpuMatcher(0)
+    try:
+        _subscribe_then_publish(gm)
+    finally:
+        gm.close()
+
+
+@pytest.mark.gpu
+def test_threaded_churn_subscribe_then_publish_gpu():
+    from emqx_amd.engine import GpuMatcher
+    gm = GpuMatcher(0)
+    try:
+        _threaded_churn(gm)
     finally:
         gm.close()

@@ -253,6 +253,34 @@ def test_pipeline_tickets_are_generational_and_cancellable(gm):
     assert np.array_equal(r3.row_ptr, r1.row_ptr)
 
 
+def test_cancel_never_blocks_on_a_busy_context(gm):
+    """egm_match_cancel (the NIF ticket destructor, a normal
+    scheduler) must not wait for the context lock a bulk build holds for
+    seconds: it is queued and applied by the next pipeline call."""
+    import threading
+    import time
+    f, t = synth.config("c0", n_topics=10_000)
+    gm.build(f.blob, f.off)
+    tk = gm.submit(t.blob, t.off, L.EGM_MODE_TRIE)
+    big, _ = synth.config("c1", n_filters=1_000_000, n_topics=1)
+    th = threading.Thread(target=lambda: gm.build(big.blob, big.off))
+    th.start()
+    time.sleep(0.3)                      # the build holds the context lock now
+    t0 = time.monotonic()
+    gm.cancel(tk)                        # queued: returns at once
+    dt = time.monotonic() - t0
+    busy = th.is_alive()
+    th.join(timeout=300)
+    assert dt < 0.1, f"cancel blocked {dt:.3f} s"
+    with pytest.raises(L.EgmError) as e:
+        gm.wait(tk)                      # the queued cancel was applied: no result
+    assert e.value.code == L.EGM_E_STATE
+    gm.build(f.blob, f.off)
+    r = gm.wait(gm.submit(t.blob, t.off, L.EGM_MODE_TRIE))   # the slot came back
+    assert len(r.row_ptr) == t.n + 1
+    print(f"cancel took {dt * 1e3:.2f} ms while the build {'was' if busy else 'was not'} running")
+
+
 def test_match_batch_many_threads_never_pipeline_full(gm):
     """more than 8 concurrent egm_match_batch callers (dirty
     schedulers) queue for pipeline slots instead of failing, also while the
