@@ -505,7 +505,8 @@ struct alignas(16) WaveLds {
   uint32_t stage_fid[WALK_STAGE];
   uint16_t stage_rank[WALK_STAGE];
   uint8_t stage_t[WALK_STAGE];       // topic in chunk of the emit
-  uint32_t words[WALK_WORDS];        // the sub-chunk's word ids, [topic][level]
+  uint32_t words[WALK_WORDS + 1];    // the sub-chunk's word ids, [topic][level] (+1: a leaf's
+                                     // unclamped next-word read, never used)
   uint32_t tinfo[WALK_CHUNK];        // D | tflags << 24 | words at the fixed stride << 31
   uint32_t cnt[WALK_CHUNK];          // ids per topic, whole chunk
   uint32_t fcnt[WALK_CHUNK];         // ids per topic in the current stage / start inside the flush
@@ -677,9 +678,10 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* words
   p.h0 = ld16(bp + 16);
   p.l1 = ld16(bp + 32);
   p.h1 = ld16(bp + 48);
-  // the next level's word (clamped; used only if level + 1 < D)
-  const uint32_t nl = min((meta & LEVEL_MAX) + 1, p.D - 1);
-  p.nw = words ? words[nl] : wid[p.act ? gbase + nl : 0u];
+  // the next level's word (used only if level + 1 < D).  From the LDS stage
+  // it is read unclamped, so the read does not wait for the topic's depth
+  // (a leaf reads the next topic's word 0, or the pad word past the stage).
+  p.nw = words ? words[(meta & LEVEL_MAX) + 1] : wid[p.act ? gbase + min((meta & LEVEL_MAX) + 1, p.D - 1) : 0u];
 }
 
 // Children and emits of one popped item.
