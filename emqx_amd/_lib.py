@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("EGM_LIB") or os.path.join(_HERE, "libemqx_gpu_match.so")  # EGM_LIB: A/B tuning
 
 EGM_OK = 0
+EGM_PREFIX_ALL = 0xFFFFFFFF
 EGM_E_INVAL = -1
 EGM_E_NOMEM = -2
 EGM_E_DEVICE = -3
@@ -99,6 +100,8 @@ SIGNATURES = {
     "egm_match_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(C.POINTER(egm_result))]),
     "egm_match_cancel": (C.c_int, [_P, C.c_uint64]),
     "egm_match_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, _P, _P, C.c_uint64, _P]),
+    "egm_match_device_counted": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, _P, C.c_int, _P, _P, _P,
+                                           C.c_uint64]),
     "egm_last_stats": (C.c_int, [_P, _u64p, _u64p, _u32p, _u32p, _u32p]),
     "egm_last_guard": (C.c_int, [_P, _u32p]),
     "egm_last_walk_counters": (C.c_int, [_P, _u64p, _u64p, _u64p, _u64p, _u64p]),
@@ -112,6 +115,10 @@ SIGNATURES = {
     "egm_last_fanout": (C.c_int, [_P, _u64p, _u32p]),
     "egm_shard_merge": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, C.POINTER(_P), C.c_uint64, _P, _P, _P,
                                   C.c_uint64]),
+    "egm_prefix_assign": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P]),
+    "egm_prefix_slot_bytes": (C.c_uint64, [C.c_uint32, C.c_uint32, C.c_uint64]),
+    "egm_prefix_route": (C.c_int, [_P, _P, _P, C.c_uint32, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, _P,
+                                   _P]),
     "egm_result_free": (None, [_P]),
     "egm_rstore_open": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "egm_rstore_close": (None, [_P]),

@@ -106,6 +106,7 @@ struct PipeSlot {
     if (ev_out) hipEventDestroy(ev_out);
   }
 };
+constexpr uint32_t PREFIX_RANKS_MAX = 16;   // ranks of one prefix partition (kernel limit)
 constexpr size_t PIPE_MAX_SLOTS = 8;     // tickets of egm_match_submit busy or held at once
 constexpr size_t PIPE_HARD_SLOTS = 16;   // all slots, egm_match_batch's included (then it waits); each
                                          // keeps buffers for the largest batch it saw (~ dirty schedulers)
@@ -193,6 +194,8 @@ struct egm_ctx {
 
   // shard merge
   DevBuf m_srow, m_tiles, m_tot;
+  // prefix partition routing
+  DevBuf p_ctr, p_dst;
 
   // fan-out
   DevBuf sub_row, sub_rp, sub_ids, f_dc, f_ds0, f_dpos, f_tiles, f_ovf, f_mrow, f_mids, f_drow, f_dfid, f_dsub;
@@ -653,8 +656,10 @@ static MatchWork work_view(egm_ctx* c, MatchWs& W) {
 }
 
 static int run_match(egm_ctx* c, MatchWs& W, const Epoch& ep, const uint8_t* d_blob, const uint32_t* d_off,
-                     uint32_t n, int mode, hipStream_t s, uint64_t* d_row, uint32_t* d_ids, uint64_t ids_cap) {
+                     uint32_t n, int mode, hipStream_t s, uint64_t* d_row, uint32_t* d_ids, uint64_t ids_cap,
+                     const uint32_t* d_n_live = nullptr) {
   MatchWork w = work_view(c, W);
+  w.n_live = d_n_live;
   if (ep.bytes < walk_sort_min_bytes()) w.key_shape = 0;   // the table fits the caches: the order buys nothing
   MatchOut o{d_row, d_ids, ids_cap};
   hipEvent_t evp[2] = {nullptr, nullptr};
@@ -905,6 +910,23 @@ int egm_match_device(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, con
     hipError_t e = hipMemcpyAsync(d_flags, W.tfl.p, n, hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) r = c->hip_fail(e, "flags copy");
   }
+  ws_done(W, s);
+  return r;
+}
+
+int egm_match_device_counted(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_off,
+                             uint32_t n_max, const uint32_t* d_n, int mode, void* hip_stream, uint64_t* d_row,
+                             uint32_t* d_ids, uint64_t ids_cap) {
+  if (!c || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES) || !d_row || !d_n) return EGM_E_INVAL;
+  if (n_max && (!d_blob || !d_off || ((uintptr_t)d_blob & 3))) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  MatchWs& W = pick_ws(c, s);
+  int r = ensure_work(c, W, n_max, blob_bytes, ids_cap, std::min<uint64_t>(blob_bytes, 65535) + 1);
+  if (r) return r;
+  std::shared_ptr<Epoch> ep = c->cur;
+  r = run_match(c, W, *ep, d_blob, d_off, n_max, mode, s, d_row, d_ids, ids_cap, d_n);
   ws_done(W, s);
   return r;
 }
@@ -1567,6 +1589,67 @@ int egm_shard_assign(const uint8_t* blob, const uint32_t* off, uint32_t n, uint3
   for (uint32_t i = 0; i < n; ++i) out[i] = filter_shard(blob + off[i], off[i + 1] - off[i], g);
   return EGM_OK;
 }
+// ---- prefix partition ----
+int egm_prefix_assign(const uint8_t* blob, const uint32_t* off, uint32_t n, uint32_t n_vparts, uint32_t n_ranks,
+                      uint8_t* vpart_rank, uint32_t* filter_rank) {
+  if (!off || !vpart_rank || !filter_rank || n_vparts == 0 || n_ranks == 0 || n_ranks > PREFIX_RANKS_MAX ||
+      (n && !blob))
+    return EGM_E_INVAL;
+  std::vector<uint64_t> load(n_vparts, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t* p = blob + off[i];
+    const uint32_t len = off[i + 1] - off[i];
+    if (prefix_replicated(p, len)) {
+      filter_rank[i] = EGM_PREFIX_ALL;
+    } else {
+      const uint32_t v = prefix_vpart(p, len, n_vparts);
+      filter_rank[i] = v;   // the vpart for now, its rank below
+      load[v] += 1;
+    }
+  }
+  // greedy: the heaviest virtual partitions first, each to the least loaded
+  // rank (ties: the lower vpart, the lower rank) — deterministic on every rank
+  std::vector<uint32_t> order(n_vparts);
+  for (uint32_t v = 0; v < n_vparts; ++v) order[v] = v;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return load[a] > load[b]; });
+  std::vector<uint64_t> rl(n_ranks, 0);
+  for (uint32_t v : order) {
+    uint32_t best = 0;
+    for (uint32_t k = 1; k < n_ranks; ++k)
+      if (rl[k] < rl[best]) best = k;
+    vpart_rank[v] = (uint8_t)best;
+    rl[best] += load[v];
+  }
+  for (uint32_t i = 0; i < n; ++i)
+    if (filter_rank[i] != EGM_PREFIX_ALL) filter_rank[i] = vpart_rank[filter_rank[i]];
+  return EGM_OK;
+}
+
+uint64_t egm_prefix_slot_bytes(uint32_t n_ranks, uint32_t cap_topics, uint64_t cap_bytes) {
+  const PrefixSlots ps{n_ranks, cap_topics, cap_bytes};
+  return ps.slot_bytes();
+}
+
+int egm_prefix_route(egm_ctx* c, const uint8_t* d_blob, const uint32_t* d_off, uint32_t n, const uint8_t* d_vpart_rank,
+                     uint32_t n_vparts, uint32_t n_ranks, uint32_t cap_topics, uint64_t cap_bytes, void* hip_stream,
+                     uint8_t* d_send) {
+  if (!c || !d_vpart_rank || !d_send || n_vparts == 0 || n_ranks == 0 || n_ranks > PREFIX_RANKS_MAX ||
+      (n && (!d_blob || !d_off)) || cap_bytes >= (1ull << 32))
+    return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipError_t e;
+  if ((e = c->p_ctr.ensure(8 * PREFIX_RANKS_MAX)) != hipSuccess) return c->hip_fail(e, "prefix counters");
+  if ((e = c->p_dst.ensure(8ull * std::max<uint32_t>(n, 1))) != hipSuccess) return c->hip_fail(e, "prefix routes");
+  c->work_begin(s);
+  const PrefixSlots ps{n_ranks, cap_topics, cap_bytes};
+  e = launch_prefix_route(d_blob, d_off, n, d_vpart_rank, n_vparts, ps, d_send, c->p_ctr.as<unsigned long long>(),
+                          c->p_dst.as<uint64_t>(), s);
+  c->work_end(s);
+  return e == hipSuccess ? EGM_OK : c->hip_fail(e, "launch_prefix_route");
+}
+
 uint64_t egm_word_hash(const uint8_t* p, uint32_t len) { return word_hash(p, len); }
 uint32_t egm_edge_bucket(uint32_t parent, uint32_t w, uint32_t mask) { return edge_bucket(parent, w, mask); }
 

@@ -54,6 +54,7 @@ constexpr uint8_t TF_WILDCARD = 1;   // topic has a '+' or '#' word (emqx_topic.
 constexpr uint8_t TF_DOLLAR   = 2;   // first word starts with '$' (emqx_trie.erl:208-215)
 constexpr uint8_t TF_HEAVY    = 4;   // matched by the overflow (heavy) kernel
 constexpr uint8_t TF_ERROR    = 8;   // could not be matched (see egm_last_error)
+constexpr uint8_t TF_SKIP     = 16;  // padding past a device-side topic count (egm_match_device_counted): no walk
 
 constexpr int EDGE_BUCKET = 4;       // slots per 64 B bucket
 
@@ -138,6 +139,36 @@ EGM_HD uint32_t edge_bucket(uint32_t parent, uint32_t wid, uint32_t mask) {
   h *= 0x85EBCA6Bu;
   h ^= h >> 13;
   return h & mask;
+}
+
+// Multi-GPU prefix partition (SURVEY §8e "partition by root word", two words
+// deep: C2's level-0 vocabulary has 16 Zipf-distributed words).  The key of a
+// filter or topic is its bytes up to (not including) the second '/': "a/b" for
+// a/b/..., the whole name for a one-level one.  Every topic a filter with
+// literal first two words can match has that filter's key; a filter whose
+// first or second word is '+' or '#' can match any key and is replicated.
+// Keys hash into n_vparts virtual partitions, mapped to ranks by the host.
+EGM_HD uint32_t prefix_key_len(const uint8_t* p, uint32_t len) {
+  uint32_t slashes = 0;
+  for (uint32_t i = 0; i < len; ++i)
+    if (p[i] == '/' && ++slashes == 2) return i;
+  return len;
+}
+
+EGM_HD uint32_t prefix_vpart(const uint8_t* p, uint32_t len, uint32_t n_vparts) {
+  return (uint32_t)(word_hash(p, prefix_key_len(p, len)) % n_vparts);
+}
+
+// A filter that must live on every rank: '+' or '#' as its first or second word.
+EGM_HD bool prefix_replicated(const uint8_t* p, uint32_t len) {
+  uint32_t ws = 0, level = 0;
+  for (uint32_t i = 0; i <= len && level < 2; ++i) {
+    if (i < len && p[i] != '/') continue;
+    if (i - ws == 1 && (p[ws] == '+' || p[ws] == '#')) return true;
+    ws = i + 1;
+    ++level;
+  }
+  return false;
 }
 
 // filter -> shard assignment for multi-GPU filter sharding

@@ -81,6 +81,7 @@ struct MatchWork {                // per-batch device workspace
   void* sort_tmp;                 // radix sort scratch
   size_t sort_tmp_bytes;
   uint32_t key_shape;             // key bits per level, nibble l = level l (0: walk in input order)
+  const uint32_t* n_live;         // device count of real topics (null: all n); the rest are skipped padding
 };
 
 constexpr uint32_t KEY_LEVELS = 4;           // levels hashed into the walk-order key
@@ -90,6 +91,7 @@ struct WalkOrderOut {                        // what k_tokenise writes for the s
   uint64_t* val;
   uint32_t* wfix;
   uint32_t shape;
+  const uint32_t* n_live;                    // topics at or past *n_live are padding: TF_SKIP (null: none)
 };
 
 constexpr uint32_t GUARD_STACK = 4u;         // a push would have overrun a work stack (the pop bound makes it impossible)
@@ -160,6 +162,26 @@ struct ShardIds {
 hipError_t launch_shard_merge(const uint32_t* cnt, uint32_t G, uint32_t n, const ShardIds& src, uint64_t* srow,
                               uint64_t* tile_sums, uint32_t* tot, uint64_t* row, uint32_t* out, uint64_t cap,
                               hipStream_t s);
+
+// Prefix partition exchange (egm_common.h prefix_vpart): a rank's
+// topic batch -> n_ranks slots of slot_bytes each, one per destination rank,
+// laid out for an equal-split all_to_all:
+//   [0, 16)          header {count, bytes, overflow, 0}
+//   [16, 16 + 4Ct)   source topic index of each slot topic
+//   [PO, PO + 4(Ct+1)) offsets into the slot's bytes (entries past count = bytes)
+//   [PB, PB + Cb)    topic bytes
+// Overflow (a destination got more than Ct topics or Cb bytes) is flagged in
+// the header; the slot is then incomplete and the step must be redone.
+struct PrefixSlots {
+  uint32_t n_ranks, cap_topics;
+  uint64_t cap_bytes;
+  __host__ __device__ uint64_t off_offsets() const { return 16 + 4ull * cap_topics; }
+  __host__ __device__ uint64_t off_bytes() const { return (off_offsets() + 4ull * (cap_topics + 1) + 15) & ~15ull; }
+  __host__ __device__ uint64_t slot_bytes() const { return (off_bytes() + cap_bytes + 15) & ~15ull; }
+};
+hipError_t launch_prefix_route(const uint8_t* blob, const uint32_t* off, uint32_t n, const uint8_t* vpart_rank,
+                               uint32_t n_vparts, const PrefixSlots& ps, uint8_t* send, unsigned long long* ctr,
+                               uint64_t* dst, hipStream_t s);
 
 // Scatter n records of rec_bytes (4, 16 or 32) from src[] to dst[idx[i]]:
 // the incremental epoch commit of egm_capi.cpp.

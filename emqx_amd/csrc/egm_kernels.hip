@@ -258,6 +258,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
   const uint32_t blk0 = blockIdx.x * TOK_BLOCK;
   if (blk0 >= n) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t n_live = wo.n_live ? min(*wo.n_live, n) : n;   // topics past it: padding (TF_SKIP)
   const uint32_t tend = min(blk0 + (uint32_t)TOK_BLOCK, n);
   uint32_t S = TOK_BLOCK;
   for (uint32_t t0 = blk0; t0 < tend;) {
@@ -277,6 +278,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         uint32_t l;
         uint8_t fl;
         tokenise_one(tab, (const uint32_t*)(blob + (ts & ~3u)), ts & 3u, len, ts + t0, wid, &l, &fl);
+        if (t0 >= n_live) fl |= TF_SKIP;
         lv[t0] = l;
         tfl[t0] = fl;
         if (wo.key) {
@@ -306,6 +308,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
       }
       D = c + 1;
       if (len > 0 && lds_byte(sw, ts) == '$') fl |= TF_DOLLAR;
+      if (t >= n_live) fl |= TF_SKIP;
     }
     uint32_t wtot;
     uint32_t ex = wave_excl_scan(D, lane, &wtot);
@@ -327,6 +330,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         uint32_t l;
         uint8_t f;
         tokenise_one(tab, sw, ts, len, off[t] + t, wid, &l, &f);
+        if (t >= n_live) f |= TF_SKIP;
         lv[t] = l;
         tfl[t] = f;
         if (wo.key) {
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         uint32_t w4[KEY_LEVELS];
 #pragma unroll
         for (uint32_t k = 0; k < KEY_LEVELS; ++k) w4[k] = kw[tid][k];
-        wo.key[t] = walk_key(w4, D, wo.shape);
+        wo.key[t] = (tflag[tid] & TF_SKIP) ? 0xFFFFFFFFu : walk_key(w4, D, wo.shape);   // padding sorts last
         wo.val[t] = sort_val(t, D, tflag[tid] & 0xFFu, D <= FIX_WORDS);
       }
     }
@@ -922,8 +926,8 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
           const uint32_t gj = __shfl(gb, (int)min(j, (uint32_t)WALK_CHUNK - 1), 64);
           if (lane < k) {
             const uint32_t ti = L.tinfo[j], Dj = ti & 0xFFFFFFu, tf = (ti >> 24) & 0x7Fu;
-            if (tf & TF_WILDCARD) {
-              if (mode == MODE_ROUTES) em = exact_walk(tab, topic_words(w, ti, gj), Dj, &fid);
+            if (tf & (TF_WILDCARD | TF_SKIP)) {   // padding: no walk, no ids
+              if (mode == MODE_ROUTES && !(tf & TF_SKIP)) em = exact_walk(tab, topic_words(w, ti, gj), Dj, &fid);
             } else {
               const bool dollar = (tf & TF_DOLLAR) != 0;
               em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
@@ -1093,9 +1097,9 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
     const bool fixed = w.order && (rec >> 63);
     const uint32_t* words = fixed ? w.wfix : w.wid;
     const uint32_t D = uni(w.lv[t]), tf = uni(w.tfl[t]), tb = uni(fixed ? t * FIX_WORDS : off[t] + t);
-    if (tf & TF_WILDCARD) {   // no trie walk: TRIE mode matches nothing, ROUTES mode one exact lookup
+    if (tf & (TF_WILDCARD | TF_SKIP)) {   // no trie walk: TRIE mode matches nothing, ROUTES mode one exact lookup
       uint32_t fid = NONE;
-      const bool em = mode == MODE_ROUTES && exact_walk(tab, words + tb, D, &fid);
+      const bool em = mode == MODE_ROUTES && !(tf & TF_SKIP) && exact_walk(tab, words + tb, D, &fid);
       if (lane == 0) {
         if (em) {
           const unsigned long long base = atomicAdd(&w.stats->cursor, 1ull);
@@ -1367,11 +1371,24 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
 }
 
 // Fixed blocks -> CSR rows in input order: one wave per 64 consecutive
-// topics, whose rows are one contiguous run of the output (whole lines
-// written), each topic's block a contiguous run of ids_fix (its walk position
-// x fix_cap): the same windowed copy as k_compact with the topics as the runs.
+// topics, whose rows are one contiguous run of the output.
+//
+// Round 4: a quarter-wave (16 lanes) copies one topic's
+// run — lane l moves ids k*16 + l of the block — so every load instruction
+// reads one 64-B line per quarter (a block is 16-B aligned: cap*4 B, cap a
+// multiple of 16... or not: the loads are then two lines) and every store
+// writes 64 contiguous bytes of the row, with no per-id owner search.  The
+// wave takes its 64 topics four at a time, two rounds per step so 8 loads per
+// lane are in flight; loads are unconditional (clamped to the run's last id:
+// a load under a branch is waited for at the branch's end) and the stores
+// are predicated.  Round 3's version (a wave scan laying the 64 runs out as
+// one range, 8 ids per lane, a 6-step LDS binary search per id to find its
+// run) stays under EGM_COMPACT_FIX_QUARTER=0 for A/B.
 // (A chunk-major variant — rank-major blocks staged through LDS and rows
 // written scattered — measured 6x slower: DESIGN.md §4.1.)
+#ifndef EGM_COMPACT_FIX_QUARTER
+#define EGM_COMPACT_FIX_QUARTER 1
+#endif
 __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact_fix(const uint32_t* __restrict__ cnt,
                                                                     const uint32_t* __restrict__ inv,
                                                                     const uint32_t* __restrict__ ids_fix,
@@ -1379,6 +1396,54 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact_fix(const uint32
                                                                     const uint64_t* __restrict__ row_ptr,
                                                                     uint32_t* __restrict__ ids, uint64_t ids_cap,
                                                                     MatchStats* stats) {
+#if EGM_COMPACT_FIX_QUARTER
+  __shared__ uint32_t s_c[COMPACT_WAVES][64];
+  __shared__ uint64_t s_src[COMPACT_WAVES][64];
+  __shared__ uint64_t s_dst[COMPACT_WAVES][64];
+  if (!compact_checks(row_ptr, n, ids_cap, stats)) return;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t q = lane >> 4, l16 = lane & 15;
+  const uint32_t ngroups = (n + 63) / 64;
+  for (uint32_t g = blockIdx.x * COMPACT_WAVES + wave; g < ngroups; g += gridDim.x * COMPACT_WAVES) {
+    const uint32_t t = min(g * 64 + lane, n - 1);
+    const uint32_t p = inv[t], ct = cnt[t];   // independent loads, in flight together
+    const uint64_t rp = row_ptr[t];
+    const uint32_t c = min(ct, cap) & ((g * 64 + lane < n && p != NONE) ? 0xFFFFFFFFu : 0u);
+    s_c[wave][lane] = c;
+    s_src[wave][lane] = (uint64_t)(p != NONE ? p : 0u) * cap;
+    s_dst[wave][lane] = rp;
+    uint32_t cm = c;   // the wave's longest run: how many 16-id steps a round needs
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cm = max(cm, (uint32_t)__shfl_xor(cm, d, 64));
+    const uint32_t steps = uni((cm + 15) / 16);
+    wave_sync();
+#pragma unroll 1
+    for (uint32_t j = 0; j < 16; j += 2) {   // topics 4j + q and 4(j+1) + q
+      const uint32_t ta = 4 * j + q, tb = ta + 4;
+      const uint32_t ca = s_c[wave][ta], cb = s_c[wave][tb];
+      const uint64_t sa = s_src[wave][ta], sb = s_src[wave][tb];
+      const uint64_t da = s_dst[wave][ta], db = s_dst[wave][tb];
+      const uint32_t la = ca ? ca - 1 : 0u, lb = cb ? cb - 1 : 0u;
+#pragma unroll 1
+      for (uint32_t k0 = 0; k0 < steps; k0 += 4) {
+        uint32_t va[4], vb[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          const uint32_t i = (k0 + k) * 16 + l16;
+          va[k] = ids_fix[sa + min(i, la)];
+          vb[k] = ids_fix[sb + min(i, lb)];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          const uint32_t i = (k0 + k) * 16 + l16;
+          if (i < ca) ids[da + i] = va[k];
+          if (i < cb) ids[db + i] = vb[k];
+        }
+      }
+    }
+    wave_sync();
+  }
+#else
   __shared__ uint32_t s_scan[COMPACT_WAVES][64];
   __shared__ uint64_t s_src[COMPACT_WAVES][64];
   __shared__ uint64_t s_dst[COMPACT_WAVES][64];
@@ -1398,6 +1463,7 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact_fix(const uint32
     copy_runs(ids_fix, ids, s_scan[wave], s_src[wave], s_dst[wave], tot, lane);
     wave_sync();
   }
+#endif
 }
 
 // ------------------------------------------------------------- launchers ----
@@ -1481,7 +1547,8 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
     if (tb > w.sort_tmp_bytes) return hipErrorInvalidValue;   // a host sizing bug: never sort into too little scratch
   }
   WalkOrderOut wo{};
-  if (sorted) wo = WalkOrderOut{w.skey, w.sval, w.wfix, w.key_shape};
+  if (sorted) wo = WalkOrderOut{w.skey, w.sval, w.wfix, w.key_shape, nullptr};
+  wo.n_live = w.n_live;
   hipLaunchKernelGGL(k_tokenise, dim3((n + TOK_BLOCK - 1) / TOK_BLOCK), dim3(TOK_BLOCK), 0, s, tab, blob,
                      off, n, w.wid, w.lv, w.tfl, wo);
   trace(s, "k_tokenise");
@@ -1735,6 +1802,108 @@ hipError_t launch_shard_merge(const uint32_t* cnt, uint32_t G, uint32_t n, const
     const uint32_t gf = (uint32_t)std::min<uint64_t>((n + 64 * MERGE_WAVES - 1) / (64 * MERGE_WAVES), 16384);
     hipLaunchKernelGGL(k_merge_fill, dim3(gf), dim3(64 * MERGE_WAVES), 0, s, cnt, srow, src, G, n, row, out, cap);
   }
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------- prefix partition --
+// Route a rank's topic batch to the ranks owning its prefix (SURVEY §8e,
+// "partition by root word"; egm_common.h prefix_vpart): each topic goes to
+// rank vpart_rank[prefix_vpart(topic)], into that rank's slot of the send
+// buffer (PrefixSlots, egm_kernels.h).  One thread per topic finds its key
+// (the bytes before the second '/') and its slot position: a block first
+// counts its topics per destination with LDS atomics on a packed
+// {topics << 40 | bytes} counter, then takes one global range per destination
+// (G atomics per block instead of one per topic: 10M per-topic atomics on 8
+// counters would serialise), so a topic's index and byte offset in its slot
+// come from one counter and stay in step.  k_prefix_copy then moves the
+// bytes, a quarter-wave per topic; k_prefix_finish writes the headers.
+constexpr uint32_t PREFIX_MAX_RANKS = 16;
+constexpr unsigned long long PFX_BYTES_MASK = (1ull << 40) - 1;
+
+__global__ __launch_bounds__(256) void k_prefix_route(const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off,
+                                                      uint32_t n, const uint8_t* __restrict__ vpart_rank,
+                                                      uint32_t n_vparts, PrefixSlots ps, uint8_t* __restrict__ send,
+                                                      unsigned long long* __restrict__ ctr, uint64_t* __restrict__ dst) {
+  __shared__ unsigned long long lctr[PREFIX_MAX_RANKS], lbase[PREFIX_MAX_RANKS];
+  const uint32_t tid = threadIdx.x, G = ps.n_ranks;
+  if (tid < G) lctr[tid] = 0;
+  __syncthreads();
+  const uint32_t t = blockIdx.x * 256 + tid;
+  uint32_t r = 0, len = 0;
+  unsigned long long loc = 0;
+  if (t < n) {
+    const uint32_t a = off[t];
+    len = off[t + 1] - a;
+    r = vpart_rank[prefix_vpart(blob + a, len, n_vparts)];
+    loc = atomicAdd(&lctr[r], (1ull << 40) | len);
+  }
+  __syncthreads();
+  if (tid < G) lbase[tid] = lctr[tid] ? atomicAdd(&ctr[tid], lctr[tid]) : 0ull;
+  __syncthreads();
+  if (t < n) {
+    const unsigned long long pos = (lbase[r] >> 40) + (loc >> 40);
+    const unsigned long long bpos = (lbase[r] & PFX_BYTES_MASK) + (loc & PFX_BYTES_MASK);
+    const bool ok = pos < ps.cap_topics && bpos + len <= ps.cap_bytes;
+    dst[t] = ok ? ((uint64_t)r | (pos << 8) | (bpos << 32)) : ~0ull;   // ~0: dropped (the header says overflow)
+    if (ok) {
+      uint8_t* slot = send + (uint64_t)r * ps.slot_bytes();
+      ((uint32_t*)(slot + 16))[pos] = t;
+      ((uint32_t*)(slot + ps.off_offsets()))[pos] = (uint32_t)bpos;
+    }
+  }
+}
+
+// A quarter-wave (16 lanes) per topic copies its bytes into its slot.
+__global__ __launch_bounds__(256) void k_prefix_copy(const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off,
+                                                     uint32_t n, PrefixSlots ps, uint8_t* __restrict__ send,
+                                                     const uint64_t* __restrict__ dst) {
+  const uint32_t q = threadIdx.x >> 4, l16 = threadIdx.x & 15;
+  for (uint64_t t = (uint64_t)blockIdx.x * 16 + q; t < n; t += (uint64_t)gridDim.x * 16) {
+    const uint64_t d = dst[t];
+    if (d == ~0ull) continue;
+    const uint32_t a = off[t], len = off[t + 1] - a;
+    uint8_t* out = send + (uint64_t)(d & 0xFF) * ps.slot_bytes() + ps.off_bytes() + (d >> 32);
+    for (uint32_t i = l16; i < len; i += 16) out[i] = blob[a + i];
+  }
+}
+
+// Headers, and the offsets past each slot's count (= its bytes: empty padding
+// topics, skipped by egm_match_device_counted through the count).
+__global__ __launch_bounds__(256) void k_prefix_finish(PrefixSlots ps, uint8_t* __restrict__ send,
+                                                       const unsigned long long* __restrict__ ctr) {
+  const uint32_t r = blockIdx.y;
+  uint8_t* slot = send + (uint64_t)r * ps.slot_bytes();
+  const unsigned long long c = ctr[r];
+  const uint64_t nt = c >> 40, nb = c & PFX_BYTES_MASK;
+  const bool ovf = nt > ps.cap_topics || nb > ps.cap_bytes;
+  const uint32_t cnt = (uint32_t)min<uint64_t>(nt, ps.cap_topics);
+  const uint32_t bytes = (uint32_t)min<uint64_t>(nb, ps.cap_bytes);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t* h = (uint32_t*)slot;
+    h[0] = cnt;
+    h[1] = bytes;
+    h[2] = ovf ? 1u : 0u;
+    h[3] = 0;
+  }
+  uint32_t* po = (uint32_t*)(slot + ps.off_offsets());
+  for (uint64_t k = cnt + (uint64_t)blockIdx.x * 256 + threadIdx.x; k <= ps.cap_topics; k += (uint64_t)gridDim.x * 256)
+    po[k] = bytes;
+}
+
+hipError_t launch_prefix_route(const uint8_t* blob, const uint32_t* off, uint32_t n, const uint8_t* vpart_rank,
+                               uint32_t n_vparts, const PrefixSlots& ps, uint8_t* send, unsigned long long* ctr,
+                               uint64_t* dst, hipStream_t s) {
+  if (ps.n_ranks == 0 || ps.n_ranks > PREFIX_MAX_RANKS || n_vparts == 0) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * ps.n_ranks, s);
+  if (e != hipSuccess) return e;
+  if (n) {
+    hipLaunchKernelGGL(k_prefix_route, dim3((n + 255) / 256), dim3(256), 0, s, blob, off, n, vpart_rank, n_vparts, ps,
+                       send, ctr, dst);
+    const uint32_t gc = (uint32_t)std::min<uint64_t>((n + 15) / 16, 65536);
+    hipLaunchKernelGGL(k_prefix_copy, dim3(gc), dim3(256), 0, s, blob, off, n, ps, send, dst);
+  }
+  const uint32_t gx = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)ps.cap_topics + 256) / 256, 1024));
+  hipLaunchKernelGGL(k_prefix_finish, dim3(gx, ps.n_ranks), dim3(256), 0, s, ps, send, ctr);
   return hipGetLastError();
 }
 

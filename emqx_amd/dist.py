@@ -7,7 +7,17 @@ Two layouts, both over ``torch.distributed`` (backend "nccl" = RCCL on ROCm,
   table (10M filters is ~2 GB of a 288 GB HBM3E card) and matches its own
   slice of the topic stream.  Topics are independent units, so there is no
   data-path collective — weak scaling.
-* **shard** (tables too large or too slow for one GPU): filters are split by
+* **prefix** (tables too large for one GPU, the layout that scales): filters
+  are partitioned by their first two words (``egm_prefix_assign``: keys hash
+  into virtual partitions mapped to ranks by filter count; a filter with '+' or
+  '#' in its first two levels is replicated), every rank routes its OWN topic
+  batch to the key owners (``egm_prefix_route``, HIP) and ONE
+  ``all_to_all_single`` exchanges the fixed-size slots; each rank matches the
+  slots it received against its partition (``egm_match_device_counted``, the
+  topic count read on the device).  No broadcast, no gather, no host sync per
+  step; results stay on the owner rank (where, in a broker, the owner's
+  subscribers are dispatched).  ``PrefixExchange``.
+* **shard** (round 3, kept for comparison): filters are split by
   ``word_hash(filter) mod G`` (egm_common.h filter_shard) with global filter
   ids; rank 0's topic batch is broadcast, every rank matches it against its
   shard, per-topic counts are all-gathered and the id lists gathered to rank 0
@@ -201,6 +211,172 @@ def gpu_merge(gm, stream: int, out_row, out_ids):
         return out_row[: n + 1], out_ids[:total]
 
     return merge
+
+
+# ---------------------------------------------------------------- prefix ----
+N_VPARTS = 4096
+
+
+def prefix_assign(strings, n_ranks: int, n_vparts: int = N_VPARTS) -> Tuple[np.ndarray, np.ndarray]:
+    """(vpart_rank u8[n_vparts], filter_rank u32[n]) — egm_prefix_assign; a
+    filter_rank of L.EGM_PREFIX_ALL means the filter lives on every rank."""
+    lib = L.load()
+    off = np.ascontiguousarray(strings.off, dtype=np.uint32)
+    n = len(off) - 1
+    vr = np.zeros(n_vparts, dtype=np.uint8)
+    fr = np.zeros(n, dtype=np.uint32)
+    rc = lib.egm_prefix_assign(C.c_void_p(strings.blob.ctypes.data), C.c_void_p(off.ctypes.data), n, n_vparts,
+                               n_ranks, C.c_void_p(vr.ctypes.data), C.c_void_p(fr.ctypes.data))
+    if rc != 0:
+        raise L.EgmError(rc, "egm_prefix_assign")
+    return vr, fr
+
+
+class PrefixSlots:
+    """The send/receive slot layout of egm_prefix_route (include/emqx_gpu_match.h)."""
+
+    def __init__(self, n_ranks: int, cap_topics: int, cap_bytes: int):
+        self.n_ranks, self.cap_topics, self.cap_bytes = n_ranks, cap_topics, cap_bytes
+        self.off_tids = 16
+        self.off_offsets = 16 + 4 * cap_topics
+        self.off_bytes = (self.off_offsets + 4 * (cap_topics + 1) + 15) & ~15
+        self.slot_bytes = (self.off_bytes + cap_bytes + 15) & ~15
+        assert self.slot_bytes == int(L.load().egm_prefix_slot_bytes(n_ranks, cap_topics, cap_bytes))
+
+    @classmethod
+    def for_batch(cls, n_ranks: int, n_topics: int, n_bytes: int, slack: float = 1.25):
+        """Capacities for batches of up to n_topics / n_bytes per rank, spread
+        over n_ranks owners with `slack` for imbalance (C2 at 8 ranks: the
+        busiest owner gets 1.03x the mean)."""
+        ct = int(n_topics * slack / n_ranks) + 1024
+        cb = int(n_bytes * slack / n_ranks) + 65536
+        return cls(n_ranks, ct, cb)
+
+    def parse(self, buf: np.ndarray, r: int):
+        """Slot r of a host copy of a send/receive buffer: (count, bytes,
+        overflow, source topic indices, offsets[count+1], topic bytes)."""
+        s = buf[r * self.slot_bytes:(r + 1) * self.slot_bytes]
+        h = s[:16].view(np.uint32)
+        cnt, nb, ovf = int(h[0]), int(h[1]), int(h[2])
+        tids = s[self.off_tids:self.off_tids + 4 * cnt].view(np.uint32)
+        offs = s[self.off_offsets:self.off_offsets + 4 * (cnt + 1)].view(np.uint32)
+        return cnt, nb, ovf, tids, offs, s[self.off_bytes:self.off_bytes + nb]
+
+
+def prefix_key(topic: bytes) -> bytes:
+    """The partition key: the bytes before the second '/' (egm_common.h prefix_key_len)."""
+    i = topic.find(b"/")
+    if i < 0:
+        return topic
+    j = topic.find(b"/", i + 1)
+    return topic if j < 0 else topic[:j]
+
+
+def prefix_route_reference(blob: np.ndarray, off: np.ndarray, vpart_rank: np.ndarray, ps: PrefixSlots) -> np.ndarray:
+    """Host restatement of egm_prefix_route (the gloo path and the GPU test's
+    checker): the same slots, topics in input order within a slot (the kernel
+    may order them differently: per-topic content is what is compared)."""
+    lib = L.load()
+    G, V = ps.n_ranks, len(vpart_rank)
+    out = np.zeros(G * ps.slot_bytes, dtype=np.uint8)
+    b = blob.tobytes()
+    per = [[] for _ in range(G)]
+    for t in range(len(off) - 1):
+        tp = b[int(off[t]):int(off[t + 1])]
+        k = prefix_key(tp)
+        r = int(vpart_rank[int(lib.egm_word_hash(k, len(k))) % V])
+        per[r].append((t, tp))
+    for r in range(G):
+        base = r * ps.slot_bytes
+        items = per[r]
+        nbytes = sum(len(x) for _, x in items)
+        ovf = len(items) > ps.cap_topics or nbytes > ps.cap_bytes
+        if ovf:   # what the kernel keeps is unspecified then: only the flag is compared
+            out[base:base + 16] = np.array([min(len(items), ps.cap_topics), min(nbytes, ps.cap_bytes), 1, 0],
+                                           dtype=np.uint32).view(np.uint8)
+            continue
+        tids = np.array([t for t, _ in items], dtype=np.uint32)
+        lens = np.array([len(x) for _, x in items], dtype=np.uint64)
+        offs = np.full(ps.cap_topics + 1, nbytes, dtype=np.uint32)
+        offs[:len(items)] = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint32) if len(items) else []
+        out[base:base + 16] = np.array([len(items), nbytes, 0, 0], dtype=np.uint32).view(np.uint8)
+        out[base + ps.off_tids:base + ps.off_tids + 4 * len(items)] = tids.view(np.uint8)
+        out[base + ps.off_offsets:base + ps.off_offsets + 4 * (ps.cap_topics + 1)] = offs.view(np.uint8)
+        data = b"".join(x for _, x in items)
+        out[base + ps.off_bytes:base + ps.off_bytes + len(data)] = np.frombuffer(data, dtype=np.uint8)
+    return out
+
+
+SlotMatch = Callable[["object", int], object]
+
+
+class PrefixExchange:
+    """One step of the prefix-partition layout on every rank (torch.distributed):
+
+      1. route this rank's own topic batch into n_ranks slots    [HIP egm_prefix_route]
+      2. all_to_all_single of the equal-size slots               [RCCL over xGMI]
+      3. match each received slot against this rank's partition [egm_match_device_counted]
+
+    ``route(blob, off, n) -> send`` (uint8 tensor of n_ranks * slot_bytes) and
+    ``match_slot(recv, g) -> result`` are injected: the GPU path in production
+    (``gpu_route`` / ``gpu_match_slot``), numpy + the oracle in the gloo tests.
+    A slot's topic count is read from its header on the device; an overflowed
+    slot (header flag) makes the step invalid — ``overflow_flag`` accumulates
+    the received flags on the device, and the caller checks it when it syncs
+    anyway (no host sync per step)."""
+
+    def __init__(self, rank: int, world: int, device, ps: PrefixSlots, route, match_slot: SlotMatch, group=None):
+        import torch
+        self.rank, self.world, self.device, self.ps = rank, world, device, ps
+        self.route, self.match_slot, self.group = route, match_slot, group
+        self.recv = torch.empty(world * ps.slot_bytes, dtype=torch.uint8, device=device)
+        self.overflow_flag = torch.zeros(1, dtype=torch.int64, device=device)
+
+    def step(self, blob, off, n: int):
+        import torch
+        import torch.distributed as dist
+        send = self.route(blob, off, n)                                          # 1. route
+        if self.world > 1:
+            dist.all_to_all_single(self.recv, send, group=self.group)           # 2. exchange
+            recv = self.recv
+        else:
+            recv = send
+        hdr = recv.view(self.world, self.ps.slot_bytes)[:, :16].view(torch.int32)
+        self.overflow_flag += hdr[:, 2].to(torch.int64).sum()                    # stays on the device
+        return [self.match_slot(recv, g) for g in range(self.world)]             # 3. match
+
+    def overflowed(self) -> bool:
+        """Any overflow so far (a host sync: call it where the caller syncs anyway)."""
+        return bool(self.overflow_flag.item())
+
+
+def gpu_route(gm, ps: PrefixSlots, d_vpart_rank, stream: int, send):
+    """route() of PrefixExchange on the GPU: egm_prefix_route into `send` (a
+    device uint8 tensor of ps.n_ranks * ps.slot_bytes)."""
+
+    def route(blob, off, n):
+        gm.prefix_route(blob.data_ptr(), off.data_ptr(), n, d_vpart_rank.data_ptr(), d_vpart_rank.numel(), ps.n_ranks,
+                        ps.cap_topics, ps.cap_bytes, stream, send.data_ptr())
+        return send
+
+    return route
+
+
+def gpu_match_slot(gm, ps: PrefixSlots, mode: int, stream: int, rows: list, ids: list):
+    """match_slot() of PrefixExchange on the GPU: slot g of the received buffer
+    matched in place (no copy) with its count read on the device; rows[g]
+    (int64[cap_topics + 1]) and ids[g] (int32) are the caller's output buffers.
+    Returns (row, ids, source topic indices) views of slot g."""
+    import torch
+
+    def match_slot(recv, g):
+        base = recv.data_ptr() + g * ps.slot_bytes
+        gm.match_device_counted(base + ps.off_bytes, ps.cap_bytes, base + ps.off_offsets, ps.cap_topics, base, mode,
+                                stream, rows[g].data_ptr(), ids[g].data_ptr(), ids[g].numel())
+        tids = recv[g * ps.slot_bytes + ps.off_tids:g * ps.slot_bytes + ps.off_offsets].view(torch.int32)
+        return rows[g], ids[g], tids
+
+    return match_slot
 
 
 def topic_slice(n: int, rank: int, world: int) -> Tuple[int, int]:

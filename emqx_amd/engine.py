@@ -218,6 +218,19 @@ class GpuMatcher:
         self._check(self.lib.egm_match_device(self.ctx, d_blob, blob_bytes, d_off, n, mode, stream or None, d_row,
                                               d_ids, ids_cap, d_flags or None), "egm_match_device")
 
+    def match_device_counted(self, d_blob: int, blob_bytes: int, d_off: int, n_max: int, d_n: int, mode: int,
+                             stream: int, d_row: int, d_ids: int, ids_cap: int):
+        """egm_match_device over a batch whose topic count (<= n_max) is at d_n on the device."""
+        self._check(self.lib.egm_match_device_counted(self.ctx, d_blob, blob_bytes, d_off, n_max, d_n, mode,
+                                                      stream or None, d_row, d_ids, ids_cap),
+                    "egm_match_device_counted")
+
+    def prefix_route(self, d_blob: int, d_off: int, n: int, d_vpart_rank: int, n_vparts: int, n_ranks: int,
+                     cap_topics: int, cap_bytes: int, stream: int, d_send: int):
+        """egm_prefix_route: a device topic batch -> n_ranks slots (egm_prefix_slot_bytes each) at d_send."""
+        self._check(self.lib.egm_prefix_route(self.ctx, d_blob, d_off, n, d_vpart_rank, n_vparts, n_ranks,
+                                              cap_topics, cap_bytes, stream or None, d_send), "egm_prefix_route")
+
     def cancel(self, ticket: int):
         """Give a submitted ticket up without its result (egm_match_cancel)."""
         self._check(self.lib.egm_match_cancel(self.ctx, ticket), "egm_match_cancel")

@@ -176,6 +176,15 @@ int egm_match_cancel(egm_ctx* ctx, uint64_t ticket);
 int egm_match_device(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_offsets,
                      uint32_t n_topics, int mode, void* hip_stream, uint64_t* d_row_ptr, uint32_t* d_ids,
                      uint64_t ids_cap, uint8_t* d_flags);
+/* egm_match_device over a batch whose topic count is on the device: the
+   first *d_n (<= n_max) topics are matched, the rest (padding; their offsets
+   must still be valid, e.g. empty topics at the end) get empty rows without a
+   walk.  For batches whose size only the device knows — the received slots of
+   the prefix partition exchange (egm_prefix_route) — so the host never waits
+   for a count.  d_row_ptr[n_max] holds the number of ids. */
+int egm_match_device_counted(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_offsets,
+                             uint32_t n_max, const uint32_t* d_n, int mode, void* hip_stream, uint64_t* d_row_ptr,
+                             uint32_t* d_ids, uint64_t ids_cap);
 /* Synchronises the last device batch and reports its counters.  overflow != 0
    means ids_cap was too small (rerun with a larger buffer) — capacity only.
    Returns EGM_E_DEVICE (counters still filled) when a walk guard tripped:
@@ -247,6 +256,34 @@ int egm_last_fanout(egm_ctx* ctx, uint64_t* n_deliveries, uint32_t* overflow);
 int egm_shard_merge(egm_ctx* ctx, uint32_t n_shards, uint32_t n_topics, const uint32_t* d_counts,
                     const uint32_t* const* d_shard_ids, uint64_t total_ids, void* hip_stream, uint64_t* d_row_ptr,
                     uint32_t* d_ids, uint64_t ids_cap);
+
+/* ---- multi-GPU prefix partition ("partition by root word") ----
+   Filters and topics are keyed by their bytes before the second '/' (the
+   first two words, or the whole of a one-level name); keys hash into
+   n_vparts virtual partitions that map to ranks.  A filter whose first or
+   second word is '+' or '#' can match any key and lives on every rank
+   (EGM_PREFIX_ALL); every other filter only on its key's rank — every topic
+   it can match has its key.  A topic is matched on exactly one rank, against
+   all the filters that can match it, so the ranks' rows together are the
+   whole table's with no merge, and a topic batch crosses xGMI once (one
+   all_to_all), with no broadcast and no gather.  The reference replicates its
+   tables instead (apps/emqx/src/emqx_trie.erl:53, emqx_router.erl:71).
+   egm_prefix_assign (host): vpart_rank[n_vparts] (greedy by filter counts,
+   deterministic) and filter_rank[n] (a rank or EGM_PREFIX_ALL).
+   egm_prefix_route (device, async on hip_stream): a batch -> n_ranks slots of
+   egm_prefix_slot_bytes() each in d_send, slot r for rank r:
+     [0,16) {count, bytes, overflow, 0}; [16, 16+4*cap_topics) source topic
+     index of each slot topic; then offsets u32[cap_topics+1] (entries past
+     count = bytes); then the topic bytes (cap_bytes), all 16-B aligned.
+   A slot past its capacity sets overflow (its content is then incomplete:
+   redo the step with larger capacities). */
+#define EGM_PREFIX_ALL 0xFFFFFFFFu
+int egm_prefix_assign(const uint8_t* blob, const uint32_t* offsets, uint32_t n, uint32_t n_vparts, uint32_t n_ranks,
+                      uint8_t* vpart_rank, uint32_t* filter_rank);
+uint64_t egm_prefix_slot_bytes(uint32_t n_ranks, uint32_t cap_topics, uint64_t cap_bytes);
+int egm_prefix_route(egm_ctx* ctx, const uint8_t* d_blob, const uint32_t* d_offsets, uint32_t n_topics,
+                     const uint8_t* d_vpart_rank, uint32_t n_vparts, uint32_t n_ranks, uint32_t cap_topics,
+                     uint64_t cap_bytes, void* hip_stream, uint8_t* d_send);
 
 void egm_result_free(void* result);
 

@@ -151,3 +151,130 @@ def test_shard_exchange_rccl_world1(gm):
         assert np.array_equal(canonical(row, ids), canonical(whole.row_ptr, whole.ids))
     finally:
         dist.destroy_process_group()
+
+
+# ---- prefix partition ------------------------------------
+def _prefix_setup(f, world, n_vparts=4096):
+    from emqx_amd.dist import prefix_assign
+    vr, fr = prefix_assign(f, world, n_vparts)
+    return vr, fr
+
+
+def test_prefix_route_kernel_vs_reference(gm):
+    """egm_prefix_route (HIP) against its host restatement: per destination
+    slot the same header, and the same source topic -> bytes pairs (the kernel
+    orders a slot's topics by block arrival, so pairs are compared as sets);
+    offsets consistent with the bytes; an undersized slot reports overflow."""
+    import torch
+    from emqx_amd.dist import PrefixSlots, prefix_route_reference
+    dev = torch.device("cuda:0")
+    f, t = synth.config("c2", n_filters=50_000, n_topics=60_000)
+    for world in (1, 3, 8):
+        vr, _ = _prefix_setup(f, world)
+        ps = PrefixSlots.for_batch(world, t.n, len(t.blob))
+        want = prefix_route_reference(t.blob, t.off, vr, ps)
+        blob = torch.from_numpy(t.blob.copy()).to(dev)
+        off = torch.from_numpy(t.off.view(np.int32).copy()).to(dev)
+        dvr = torch.from_numpy(vr).to(dev)
+        send = torch.zeros(world * ps.slot_bytes, dtype=torch.uint8, device=dev)
+        gm.prefix_route(blob.data_ptr(), off.data_ptr(), t.n, dvr.data_ptr(), len(vr), world, ps.cap_topics,
+                        ps.cap_bytes, torch.cuda.current_stream().cuda_stream, send.data_ptr())
+        torch.cuda.synchronize()
+        got = send.cpu().numpy()
+        tl = t.to_list()
+        total = 0
+        for r in range(world):
+            gc, gb, go, gt, goff, gdata = ps.parse(got, r)
+            wc, wb, wo, wt, woff, wdata = ps.parse(want, r)
+            assert (gc, gb, go) == (wc, wb, wo) == (wc, wb, 0), (world, r)
+            full = got[r * ps.slot_bytes + ps.off_offsets:][:4 * (ps.cap_topics + 1)].view(np.uint32)
+            assert np.all(full[gc:] == gb)   # padding topics: empty, at the end
+            pairs = {int(gt[k]): bytes(gdata[int(goff[k]):int(goff[k + 1])]) for k in range(gc)}
+            assert len(pairs) == gc and all(pairs[k] == tl[k] for k in pairs)
+            assert set(pairs) == set(int(x) for x in wt)
+            total += gc
+        assert total == t.n
+    # capacities too small: overflow flagged in the header
+    small = PrefixSlots(2, 100, 1 << 16)
+    vr, _ = _prefix_setup(f, 2)
+    send = torch.zeros(2 * small.slot_bytes, dtype=torch.uint8, device=dev)
+    gm.prefix_route(blob.data_ptr(), off.data_ptr(), t.n, torch.from_numpy(vr).to(dev).data_ptr(), len(vr), 2,
+                    small.cap_topics, small.cap_bytes, 0, send.data_ptr())
+    torch.cuda.synchronize()
+    assert all(small.parse(send.cpu().numpy(), r)[2] == 1 for r in range(2))
+
+
+def _prefix_logical(f, t, world, mode=L.EGM_MODE_ROUTES):
+    """`world` ranks emulated on one GPU: each holds its partition (replicated
+    filters + its keys, global ids) in a context of its own and routes its own
+    slice of the batch; the all_to_all is a device copy of slot r of every
+    sender into rank r's receive buffer; each rank matches its received slots
+    with egm_match_device_counted (count read on the device).  Returns, per
+    topic of the batch, its ids (as a CSR in batch order) and the partition
+    sizes."""
+    import torch
+    from emqx_amd.dist import PrefixSlots, topic_slice
+    dev = torch.device("cuda:0")
+    vr, fr = _prefix_setup(f, world)
+    fl = f.to_list()
+    parts = [t.subset(np.arange(*topic_slice(t.n, r, world))) for r in range(world)]
+    ps = PrefixSlots.for_batch(world, max(p.n for p in parts), max(len(p.blob) for p in parts))
+    dvr = torch.from_numpy(vr).to(dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    sends, sizes, ctxs = [], [], []
+    for r in range(world):
+        idx = np.nonzero((fr == r) | (fr == L.EGM_PREFIX_ALL))[0]
+        sizes.append(len(idx))
+        g = GpuMatcher(0, max_batch=ps.cap_topics)
+        blob, off = pack_strings([fl[i] for i in idx])
+        g.build(blob, off, idx.astype(np.uint32))
+        ctxs.append(g)
+        p = parts[r]
+        b = torch.from_numpy(p.blob.copy()).to(dev)
+        o = torch.from_numpy(p.off.view(np.int32).copy()).to(dev)
+        send = torch.zeros(world * ps.slot_bytes, dtype=torch.uint8, device=dev)
+        g.prefix_route(b.data_ptr(), o.data_ptr(), p.n, dvr.data_ptr(), len(vr), world, ps.cap_topics,
+                       ps.cap_bytes, stream, send.data_ptr())
+        sends.append(send)
+    rows_by_topic = [None] * t.n
+    for q in range(world):
+        recv = torch.cat([sends[r][q * ps.slot_bytes:(q + 1) * ps.slot_bytes] for r in range(world)])
+        for r in range(world):
+            base = recv.data_ptr() + r * ps.slot_bytes
+            row = torch.zeros(ps.cap_topics + 1, dtype=torch.int64, device=dev)
+            ids = torch.zeros(ps.cap_topics * 64 + 4096, dtype=torch.int32, device=dev)
+            ctxs[q].match_device_counted(base + ps.off_bytes, ps.cap_bytes, base + ps.off_offsets, ps.cap_topics, base,
+                                         mode, stream, row.data_ptr(), ids.data_ptr(), ids.numel())
+            torch.cuda.synchronize()
+            st = ctxs[q].last_stats()
+            assert st["overflow"] == 0 and st["errors"] == 0
+            cnt, nb, ovf, tids, offs, data = ps.parse(recv.cpu().numpy(), r)
+            assert ovf == 0
+            rown = row.cpu().numpy()
+            idn = ids.cpu().numpy().view(np.uint32)
+            assert np.all(rown[cnt:] == rown[cnt])   # padding topics: empty rows
+            lo = topic_slice(t.n, r, world)[0]
+            for k in range(cnt):
+                i = lo + int(tids[k])
+                assert rows_by_topic[i] is None      # matched on exactly one rank
+                rows_by_topic[i] = idn[rown[k]:rown[k + 1]]
+    for g in ctxs:
+        g.close()
+    row = np.zeros(t.n + 1, np.uint64)
+    row[1:] = np.cumsum([len(x) for x in rows_by_topic])
+    ids = np.concatenate(rows_by_topic) if t.n else np.zeros(0, np.uint32)
+    return row, ids.astype(np.uint32), sizes
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_prefix_partitions_equal_whole_table(gm, world):
+    """The prefix layout's rows, over every rank, equal the whole table's
+    (ROUTES mode, C2 shape at 300K filters); no rank holds the whole table."""
+    f, t = synth.config("c2", n_filters=300_000, n_topics=150_000)
+    row, ids, sizes = _prefix_logical(f, t, world)
+    gm.build(f.blob, f.off)
+    want = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    assert np.array_equal(row, want.row_ptr)
+    assert np.array_equal(canonical(row, ids), canonical(want.row_ptr, want.ids))
+    if world > 1:
+        assert max(sizes) < f.n

@@ -84,6 +84,8 @@ for step in "$@"; do
       run granule_tcc 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d "$R/gpurun_out/${TAG}_granule_tcc" -o run --output-format csv -- "$R/tools/granule" ;;
     walkmix)   # what bounds the walk: its memory mix with 0-600 VALU per round at 8-32 waves per CU (tools/walkmix.hip)
       run walkmix 300 "$R/tools/walkmix" ;;
+    d2h)   # device <-> pinned host copy rates (tools/d2hbench.hip)
+      run d2h 120 "$R/tools/d2hbench" ;;
     c4m) run c4m 400 python $R/bench.py --config c4 --filters 10000000 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
     c4m_*)  # the same on variant V (tools/build_variant.py)
       v=${step#c4m_}
