@@ -16,12 +16,20 @@ the line's `pipelined` (`--streams 2` makes that the timed mode instead).
 Layouts (emqx_amd/dist.py), named in the line's config.workload:
   replicate (default)  every GPU holds the 10M-filter table and matches its own
                        10M-topic batch; no data-path collective -> "weak".
-  shard                filters split over the GPUs, rank 0's batch broadcast,
-                       counts and ids gathered to rank 0 over RCCL and merged
-                       by the HIP merge kernel -> "strong" (BASELINE config C2
-                       as worded); runs its collectives at every world size.
+  prefix               filters partitioned by their first two words (a filter
+                       with '+'/'#' there on every rank); every GPU routes its
+                       OWN 10M-topic batch to the prefix owners with one RCCL
+                       all_to_all and matches what it receives against its
+                       partition -> "weak"; no broadcast, no gather, no host
+                       sync per step (SURVEY §8e "partition by root word").
+  shard                (round 3) filters split by hash, rank 0's batch
+                       broadcast, counts and ids gathered to rank 0 over RCCL
+                       and merged by the HIP merge kernel -> "strong".
 
-    python bench.py [--gpus N --steps K --warmup W] [--config c2] [--mode replicate|shard]
+At N>1 the replicate `value` is followed by the prefix layout timed on the
+same node (the line's `sharded`; --sharded-layout shard for the round-3 one).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config c2] [--mode replicate|prefix|shard]
 
 Rank 0 prints ONE JSON line on stdout; progress goes to stderr.
 """
@@ -184,6 +192,9 @@ def _heartbeat(period: float = 30.0):
 LAYOUTS = {
     "replicate": "replicated table: every GPU holds all filters and matches its own topic batch "
                  "(no data-path collective)",
+    "prefix": "prefix-partitioned: filters split by their first two words (those with '+'/'#' there on every "
+              "rank), every GPU routes its own topic batch to the prefix owners with one RCCL all_to_all and "
+              "matches what it receives; results stay on the owner (no broadcast, no gather)",
     "shard": "filter-sharded: filters split over the GPUs by word_hash(filter) mod N, rank 0's topic batch "
              "broadcast, per-topic counts and ids gathered to rank 0 and merged by the HIP merge kernel "
              "(RCCL over xGMI; at N=1 the collectives are no-ops)",
@@ -307,6 +318,112 @@ class ShardLeg:
         return None if self.fanout else sum(self.ex.last_totals)
 
 
+class PrefixLeg:
+    """The prefix-partition layout on this rank (dist.PrefixExchange):
+    this rank's partition of the filters (egm_prefix_assign: replicated filters
+    + its prefixes, global ids) in `gm`, its own topic batch in HBM; a step
+    routes the batch (egm_prefix_route), exchanges the slots with one
+    all_to_all_single and matches each received slot in place
+    (egm_match_device_counted: the slot's count is read on the device)."""
+
+    def __init__(self, gm, f, t, rank, world, dev, stream, mode, have_pg, slack=1.25):
+        import torch
+        import torch.distributed as dist
+        from emqx_amd import _lib as L
+        from emqx_amd.dist import PrefixExchange, PrefixSlots, gpu_match_slot, gpu_route, prefix_assign
+        self.gm, self.rank, self.world, self.dev, self.sp, self.mode = gm, rank, world, dev, stream, mode
+        vr, fr = prefix_assign(f, world)
+        idx = np.nonzero((fr == rank) | (fr == L.EGM_PREFIX_ALL))[0].astype(np.uint32)
+        self.replicated = int(np.count_nonzero(fr == L.EGM_PREFIX_ALL))
+        sub = f.subset(idx)
+        gm.build(sub.blob, sub.off, idx)
+        self.n_filters = len(idx)
+        del sub, fr
+        self.n = t.n
+        # the slots are the layout's (equal all_to_all splits): sized from the largest batch of any rank
+        mx = torch.tensor([t.n, len(t.blob)], dtype=torch.int64, device=dev)
+        if have_pg:
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        self.ps = ps = PrefixSlots.for_batch(world, int(mx[0].item()), int(mx[1].item()), slack)
+        self.d_blob = torch.from_numpy(t.blob).to(dev)
+        self.d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+        self.d_vr = torch.from_numpy(vr).to(dev)
+        self.send = torch.zeros(world * ps.slot_bytes, dtype=torch.uint8, device=dev)
+        self.rows = [torch.zeros(ps.cap_topics + 1, dtype=torch.int64, device=dev) for _ in range(world)]
+        self.cap = 64 * ps.cap_topics + 4096
+        self.idss = [torch.zeros(self.cap, dtype=torch.int32, device=dev) for _ in range(world)]
+        self._make()
+
+    def _make(self):
+        from emqx_amd.dist import PrefixExchange, gpu_match_slot, gpu_route
+        route = gpu_route(self.gm, self.ps, self.d_vr, self.sp, self.send)
+        match = gpu_match_slot(self.gm, self.ps, self.mode, self.sp, self.rows, self.idss)
+        self.ex = PrefixExchange(self.rank, self.world, self.dev, self.ps, route, match)
+
+    def step(self):
+        return self.ex.step(self.d_blob, self.d_off, self.n)
+
+    def size(self):
+        """Untimed steps until every received slot's ids fit (grown from the
+        device totals); a slot overflow means the slack is too small."""
+        import torch
+        for _ in range(4):
+            self.step()
+            torch.cuda.synchronize(self.dev)
+            if self.ex.overflowed():
+                raise RuntimeError("prefix leg: a destination slot overflowed (raise the slack)")
+            need = max(int(r[self.ps.cap_topics].item()) for r in self.rows)
+            if need <= self.cap:
+                return
+            self.cap = int(need * 1.25) + 1024
+            self.idss = [torch.zeros(self.cap, dtype=torch.int32, device=self.dev) for _ in range(self.world)]
+            self._make()
+        raise RuntimeError("prefix leg: buffers did not settle")
+
+    def merged_ids(self):
+        return None
+
+    def check(self):
+        """After the timed steps (the caller has synced): no slot overflow, ids fit."""
+        assert not self.ex.overflowed(), "prefix slot overflow"
+        ids = [int(r[self.ps.cap_topics].item()) for r in self.rows]
+        assert max(ids) <= self.cap, (ids, self.cap)
+        return sum(ids)
+
+    def census(self):
+        """One untimed step with a sync after every slot's match: the step's
+        totals (levels, states created, ids, topics received) for the byte model."""
+        import torch
+        st = {"levels": 0, "visited": 0, "ids": 0, "topics": 0}
+        self.ex.route(self.d_blob, self.d_off, self.n)
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_to_all_single(self.ex.recv, self.send)
+            recv = self.ex.recv
+        else:
+            recv = self.send
+        torch.cuda.synchronize(self.dev)
+        host = recv.cpu().numpy()
+        for g in range(self.world):
+            cnt, nb, ovf, tids, offs, data = self.ps.parse(host, g)
+            self.ex.match_slot(recv, g)
+            ls = self.gm.last_stats()
+            st["levels"] += int(np.count_nonzero(data == ord("/"))) + cnt
+            st["visited"] += ls["visited"]
+            st["ids"] += ls["n_ids"]
+            st["topics"] += cnt
+        return st
+
+
+def prefix_cost_model(n, blob_bytes, world, ps):
+    """Bytes one prefix-partition step moves: each rank sends
+    (N-1)/N of its slots over xGMI in one all_to_all; the route kernel reads
+    the batch and writes the slots."""
+    slots = world * ps.slot_bytes
+    return {"all_to_all_bytes_per_rank": int(slots * (world - 1) / world), "slot_bytes": ps.slot_bytes,
+            "cap_topics_per_slot": ps.cap_topics, "route_bytes": blob_bytes + 4 * (n + 1) + 8 * n + slots}
+
+
 def shard_cost_model(n, blob_bytes, world, merged_ids):
     """Bytes one sharded step moves over xGMI: the broadcast
     of the batch to N-1 ranks, the gather of N-1 shards' counts and ids to
@@ -371,6 +488,9 @@ def main():
                          "(egm_fanout_device_compact), or as (filter, subscriber) pairs (egm_fanout_device)")
     ap.add_argument("--sharded-timeout", type=float, default=300.0,
                     help="seconds the sharded leg may take before the line is printed without it")
+    ap.add_argument("--sharded-layout", default="prefix", choices=["prefix", "shard"],
+                    help="the layout of the sharded leg: prefix partition (one all_to_all, weak) or the round-3 "
+                         "filter shards (broadcast + gather + merge, strong); with fan-out always shard")
     ap.add_argument("--sharded-leg", default="auto", choices=["auto", "on", "off"],
                     help="replicate mode at N>1 (auto) or any N (on): also time the filter-sharded layout "
                          "(BASELINE C2 as worded: broadcast + RCCL gather + GPU merge; with fan-out, fan-out on "
@@ -399,6 +519,7 @@ def main():
     dev = torch.device("cuda", local)
     have_pg = _init_dist(args, rank, world, dev)
     shard = args.mode == "shard"
+    prefix = args.mode == "prefix"
     mode = L.EGM_MODE_ROUTES if args.match == "routes" else L.EGM_MODE_TRIE
 
     c = synth.CONFIGS[args.config]
@@ -422,9 +543,9 @@ def main():
 
     gm = GpuMatcher(local, max_batch=nt)
     t0 = time.time()
-    nstreams = 1 if (shard or fanout) else max(1, args.streams)
-    piped = args.pipelined == "on" and not shard and not fanout and nstreams == 1
-    serial_leg = args.pipelined == "on" and not shard and not fanout and nstreams > 1
+    nstreams = 1 if (shard or prefix or fanout) else max(1, args.streams)
+    piped = args.pipelined == "on" and args.mode == "replicate" and not fanout and nstreams == 1
+    serial_leg = args.pipelined == "on" and args.mode == "replicate" and not fanout and nstreams > 1
     nbuf = 2 if piped else nstreams
     streams = [torch.cuda.Stream(dev) for _ in range(nbuf)]
     stream = streams[0]
@@ -433,6 +554,10 @@ def main():
     leg = None
     if shard:
         leg = ShardLeg(gm, f, t, rank, world, dev, sp, mode, fanout, seed)
+    elif prefix:
+        if fanout:
+            raise SystemExit("--mode prefix: match only (the fan-out would run on the owner rank; not timed here)")
+        leg = PrefixLeg(gm, f, t, rank, world, dev, sp, mode, have_pg)
     else:
         gm.build(f.blob, f.off)
     tstats = gm.stats()
@@ -524,7 +649,9 @@ def main():
     torch.cuda.synchronize(dev)
     st = gm.last_stats()
     assert st["overflow"] == 0 and st["errors"] == 0, st
-    if leg is not None:
+    if prefix:
+        leg.check()
+    elif leg is not None:
         assert not leg.ex.last_overflow
 
     gm.set_timing(True)
@@ -543,6 +670,8 @@ def main():
         elapsed = float(e.item())
     tim = gm.get_timing()
     st = gm.last_stats()
+    if prefix:
+        leg.check()
     deliveries = int(d_drow[n].item()) if (fanout and leg is None) else None
     if fanout and leg is not None:   # every rank's own part of the batch's deliveries, summed
         dt = torch.tensor([leg.last_deliveries], dtype=torch.int64, device=dev)
@@ -624,15 +753,21 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # ---- roofline (dominant kernel = k_walk), SURVEY §8d byte model ----
-    sum_d = levels_sum(t.blob, t.off)
-    n_ids = st["n_ids"]
-    visited = st["visited"]
-    walk_bytes = 8 * sum_d + 32 * visited + 4 * (n_ids + n)
     walk_ms = tim["walk_ms"] / max(1, tim["walk_launches"])
+    if prefix:
+        # one walk launch per received slot: the byte model over the step's
+        # totals (an untimed census step), the kernel time over its launches
+        cz = leg.census()
+        sum_d, n_ids, visited, n_walked = cz["levels"], cz["ids"], cz["visited"], cz["topics"]
+        walk_ms *= world
+    else:
+        sum_d = levels_sum(t.blob, t.off)
+        n_ids, visited, n_walked = st["n_ids"], st["visited"], n
+    walk_bytes = 8 * sum_d + 32 * visited + 4 * (n_ids + n_walked)
     achieved = walk_bytes / (walk_ms * 1e-3) / 1e9
     path_bytes = (nbytes + 4 * n) + 16 * sum_d + 32 * visited + 4 * (n_ids + n)
 
-    traffic = walk_traffic(args.config, f.n, n) if (not shard and world == 1) else None
+    traffic = walk_traffic(args.config, f.n, n) if (args.mode == "replicate" and world == 1) else None
     host = None
     if _host_leg(args, world, shard):
         log("[rank 0] timing the host-visible path ...")
@@ -685,7 +820,10 @@ def main():
             "pipelined": pipelined,
             "serial": serial,
             "sharded": None,
-            "xgmi_model": (shard_cost_model(n, nbytes, world, merged_ids) if shard else None),
+            "xgmi_model": (shard_cost_model(n, nbytes, world, merged_ids) if shard else
+                           prefix_cost_model(n, nbytes, world, leg.ps) if prefix else None),
+            "partition": ({"filters_on_rank": leg.n_filters, "replicated_filters": leg.replicated,
+                           "topics_matched_on_rank0": n_walked} if prefix else None),
             "host_e2e": host,
             "cpu_baseline": cpu,
         }
@@ -758,6 +896,8 @@ def sharded_leg(args, f, t, rank, world, dev, mode, fanout, seed, have_pg):
     import torch
     import torch.distributed as dist
     from emqx_amd.engine import GpuMatcher
+    if args.sharded_layout == "prefix" and not fanout:
+        return prefix_leg(args, f, t, rank, world, dev, mode, have_pg)
     meta = torch.tensor([t.n, len(t.blob)] if rank == 0 else [0, 0], dtype=torch.int64, device=dev)
     if have_pg:
         dist.broadcast(meta, 0)
@@ -799,6 +939,53 @@ def sharded_leg(args, f, t, rank, world, dev, mode, fanout, seed, have_pg):
                 dist.all_reduce(dtot)
             out["deliveries_per_step"] = int(dtot.item())
         return out
+    finally:
+        gm2.close()
+
+
+def prefix_leg(args, f, t, rank, world, dev, mode, have_pg):
+    """The prefix-partition layout timed beside the replicate `value` (VERDICT
+    r3 item 5): a second context per rank holds this rank's partition, each
+    rank's own batch is routed to the prefix owners every step.  value = the
+    topics of all ranks' batches per second for the whole node (weak)."""
+    import torch
+    import torch.distributed as dist
+    from emqx_amd.engine import GpuMatcher
+    gm2 = GpuMatcher(dev.index, max_batch=t.n)
+    s = torch.cuda.Stream(dev)
+    try:
+        t0 = time.time()
+        with torch.cuda.stream(s):
+            leg = PrefixLeg(gm2, f, t, rank, world, dev, s.cuda_stream, mode, have_pg)
+            log(f"[rank {rank}] prefix leg: {leg.n_filters} filters on this rank ({leg.replicated} replicated), "
+                f"built in {time.time() - t0:.1f}s")
+            leg.size()
+            for _ in range(args.warmup):
+                leg.step()
+            torch.cuda.synchronize(dev)
+            if have_pg:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                leg.step()
+            torch.cuda.synchronize(dev)
+            el = time.perf_counter() - t0
+            ids = leg.check()
+        if have_pg:
+            dist.barrier()
+            e = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = float(e.item())
+            fr = torch.tensor([leg.n_filters], dtype=torch.int64, device=dev)
+            dist.all_reduce(fr, op=dist.ReduceOp.MAX)
+            max_filters = int(fr.item())
+        else:
+            max_filters = leg.n_filters
+        return {"value": t.n * world * args.steps / el, "unit": "topics/s", "ms_per_step": el / args.steps * 1e3,
+                "scaling": "weak", "layout": LAYOUTS["prefix"], "filters_per_rank_max": max_filters,
+                "replicated_filters": leg.replicated, "filters_total": f.n, "ids_on_rank0": ids,
+                "xgmi_model": prefix_cost_model(t.n, len(t.blob), world, leg.ps)}
     finally:
         gm2.close()
 
@@ -860,7 +1047,7 @@ def order_experiment(args, gm, run_local, bufs, dev, n):
 
 
 def _host_leg(args, world, shard):
-    return args.host_e2e == "on" and world == 1 and not shard
+    return args.host_e2e == "on" and world == 1 and args.mode == "replicate"
 
 
 if __name__ == "__main__":

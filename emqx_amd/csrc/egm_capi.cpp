@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <memory>
@@ -97,15 +98,35 @@ struct PipeSlot {
   int mode = 0;
   uint64_t bytes = 0, maxlen = 0, cap = 0;
   PinBuf h_in, h_out, h_stats;
-  DevBuf d_blob, d_off, d_row, d_ids, d_flags, d_cnt;
-  hipEvent_t ev_in = nullptr, ev_done = nullptr, ev_out = nullptr;
+  DevBuf d_blob, d_off, d_row, d_ids, d_flags;
+  // ev_in: staged input copied in; ev_match: matched (stream s); ev_done: the
+  // CSR written into h_out by the copy-out kernel (d2h stream)
+  hipEvent_t ev_in = nullptr, ev_match = nullptr, ev_done = nullptr;
   uint64_t epoch = 0;
   ~PipeSlot() {
     if (ev_in) hipEventDestroy(ev_in);
+    if (ev_match) hipEventDestroy(ev_match);
     if (ev_done) hipEventDestroy(ev_done);
-    if (ev_out) hipEventDestroy(ev_out);
   }
 };
+
+// Layout of a pipeline result in the slot's pinned buffer (h_out): header,
+// egm_result, then row_ptr, ids (room for `cap`), flags, counts — each 16-B
+// aligned, as the copy-out kernel writes them.
+struct OutLayout {
+  size_t o_res, o_row, o_ids, o_fl, o_cnt, total;
+};
+inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+inline OutLayout out_layout(uint64_t n, uint64_t cap) {
+  OutLayout o;
+  o.o_res = sizeof(ResultHdr);
+  o.o_row = al16(o.o_res + sizeof(egm_result));
+  o.o_ids = al16(o.o_row + (n + 1) * 8);
+  o.o_fl = al16(o.o_ids + cap * 4);
+  o.o_cnt = al16(o.o_fl + n);
+  o.total = o.o_cnt + n * 4 + 16;
+  return o;
+}
 constexpr uint32_t PREFIX_RANKS_MAX = 16;   // ranks of one prefix partition (kernel limit)
 constexpr size_t PIPE_MAX_SLOTS = 8;     // tickets of egm_match_submit busy or held at once
 constexpr size_t PIPE_HARD_SLOTS = 16;   // all slots, egm_match_batch's included (then it waits); each
@@ -741,6 +762,26 @@ static bool use_bulk_build(uint32_t n, const uint32_t* ids) {
   return true;
 }
 
+// fn(lo, hi) over [0, n) on up to 8 threads, `grain` items or more each
+// (the host side of a 1M-topic batch: one core stages ~10 GB/s into pinned
+// memory, the PCIe link takes ~50; round 3 copied a 39 MB batch on one core).
+template <class F>
+static void par_for(size_t n, size_t grain, F fn) {
+  const unsigned nt = (unsigned)std::min<size_t>(8, std::max<size_t>(1, n / std::max<size_t>(grain, 1)));
+  if (nt <= 1) {
+    fn((size_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t per = (n + nt - 1) / nt;
+  for (unsigned k = 1; k < nt; ++k) {
+    const size_t lo = k * per, hi = std::min(n, lo + per);
+    if (lo < hi) th.emplace_back([=] { fn(lo, hi); });
+  }
+  fn((size_t)0, std::min(n, per));
+  for (auto& x : th) x.join();
+}
+
 extern "C" {
 
 const char* egm_version(void) { return "emqx_gpu_match 0.1 (gfx950)"; }
@@ -1010,22 +1051,8 @@ int egm_get_timing(egm_ctx* c, double* walk_ms, uint64_t* walk_n, double* fan_ms
   return EGM_OK;
 }
 
-// Copy n bytes with up to 8 threads (large batches: one host core moves
-// ~10 GB/s, the PCIe link ~50).
 static void par_copy(void* dst, const void* src, size_t bytes) {
-  const size_t chunk = 64u << 20;
-  if (bytes <= chunk) {
-    memcpy(dst, src, bytes);
-    return;
-  }
-  const unsigned nt = (unsigned)std::min<size_t>(8, (bytes + chunk - 1) / chunk);
-  std::vector<std::thread> th;
-  const size_t per = (bytes + nt - 1) / nt;
-  for (unsigned k = 0; k < nt; ++k) {
-    const size_t lo = k * per, hi = std::min(bytes, lo + per);
-    if (lo < hi) th.emplace_back([=] { memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, hi - lo); });
-  }
-  for (auto& x : th) x.join();
+  par_for(bytes, 4u << 20, [=](size_t lo, size_t hi) { memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, hi - lo); });
 }
 
 // Enqueue one staged batch of slot S: H2D on the copy stream, the match on
@@ -1043,8 +1070,9 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   if ((e = S.d_row.ensure((n + 1) * 8)) != hipSuccess) return c->hip_fail(e, "pipe row");
   if ((e = S.d_ids.ensure((S.cap + 1) * 4)) != hipSuccess) return c->hip_fail(e, "pipe ids");
   if ((e = S.d_flags.ensure(n + 8)) != hipSuccess) return c->hip_fail(e, "pipe flags");
-  if ((e = S.d_cnt.ensure(n * 4 + 16)) != hipSuccess) return c->hip_fail(e, "pipe counts");
   if ((e = S.h_stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "pipe stats");
+  const OutLayout ol = out_layout(n, S.cap);
+  if ((e = S.h_out.ensure(ol.total)) != hipSuccess) return c->hip_fail(e, "pipe pinned result");
   if ((e = hipStreamWaitEvent(s, S.ev_in, 0)) != hipSuccess) return c->hip_fail(e, "pipe wait input");
   r = run_match(c, W, *ep, S.d_blob.as<uint8_t>(), S.d_off.as<uint32_t>(), S.n, S.mode, s, S.d_row.as<uint64_t>(),
                 S.d_ids.as<uint32_t>(), S.cap);
@@ -1054,13 +1082,20 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   }
   c->last_pending = false;   // this batch's counters travel with the slot
   if ((n && (e = hipMemcpyAsync(S.d_flags.p, W.tfl.p, n, hipMemcpyDeviceToDevice, s)) != hipSuccess) ||
-      (n && (e = hipMemcpyAsync(S.d_cnt.p, W.cnt.p, n * 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) ||
       (e = hipMemcpyAsync(S.h_stats.p, W.stats.p, sizeof(MatchStats), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipEventRecord(S.ev_done, s)) != hipSuccess) {
+      (e = hipEventRecord(S.ev_match, s)) != hipSuccess) {
     ws_done(W, s);
     return c->hip_fail(e, "pipe epilogue");
   }
   ws_done(W, s);
+  // the CSR straight into pinned memory, sized on the device, on the copy
+  // stream: it runs beside the next batch's match
+  uint8_t* h = (uint8_t*)S.h_out.p;
+  if ((e = hipStreamWaitEvent(c->d2h_stream, S.ev_match, 0)) != hipSuccess ||
+      (e = launch_copy_out(S.d_row.as<uint64_t>(), (uint32_t)n, S.d_ids.as<uint32_t>(), S.cap, S.d_flags.as<uint8_t>(),
+                           h + ol.o_row, h + ol.o_ids, h + ol.o_fl, c->d2h_stream)) != hipSuccess ||
+      (e = hipEventRecord(S.ev_done, c->d2h_stream)) != hipSuccess)
+    return c->hip_fail(e, "pipe copy-out");
   return EGM_OK;
 }
 
@@ -1096,8 +1131,8 @@ static int pipe_new_slot(egm_ctx* c, long* k) {
   c->pipe.emplace_back(new PipeSlot());
   PipeSlot& N = *c->pipe.back();
   if (hipEventCreateWithFlags(&N.ev_in, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&N.ev_done, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&N.ev_out, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&N.ev_match, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&N.ev_done, hipEventDisableTiming) != hipSuccess) {
     c->pipe.pop_back();
     return c->fail(EGM_E_DEVICE, "pipe events");
   }
@@ -1150,13 +1185,22 @@ static int submit_locked(egm_ctx* c, std::unique_lock<std::recursive_mutex>& g, 
   uint8_t* hin = (uint8_t*)S.h_in.p;
   if (bytes) par_copy(hin, blob + base0, bytes);
   uint32_t* hoff = (uint32_t*)(hin + o_off);
-  uint64_t maxlen = 0;
-  for (uint32_t i = 0; i <= n; ++i) hoff[i] = n ? off[i] - base0 : 0;
-  for (uint32_t i = 0; i < n; ++i) maxlen = std::max<uint64_t>(maxlen, hoff[i + 1] - hoff[i]);
+  std::atomic<uint64_t> maxlen{0};
+  hoff[0] = 0;
+  par_for(n, 1u << 18, [&](size_t lo, size_t hi) {   // offsets rebased to 0, and the longest topic
+    uint64_t m = 0;
+    for (size_t i = lo; i < hi; ++i) {
+      hoff[i + 1] = off[i + 1] - base0;
+      m = std::max<uint64_t>(m, (uint64_t)off[i + 1] - off[i]);
+    }
+    uint64_t cur = maxlen.load();
+    while (m > cur && !maxlen.compare_exchange_weak(cur, m)) {
+    }
+  });
   S.n = n;
   S.mode = mode;
   S.bytes = bytes;
-  S.maxlen = maxlen;
+  S.maxlen = maxlen.load();
   S.cap = std::max<uint64_t>(std::max<uint64_t>((uint64_t)n * 4 + 1024, S.cap), c->out_ids.cap / 4);
   if ((e = S.d_blob.ensure(bytes + 16)) != hipSuccess) return c->hip_fail(e, "pipe blob");
   if ((e = S.d_off.ensure(((uint64_t)n + 1) * 4)) != hipSuccess) return c->hip_fail(e, "pipe offsets");
@@ -1232,40 +1276,33 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   }
   c->last = st;   // egm_last_stats reports the waited batch
   const uint64_t n = S.n, nids = st.total_ids;
-  // result: header + struct + counts + row_ptr + ids + flags, in the slot's pinned memory
-  const size_t o_res = sizeof(ResultHdr), o_cnt = (o_res + sizeof(egm_result) + 15) & ~(size_t)15,
-               o_row = (o_cnt + n * 4 + 15) & ~(size_t)15, o_ids = o_row + (n + 1) * 8,
-               o_fl = (o_ids + nids * 4 + 15) & ~(size_t)15, total = o_fl + n + 16;
-  if ((e = S.h_out.ensure(total)) != hipSuccess) return done(c->hip_fail(e, "pipe pinned result"));
+  // the copy-out kernel wrote row_ptr, ids and flags into h_out (ev_done)
+  const OutLayout ol = out_layout(n, S.cap);
   uint8_t* h = (uint8_t*)S.h_out.p;
   ResultHdr* hdr = (ResultHdr*)h;
-  egm_result* res = (egm_result*)(h + o_res);
+  egm_result* res = (egm_result*)(h + ol.o_res);
   memset(res, 0, sizeof(*res));
   res->n_topics = S.n;
   res->n_ids = nids;
-  res->counts = (uint32_t*)(h + o_cnt);
-  res->row_ptr = (uint64_t*)(h + o_row);
-  res->ids = (uint32_t*)(h + o_ids);
-  res->flags = (uint8_t*)(h + o_fl);
+  res->counts = (uint32_t*)(h + ol.o_cnt);
+  res->row_ptr = (uint64_t*)(h + ol.o_row);
+  res->ids = (uint32_t*)(h + ol.o_ids);
+  res->flags = (uint8_t*)(h + ol.o_fl);
   res->epoch = S.epoch;
   res->visited = st.visited;
   res->n_error = st.errors;
-  hipStream_t d = c->d2h_stream;
-  if ((e = hipMemcpyAsync(res->row_ptr, S.d_row.p, (n + 1) * 8, hipMemcpyDeviceToHost, d)) != hipSuccess ||
-      (nids && (e = hipMemcpyAsync(res->ids, S.d_ids.p, nids * 4, hipMemcpyDeviceToHost, d)) != hipSuccess) ||
-      (n && (e = hipMemcpyAsync(res->counts, S.d_cnt.p, n * 4, hipMemcpyDeviceToHost, d)) != hipSuccess) ||
-      (n && (e = hipMemcpyAsync(res->flags, S.d_flags.p, n, hipMemcpyDeviceToHost, d)) != hipSuccess) ||
-      (e = hipEventRecord(S.ev_out, d)) != hipSuccess)
-    return done(c->hip_fail(e, "pipe D2H"));
   g.unlock();
-  e = hipEventSynchronize(S.ev_out);
-  uint32_t heavy = 0;
-  if (e == hipSuccess) {
+  uint32_t heavy = 0;   // host work outside the lock: counts (not copied: row_ptr has them) and heavy topics
+  {
+    const uint64_t* rp = res->row_ptr;
+    uint32_t* cn = res->counts;
     const uint8_t* fl = res->flags;
-    for (uint64_t i = 0; i < n; ++i) heavy += (fl[i] & TF_HEAVY) ? 1u : 0u;
+    for (uint64_t i = 0; i < n; ++i) {
+      cn[i] = (uint32_t)(rp[i + 1] - rp[i]);
+      heavy += (fl[i] & TF_HEAVY) ? 1u : 0u;
+    }
   }
   g.lock();
-  if (e != hipSuccess) return done(c->hip_fail(e, "pipe D2H"));
   if (res->row_ptr[n] != nids) return done(c->fail(EGM_E_DEVICE, "row_ptr total mismatch"));
   res->n_heavy = heavy;
   hdr->magic = RES_PIPE;

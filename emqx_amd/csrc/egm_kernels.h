@@ -163,6 +163,11 @@ hipError_t launch_shard_merge(const uint32_t* cnt, uint32_t G, uint32_t n, const
                               uint64_t* tile_sums, uint32_t* tot, uint64_t* row, uint32_t* out, uint64_t cap,
                               hipStream_t s);
 
+// Host-visible result copy: row_ptr, the row_ptr[n] ids (<= ids_cap) and the
+// flags of a device CSR into pinned host memory (16-B aligned sections).
+hipError_t launch_copy_out(const uint64_t* row, uint32_t n, const uint32_t* ids, uint64_t ids_cap,
+                           const uint8_t* flags, uint8_t* h_row, uint8_t* h_ids, uint8_t* h_fl, hipStream_t s);
+
 // Prefix partition exchange (egm_common.h prefix_vpart): a rank's
 // topic batch -> n_ranks slots of slot_bytes each, one per destination rank,
 // laid out for an equal-split all_to_all:
