@@ -219,7 +219,8 @@ struct egm_ctx {
   DevBuf p_ctr, p_dst;
 
   // fan-out
-  DevBuf sub_row, sub_rp, sub_ids, f_dc, f_ds0, f_dpos, f_tiles, f_ovf, f_mrow, f_mids, f_drow, f_dfid, f_dsub;
+  DevBuf sub_row, sub_rp, sub_ids, f_dc, f_ds0, f_dpos, f_wbase, f_tiles, f_ovf, f_mrow, f_mids, f_drow, f_dfid,
+      f_dsub;
   uint32_t n_fid_slots = 0;
 
   // timing
@@ -1397,11 +1398,13 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   if (e != hipSuccess) return c->hip_fail(e, "match_row readback");
   if (nids >= 0xFFFFFFF0ull) return c->fail(EGM_E_INVAL, "too many matched ids for one fan-out batch");
   if (nids > mids_len) return c->fail(EGM_E_OVERFLOW, "match row total exceeds the id buffer (overflowed match batch)");
-  if ((e = c->f_dc.ensure((nids + 1) * 4)) != hipSuccess) return c->hip_fail(e, "f_dc");
+  const uint64_t nwin = (nids + 63) / 64;
+  if ((e = c->f_dc.ensure((nwin + 1) * 4)) != hipSuccess) return c->hip_fail(e, "f_dc");   // window totals
   if ((e = c->f_ds0.ensure((nids + 1) * 8)) != hipSuccess) return c->hip_fail(e, "f_ds0");
+  if ((e = c->f_wbase.ensure((nwin + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_wbase");
   if (!d_entry_pos && (e = c->f_dpos.ensure((nids + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_dpos");
   uint64_t* dpos = d_entry_pos ? d_entry_pos : c->f_dpos.as<uint64_t>();   // the caller's, in the compact form
-  if ((e = c->f_tiles.ensure((scan_tiles((uint32_t)nids) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_tiles");
+  if ((e = c->f_tiles.ensure((scan_tiles((uint32_t)nwin) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_tiles");
   if ((e = c->f_ovf.ensure(16)) != hipSuccess) return c->hip_fail(e, "f_ovf");
   SubTable st{c->sub_row.as<uint64_t>(), c->sub_ids.as<uint32_t>(), c->n_fid_slots, c->sub_rp.as<uint4>()};
   hipEvent_t evp[2] = {nullptr, nullptr};
@@ -1411,8 +1414,8 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   }
   c->work_begin(s);
   e = launch_fanout(st, d_mrow, d_mids, n, nids, d_drow, d_fid, d_sub, cap, c->f_dc.as<uint32_t>(),
-                    c->f_ds0.as<uint64_t>(), dpos, c->f_tiles.as<uint64_t>(), c->f_ovf.as<unsigned int>(), s,
-                    c->timing ? evp : nullptr);
+                    c->f_ds0.as<uint64_t>(), dpos, c->f_wbase.as<uint64_t>(), c->f_tiles.as<uint64_t>(),
+                    c->f_ovf.as<unsigned int>(), s, c->timing ? evp : nullptr);
   if (c->timing) {
     c->ev_fan.push_back(evp[0]);
     c->ev_fan.push_back(evp[1]);

@@ -125,20 +125,28 @@ EGM_HD uint64_t word_hash(const uint8_t* p, uint32_t len) {
   return word_hash_finish(h, len);
 }
 
-// Both per-pop hashes are 32-bit and cost the walker two multiplies each
-// (round 4: the 64-bit fmix64 forms took ~27 VALU per pop, and the walk is
-// bound partly by its instruction issue).
+// The per-pop hashes.  Round 4 tried 32-bit forms (two multiplies each
+// instead of fmix64's ~27 VALU per pop): EGM_EDGE_HASH32 / EGM_SIG_HASH32,
+// A/B only (profiles/r4_*): the 32-bit edge hash made the C2 walk 4 % slower.
 EGM_HD uint32_t sig_bit(uint32_t wid) {   // literal-child signature bit of a word
+#ifdef EGM_SIG_HASH32
   const uint32_t h = wid * 0x9E3779B1u;   // Fibonacci hashing of the word id
+#else
+  const uint32_t h = (uint32_t)(mix64(0x9E3779B97F4A7C15ull ^ wid) >> 32);
+#endif
   return 1u << (SIG_SHIFT + (uint32_t)(((uint64_t)h * SIG_BITS) >> 32));
 }
 
 EGM_HD uint32_t edge_bucket(uint32_t parent, uint32_t wid, uint32_t mask) {
+#ifdef EGM_EDGE_HASH32
   uint32_t h = (parent * 0x9E3779B1u) ^ wid;   // for a fixed parent, a bijection of the word
   h ^= h >> 16;
   h *= 0x85EBCA6Bu;
   h ^= h >> 13;
   return h & mask;
+#else
+  return (uint32_t)(mix64(((uint64_t)parent << 32) | wid) & mask);
+#endif
 }
 
 // Multi-GPU prefix partition (SURVEY §8e "partition by root word", two words

@@ -145,10 +145,13 @@ struct SubTable {
   const uint4* rp;                // [n_fid_slots] {row start lo, hi, count, 0} (launch_sub_pairs)
 };
 hipError_t launch_sub_pairs(const uint64_t* row, uint32_t n_slots, uint4* rp, hipStream_t s);
+// Scratch: wsum u32[nids/64 + 1] (window totals), dsrc u64[nids] (packed row
+// start | count), wbase u64[nids/64 + 2] (scanned window totals), dpos
+// u64[nids + 1] (each entry's first delivery: the compact form's output).
 hipError_t launch_fanout(const SubTable& st, const uint64_t* match_row, const uint32_t* match_ids,
                          uint32_t n, uint64_t nids, uint64_t* deliv_row, uint32_t* deliv_fid,
-                         uint32_t* deliv_sub, uint64_t deliv_cap, uint32_t* dcount, uint64_t* dsrc,
-                         uint64_t* dpos, uint64_t* tile_sums, unsigned int* overflow, hipStream_t s,
+                         uint32_t* deliv_sub, uint64_t deliv_cap, uint32_t* wsum, uint64_t* dsrc,
+                         uint64_t* dpos, uint64_t* wbase, uint64_t* tile_sums, unsigned int* overflow, hipStream_t s,
                          hipEvent_t* ev);
 
 // Filter-shard merge: G shard CSRs of one topic batch ->

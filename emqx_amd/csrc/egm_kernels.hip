@@ -503,11 +503,17 @@ static_assert(WALK_STAGE <= 0xFFFF, "flush slots and spill starts are packed as 
 static_assert(light_dmax(WALK_STACK) >= DEEP_MIN, "the first pass must take the chunks it does not hand on");
 static_assert(light_dmax(WALK_STACK_DEEP) >= 16, "stack too small");
 
+#ifndef EGM_FLUSH_V2
+#define EGM_FLUSH_V2 1   // round 4 flush (below); 0: round 3's multi-split flush (A/B)
+#endif
+
 template <uint32_t STK>
 struct alignas(16) WaveLds {
   uint4 stack[STK];
   uint32_t stage_fid[WALK_STAGE];
+#if !EGM_FLUSH_V2
   uint16_t stage_rank[WALK_STAGE];
+#endif
   uint8_t stage_t[WALK_STAGE];       // topic in chunk of the emit
   uint32_t words[WALK_WORDS + 1];    // the sub-chunk's word ids, [topic][level] (+1: a leaf's
                                      // unclamped next-word read, never used)
@@ -552,6 +558,77 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
   return r;
 }
 
+#if EGM_FLUSH_V2
+// Write the stage out (round 4).  One pass over the staged entries in arrival
+// order: an LDS atomic on the topic's flush counter ranks each entry inside
+// its topic, and the entry is stored at once into the topic's fixed block
+// (ids_fix, walk position x fix_cap) at cnt + rank — its place inside the
+// block is free (a row is a set).  Two dependent LDS round trips per 64
+// entries.  Entries past a topic's fixed block (1.5 % of C2's ids) are
+// compacted to the front of the stage and, only when there are any, written
+// to the wave's ids slab as one piece per topic {topic, count, ids_tmp offset,
+// offset inside the topic's CSR row}, so neither compaction needs atomics.
+// Round 3's flush ranked entries with a 6-ballot multi-split, scanned three
+// times and stored in topic order after inverting slot -> entry: ~600
+// instructions and ~15 dependent LDS round trips per flush, once every ~4.7
+// walk iterations at C2.
+template <class LDS>
+__device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t t0, uint32_t my_t, uint32_t lane,
+                                            const MatchWork& w, Slab& sid, Slab& spc) {
+  const uint32_t cap = w.fix_cap;
+  uint32_t nsp = 0;   // wave-uniform: entries past their topic's fixed block
+#pragma unroll 1
+  for (uint32_t q0 = 0; q0 < nstage; q0 += 64) {
+    const uint32_t q = q0 + lane;
+    const bool act = q < nstage;
+    const uint32_t qc = act ? q : 0u;
+    const uint32_t tt = L.stage_t[qc], fid = L.stage_fid[qc];
+    uint32_t k = 0;
+    if (act) k = atomicAdd(&L.fcnt[tt], 1u) + L.cnt[tt];
+    const bool fix = act && k < cap;
+#ifndef EGM_AB_NO_ID_STORES   // measurement only (tools/build_variant.py): the walk without its id stores
+    if (fix) w.ids_fix[(uint64_t)(t0 + tt) * cap + k] = fid;
+#endif
+    const uint64_t sb = __ballot(act && !fix);
+    if (sb) {   // rare; every lane has read its entry (the writes land at or below the reading lane's slot)
+      wave_sync();
+      if (act && !fix) {
+        const uint32_t p = nsp + mbcnt(sb);
+        L.stage_fid[p] = fid;
+        L.stage_t[p] = (uint8_t)tt;
+      }
+      nsp += popc(sb);
+    }
+  }
+  wave_sync();
+  const uint32_t fl = L.fcnt[lane];   // the chunk's topic `lane`: ids in this flush
+  if (nsp) {
+    const uint32_t c0 = L.cnt[lane];
+    const uint32_t nfix = c0 >= cap ? 0u : min(fl, cap - c0);
+    const uint32_t over = fl - nfix;    // ids past the fixed block: spilled
+    uint32_t tot, ptot;
+    const uint32_t ex = wave_excl_scan(over, lane, &tot);
+    const uint32_t pex = wave_excl_scan(over ? 1u : 0u, lane, &ptot);
+    const unsigned long long base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
+    const unsigned long long pbase = slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
+    const bool ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
+    if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
+    if (over && ok) w.pieces[pbase + pex] = make_uint4(my_t, over, (uint32_t)(base + ex), c0 + nfix);
+    L.fcnt[lane] = ex;   // the topic's spill cursor inside this flush's run
+    wave_sync();
+#pragma unroll 1
+    for (uint32_t q = lane; q < nsp; q += 64) {
+      const uint32_t tt = L.stage_t[q], fid = L.stage_fid[q];
+      const uint32_t pos = atomicAdd(&L.fcnt[tt], 1u);
+      if (ok) w.ids_tmp[base + pos] = fid;
+    }
+    wave_sync();
+  }
+  L.cnt[lane] += fl;
+  L.fcnt[lane] = 0;
+  wave_sync();
+}
+#else
 // Write the stage out.  Entries are ranked within their topic by a
 // conflict-free multi-split (lanes holding the same topic find each other
 // with 6 ballots; one LDS add per topic per 64 entries).  A topic's first
@@ -634,6 +711,8 @@ __device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t t0
   L.fcnt[lane] = 0;
   wave_sync();
 }
+
+#endif  // EGM_FLUSH_V2
 
 // Slot search from slot k0 of bucket b on (rare: both first slots hold other keys).
 __device__ __forceinline__ bool edge_probe_from(const DevTable& tab, uint32_t b, int k0, uint32_t node, uint32_t w,
@@ -1387,7 +1466,7 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
 // (A chunk-major variant — rank-major blocks staged through LDS and rows
 // written scattered — measured 6x slower: DESIGN.md §4.1.)
 #ifndef EGM_COMPACT_FIX_QUARTER
-#define EGM_COMPACT_FIX_QUARTER 1
+#define EGM_COMPACT_FIX_QUARTER 0   // A/B (r4a): 1.19 ms against 0.97 — not kept
 #endif
 __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact_fix(const uint32_t* __restrict__ cnt,
                                                                     const uint32_t* __restrict__ inv,
@@ -1607,26 +1686,40 @@ __global__ __launch_bounds__(256) void k_sub_pairs(const uint64_t* __restrict__ 
   }
 }
 
+// Round 4: the count kernel writes one packed record per
+// match entry {subscriber row start:40 | count:24} and one subscriber total per
+// window of 64 entries; the window totals are scanned (nids/64 of them), and
+// the fill derives each entry's delivery offset with a wave scan inside its
+// window.  Round 3 wrote a count AND a start per entry and scanned all nids
+// counts into u64 offsets before the fill read them back (~8.8 GB of
+// intermediate traffic at C4, ~4.3 ms of scans).
+constexpr uint32_t FAN_CNT_BITS = 24;
+constexpr uint32_t FAN_CNT_SAT = (1u << FAN_CNT_BITS) - 1;   // saturated: the fill re-reads the row record
 __global__ __launch_bounds__(256) void k_fan_count(const uint32_t* __restrict__ mids, uint64_t nids,
-                                                   SubTable st, uint32_t* __restrict__ dc,
+                                                   SubTable st, uint32_t* __restrict__ wsum,
                                                    uint64_t* __restrict__ ds0) {
-  constexpr uint32_t U = 4;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nids; i0 += stride * U) {
+  constexpr uint32_t U = 4;   // windows per wave in flight
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nwin = (nids + 63) / 64;
+  const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t w0 = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w0 < nwin; w0 += wstride * U) {
     uint32_t f[U];
     uint4 r[U];
 #pragma unroll
-    for (uint32_t u = 0; u < U; ++u) f[u] = mids[min(i0 + u * stride, nids - 1)];
+    for (uint32_t u = 0; u < U; ++u) f[u] = mids[min((w0 + u * wstride) * 64 + lane, nids - 1)];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) r[u] = st.rp[f[u] < st.n_fid_slots ? f[u] : 0u];   // unconditional
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
-      const uint64_t i = i0 + u * stride;
-      if (i < nids) {
-        const bool ok = f[u] < st.n_fid_slots;
-        dc[i] = ok ? r[u].z : 0u;
-        ds0[i] = ok ? ((uint64_t)r[u].y << 32 | r[u].x) : 0ull;   // the fill reads this coalesced
-      }
+      const uint64_t w = w0 + u * wstride, i = w * 64 + lane;
+      const bool ok = i < nids && f[u] < st.n_fid_slots;
+      const uint32_t c = ok ? r[u].z : 0u;
+      if (i < nids)
+        ds0[i] = ok ? (((uint64_t)r[u].y << 32 | r[u].x) << FAN_CNT_BITS) | min(c, FAN_CNT_SAT) : 0ull;
+      uint32_t sum = c;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+      if (lane == 0 && w < nwin) wsum[w] = sum;
     }
   }
 }
@@ -1644,32 +1737,44 @@ __global__ __launch_bounds__(256) void k_fan_rows(const uint64_t* __restrict__ m
 
 constexpr int FAN_WAVES = 4;
 constexpr uint32_t FAN_BIG = 128;   // entries with this many subscribers are copied by the whole wave
+// One wave per window of 64 match entries, whose deliveries are contiguous:
+// the entry offsets (dpos, the compact form's output and the rows' source)
+// come from the window's scanned total plus a wave scan of the entries'
+// counts; then small rows are written lane per delivery (owner found by a
+// 6-step LDS search) and big rows streamed by the whole wave.  An overflowed
+// batch (total > cap) still gets its offsets, so the caller learns the size.
 __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __restrict__ mids, uint64_t nids,
-                                                             SubTable st, const uint32_t* __restrict__ dc,
+                                                             SubTable st, const uint64_t* __restrict__ wbase,
                                                              const uint64_t* __restrict__ ds0,
-                                                             const uint64_t* __restrict__ dpos,
+                                                             uint64_t* __restrict__ dpos,
                                                              uint32_t* __restrict__ dfid, uint32_t* __restrict__ dsub,
                                                              uint64_t cap, unsigned int* overflow) {
-  if (dpos[nids] > cap) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *overflow = 1u;
-    return;
-  }
+  const uint64_t nwin = (nids + 63) / 64;
+  const bool ovf = wbase[nwin] > cap;
+  if (ovf && blockIdx.x == 0 && threadIdx.x == 0) *overflow = 1u;
   __shared__ uint32_t s_pre[FAN_WAVES][64], s_off[FAN_WAVES][64], s_fid[FAN_WAVES][64], s_cnt[FAN_WAVES][64];
   __shared__ uint64_t s_src[FAN_WAVES][64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t nwin = (nids + 63) / 64;
   for (uint64_t w = (uint64_t)blockIdx.x * FAN_WAVES + wave; w < nwin; w += (uint64_t)gridDim.x * FAN_WAVES) {
     const uint64_t w0 = w * 64, i = w0 + lane, ic = min(i, nids - 1);
-    const uint64_t base = dpos[w0];
-    const uint32_t c = i < nids ? dc[ic] : 0u;
+    const uint64_t base = wbase[w];
+    const uint64_t v = ds0[ic];
+    const uint32_t f = mids[ic];
+    uint32_t c = i < nids ? (uint32_t)(v & FAN_CNT_SAT) : 0u;
+    if (c == FAN_CNT_SAT) c = st.rp[f].z;   // a row of 2^24 or more subscribers (rare): its exact count
+    uint32_t tot;
+    const uint32_t off = wave_excl_scan(c, lane, &tot);
+    if (i < nids) dpos[i] = base + off;
+    if (i == nids - 1) dpos[nids] = base + off + c;
+    if (ovf) continue;
     const bool big = c >= FAN_BIG;
     uint32_t tot_s;
     const uint32_t pre_s = wave_excl_scan(big ? 0u : c, lane, &tot_s);   // small entries, packed
     s_pre[wave][lane] = pre_s;
-    s_off[wave][lane] = (uint32_t)(dpos[min(i, nids)] - base);            // real offset in the window
-    s_fid[wave][lane] = mids[ic];
+    s_off[wave][lane] = off;
+    s_fid[wave][lane] = f;
     s_cnt[wave][lane] = c;
-    s_src[wave][lane] = ds0[ic];
+    s_src[wave][lane] = v >> FAN_CNT_BITS;
     wave_sync();
     // small entries: lane per delivery, the owning entry found by a 6-step search
     for (uint32_t q = lane; q < tot_s; q += 64) {
@@ -1687,17 +1792,17 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
     // big entries (C4: 2 000-subscriber filters): the wave streams the row, 4 per lane in flight
     for (uint64_t mb = __ballot(big); mb; mb &= mb - 1) {
       const uint32_t k = (uint32_t)__builtin_ctzll(mb);
-      const uint32_t cnt = s_cnt[wave][k], f = s_fid[wave][k];
+      const uint32_t cnt = s_cnt[wave][k], fk = s_fid[wave][k];
       const uint64_t src = s_src[wave][k], dst = base + s_off[wave][k];
       for (uint32_t j0 = lane; j0 < cnt; j0 += 256) {
-        uint32_t v[4];
+        uint32_t vv[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = st.subs[src + min(j0 + 64u * r, cnt - 1)];
+        for (int r = 0; r < 4; ++r) vv[r] = st.subs[src + min(j0 + 64u * r, cnt - 1)];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (j0 + 64u * r < cnt) {
-            if (dfid) dfid[dst + j0 + 64u * r] = f;
-            dsub[dst + j0 + 64u * r] = v[r];
+            if (dfid) dfid[dst + j0 + 64u * r] = fk;
+            dsub[dst + j0 + 64u * r] = vv[r];
           }
       }
     }
@@ -1707,20 +1812,26 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
 
 hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_t* mids, uint32_t n,
                          uint64_t nids, uint64_t* drow, uint32_t* dfid, uint32_t* dsub, uint64_t cap,
-                         uint32_t* dc, uint64_t* ds0, uint64_t* dpos, uint64_t* tile_sums,
+                         uint32_t* wsum, uint64_t* ds0, uint64_t* dpos, uint64_t* wbase, uint64_t* tile_sums,
                          unsigned int* overflow, hipStream_t s, hipEvent_t* ev) {
   hipError_t e = hipMemsetAsync(overflow, 0, 4, s);
   if (e != hipSuccess) return e;
   if (ev) hipEventRecord(ev[0], s);
-  const uint32_t g = (uint32_t)std::min<uint64_t>((nids + 255) / 256 + 1, 8192);
-  if (nids) hipLaunchKernelGGL(k_fan_count, dim3(g), dim3(256), 0, s, mids, nids, st, dc, ds0);
-  scan_counts(dc, (uint32_t)nids, tile_sums, dpos, s);
-  hipLaunchKernelGGL(k_fan_rows, dim3(std::min<uint32_t>(n / 256 + 1, 8192)), dim3(256), 0, s, mrow, n, dpos, drow);
+  const uint64_t nwin = (nids + 63) / 64;
   if (nids) {
-    const uint32_t gf = (uint32_t)std::min<uint64_t>((nids + 64 * FAN_WAVES - 1) / (64 * FAN_WAVES), 16384);
-    hipLaunchKernelGGL(k_fan_fill, dim3(gf), dim3(64 * FAN_WAVES), 0, s, mids, nids, st, dc, ds0, dpos, dfid, dsub,
-                       cap, overflow);
+    const uint32_t g = (uint32_t)std::min<uint64_t>((nwin + 3) / 4 + 1, 8192);
+    hipLaunchKernelGGL(k_fan_count, dim3(g), dim3(256), 0, s, mids, nids, st, wsum, ds0);
   }
+  scan_counts(wsum, (uint32_t)nwin, tile_sums, wbase, s);   // window totals -> window bases, wbase[nwin] = all
+  if (nids) {
+    const uint32_t gf = (uint32_t)std::min<uint64_t>((nwin + FAN_WAVES - 1) / FAN_WAVES, 16384);
+    hipLaunchKernelGGL(k_fan_fill, dim3(gf), dim3(64 * FAN_WAVES), 0, s, mids, nids, st, wbase, ds0, dpos, dfid, dsub,
+                       cap, overflow);
+  } else {
+    e = hipMemsetAsync(dpos, 0, 8, s);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_fan_rows, dim3(std::min<uint32_t>(n / 256 + 1, 8192)), dim3(256), 0, s, mrow, n, dpos, drow);
   if (ev) hipEventRecord(ev[1], s);
   return hipGetLastError();
 }

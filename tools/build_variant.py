@@ -2,6 +2,10 @@
 
     python tools/build_variant.py TAG -DEGM_WALK_STACK=320 ...
       -> emqx_amd/libemqx_gpu_match_TAG.so   (select it with EGM_LIB=<path>)
+
+Every source — the kernels AND the host table builder — is compiled with the
+flags, so a flag that changes a layout or hash shared by both (egm_common.h)
+stays consistent inside the variant.
 """
 import os
 import subprocess
@@ -13,10 +17,15 @@ from emqx_amd import build as B  # noqa: E402
 
 tag, flags = sys.argv[1], sys.argv[2:]
 out = os.path.join(B.HERE, f"libemqx_gpu_match_{tag}.so")
-obj = f"/tmp/egm_kernels_{tag}.o"
-B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-fPIC", "-std=c++17", *flags, "-c",
-        os.path.join(B.CSRC, "egm_kernels.hip"), "-o", obj], True)
-B.build_lib()
-objs = [obj] + [os.path.join(B.BUILD, n) for n in ("egm_table.o", "egm_bulk.o", "egm_capi.o", "egm_retain.o")]
+bdir = f"/tmp/egm_var_{tag}"
+os.makedirs(bdir, exist_ok=True)
+objs = [os.path.join(bdir, "egm_kernels.o")]
+B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
+        "-Wno-unused-value", *flags, "-c", os.path.join(B.CSRC, "egm_kernels.hip"), "-o", objs[0]], True)
+for name in ("egm_table.cpp", "egm_bulk.cpp", "egm_capi.cpp", "egm_retain.cpp"):
+    o = os.path.join(bdir, name.replace(".cpp", ".o"))
+    B._run(["g++", "-O3", "-fPIC", "-std=c++17", "-pthread", "-D__HIP_PLATFORM_AMD__", f"-I{B.ROCM}/include", *flags,
+            "-c", os.path.join(B.CSRC, name), "-o", o], True)
+    objs.append(o)
 B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-pthread", "-o", out] + objs, True)
 print(out)
