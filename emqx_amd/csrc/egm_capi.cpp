@@ -536,6 +536,7 @@ static int commit_locked(egm_ctx* c, uint64_t* epoch) {
   ep->view.dict_mask = t.dict_mask();
   ep->view.dict_blob = S.dict_blob.as<uint8_t>();
   ep->view.dict_off = S.dict_off.as<uint64_t>();
+  ep->view.sig_packed = t.n_words() <= (1u << 27) ? 1u : 0u;
   ep->n_filters = t.n_filters();
   ep->n_nodes = t.n_nodes_live();
   ep->n_edges = t.n_edges();
@@ -1293,16 +1294,23 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   res->visited = st.visited;
   res->n_error = st.errors;
   g.unlock();
-  uint32_t heavy = 0;   // host work outside the lock: counts (not copied: row_ptr has them) and heavy topics
+  // host work outside the lock, on up to 8 threads: counts (not copied over
+  // PCIe: row_ptr has them) and the heavy-topic total
+  std::atomic<uint32_t> heavy_n{0};
   {
     const uint64_t* rp = res->row_ptr;
     uint32_t* cn = res->counts;
     const uint8_t* fl = res->flags;
-    for (uint64_t i = 0; i < n; ++i) {
-      cn[i] = (uint32_t)(rp[i + 1] - rp[i]);
-      heavy += (fl[i] & TF_HEAVY) ? 1u : 0u;
-    }
+    par_for(n, 1u << 17, [&](size_t lo, size_t hi) {
+      uint32_t h = 0;
+      for (size_t i = lo; i < hi; ++i) {
+        cn[i] = (uint32_t)(rp[i + 1] - rp[i]);
+        h += (fl[i] & TF_HEAVY) ? 1u : 0u;
+      }
+      heavy_n += h;
+    });
   }
+  const uint32_t heavy = heavy_n.load();
   g.lock();
   if (res->row_ptr[n] != nids) return done(c->fail(EGM_E_DEVICE, "row_ptr total mismatch"));
   res->n_heavy = heavy;

@@ -128,13 +128,17 @@ EGM_HD uint64_t word_hash(const uint8_t* p, uint32_t len) {
 // The per-pop hashes.  Round 4 tried 32-bit forms (two multiplies each
 // instead of fmix64's ~27 VALU per pop): EGM_EDGE_HASH32 / EGM_SIG_HASH32,
 // A/B only (profiles/r4_*): the 32-bit edge hash made the C2 walk 4 % slower.
-EGM_HD uint32_t sig_bit(uint32_t wid) {   // literal-child signature bit of a word
+EGM_HD uint32_t sig_index(uint32_t wid) {   // 0 .. SIG_BITS-1
 #ifdef EGM_SIG_HASH32
   const uint32_t h = wid * 0x9E3779B1u;   // Fibonacci hashing of the word id
 #else
   const uint32_t h = (uint32_t)(mix64(0x9E3779B97F4A7C15ull ^ wid) >> 32);
 #endif
-  return 1u << (SIG_SHIFT + (uint32_t)(((uint64_t)h * SIG_BITS) >> 32));
+  return (uint32_t)(((uint64_t)h * SIG_BITS) >> 32);
+}
+
+EGM_HD uint32_t sig_bit(uint32_t wid) {   // literal-child signature bit of a word
+  return 1u << (SIG_SHIFT + sig_index(wid));
 }
 
 EGM_HD uint32_t edge_bucket(uint32_t parent, uint32_t wid, uint32_t mask) {

@@ -17,6 +17,7 @@ struct DevTable {                 // one epoch of the filter graph in HBM
   uint32_t dict_mask;
   const uint8_t* dict_blob;
   const uint64_t* dict_off;
+  uint32_t sig_packed;            // word ids < 2^27: the walk stages words as id | sig_index << 27
 };
 
 struct MatchStats {               // device-side counters, zeroed per batch

@@ -482,6 +482,9 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #ifndef EGM_WALK_STAGE
 #define EGM_WALK_STAGE 320   // staged emits per flush (7 B each; >= 4 emits x 64 lanes)
 #endif
+#ifndef EGM_WALK_PAIRS
+#define EGM_WALK_PAIRS 0     // A/B: the first pass pops two items per lane per iteration
+#endif
 #ifndef EGM_WALK_WORDS
 #define EGM_WALK_WORDS 448   // staged topic word ids per wave (a chunk's topics, [topic][level])
 #endif
@@ -734,10 +737,29 @@ __device__ __forceinline__ bool edge_probe_from(const DevTable& tab, uint32_t b,
   }
 }
 
+// Staged word ids (round 4): while the dictionary's ids fit 27 bits, the walk
+// stages a topic's words in LDS as id | sig_index(id) << 27, so a pop gets
+// the next word's literal-child signature bit with two VALU instead of
+// re-hashing the word (fmix64: ~13 VALU, five of them quarter-rate
+// multiplies, on every pop).  The reserved ids (WID_NONE/PLUS/HASH, >=
+// WID_MAX) keep their top bits (31), which no packed id has (< 28).
+#ifndef EGM_WORD_SIG
+#define EGM_WORD_SIG 1
+#endif
+constexpr uint32_t WP_SHIFT = 27;
+__device__ __forceinline__ uint32_t word_pack(uint32_t w) {
+  return w >= WID_MAX ? w : (w | (sig_index(w) << WP_SHIFT));
+}
+__device__ __forceinline__ uint32_t word_plain(uint32_t p) { return (p >> WP_SHIFT) == 31u ? p : (p & ((1u << WP_SHIFT) - 1u)); }
+__device__ __forceinline__ uint32_t word_sig(uint32_t p) {
+  const uint32_t k = p >> WP_SHIFT;
+  return k < SIG_BITS ? (1u << (SIG_SHIFT + k)) : 0u;
+}
+
 // One popped item between issuing its reads and consuming them.
 struct Pend {
   uint4 it;                 // the item
-  uint32_t D, nw;           // its topic's depth, the word at level + 1
+  uint32_t D, nw, nsig;     // its topic's depth, the word at level + 1 and its signature bit
   bool act, lit, plus, d1;  // d1: a one-word '$' topic (do_match/1's lookup_topic probe)
   uint4 prec, l0, h0, l1, h1;
 };
@@ -764,7 +786,20 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* words
   // the next level's word (used only if level + 1 < D).  From the LDS stage
   // it is read unclamped, so the read does not wait for the topic's depth
   // (a leaf reads the next topic's word 0, or the pad word past the stage).
-  p.nw = words ? words[(meta & LEVEL_MAX) + 1] : wid[p.act ? gbase + min((meta & LEVEL_MAX) + 1, p.D - 1) : 0u];
+  if (words) {
+    const uint32_t raw = words[(meta & LEVEL_MAX) + 1];
+#if EGM_WORD_SIG
+    if (tab.sig_packed) {
+      p.nw = word_plain(raw);
+      p.nsig = word_sig(raw);
+      return;
+    }
+#endif
+    p.nw = raw;
+  } else {
+    p.nw = wid[p.act ? gbase + min((meta & LEVEL_MAX) + 1, p.D - 1) : 0u];
+  }
+  p.nsig = p.nw < WID_MAX ? sig_bit(p.nw) : 0u;
 }
 
 // Children and emits of one popped item.
@@ -789,7 +824,7 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend
   const uint32_t base_meta = (level + 1) | (meta & (0x7Fu << MT_SHIFT));
   // the literal probe of a child is only worth a read if its signature has
   // the next word's bit (egm_common.h)
-  const uint32_t nsig = nw < WID_MAX ? sig_bit(nw) : 0u;
+  const uint32_t nsig = p.nsig;
   // literal child: pick the matching slot's fields with masks, not a select
   // of the two loaded slots (LLVM folds that into a phi of addresses into the
   // per-item array and keeps the array in scratch)
@@ -856,9 +891,8 @@ __device__ bool exact_walk(const DevTable& tab, const uint32_t* __restrict__ wor
 }
 
 // The root state of a topic: its '#' emit (never for a '$' topic) and the
-// transitions it has to take.
-__device__ __forceinline__ uint32_t root_flags(uint4 root, bool dollar, uint32_t w0) {
-  const uint32_t s0 = w0 < WID_MAX ? sig_bit(w0) : 0u;
+// transitions it has to take (s0: the signature bit of its first word).
+__device__ __forceinline__ uint32_t root_flags(uint4 root, bool dollar, uint32_t s0) {
   return (dollar ? 0u : (root.w & F_PLUS)) | ((root.w & s0) ? (root.w & F_LIT) : 0u);
 }
 
@@ -971,15 +1005,16 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
         const uint32_t j = sub + lane, Dj = L.tinfo[j] & 0xFFFFFFu;
         const uint32_t* src = topic_words(w, L.tinfo[j], gsub);
         uint32_t* dst = L.words + lane * dmax;
+        const bool pk = EGM_WORD_SIG && tab.sig_packed;
         uint32_t i = 0;
         for (; i + 4 <= Dj; i += 4) {
           const uint32_t a0 = src[i], a1 = src[i + 1], a2 = src[i + 2], a3 = src[i + 3];
-          dst[i] = a0;
-          dst[i + 1] = a1;
-          dst[i + 2] = a2;
-          dst[i + 3] = a3;
+          dst[i] = pk ? word_pack(a0) : a0;
+          dst[i + 1] = pk ? word_pack(a1) : a1;
+          dst[i + 2] = pk ? word_pack(a2) : a2;
+          dst[i + 3] = pk ? word_pack(a3) : a3;
         }
-        for (; i < Dj; ++i) dst[i] = src[i];
+        for (; i < Dj; ++i) dst[i] = pk ? word_pack(src[i]) : src[i];
       }
       wave_sync();
       uint32_t next = sub, sp = 0;
@@ -1012,8 +1047,10 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
               em = (root.w & F_HASH) && !dollar;   // filter '#': never for a '$' topic
               fid = root.y;
               created += 1;
-              const uint32_t w0 = L.words[(j & (S - 1)) * dmax];
-              const uint32_t rf = root_flags(root, dollar, w0);
+              const uint32_t w0r = L.words[(j & (S - 1)) * dmax];
+              const bool pk = EGM_WORD_SIG && tab.sig_packed;
+              const uint32_t w0 = pk ? word_plain(w0r) : w0r;
+              const uint32_t rf = root_flags(root, dollar, pk ? word_sig(w0r) : (w0 < WID_MAX ? sig_bit(w0) : 0u));
               has = rf != 0;
               it = make_uint4(0, (j << MT_SHIFT) | (rf << MF_SHIFT), root.x, w0);
             }
@@ -1044,64 +1081,90 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
         // narrows the wave instead.
         const uint32_t room = STK - sp;
         const uint32_t lim = room > dmax ? room - dmax : 1u;
-        const uint32_t want = min(64u, sp), take = min(want, lim), bi = sp - take;
+        // EGM_WALK_PAIRS (A/B): the first pass pops up to 128 items per
+        // iteration, two per lane — twice the reads in flight per wave and
+        // the iteration's fixed work shared by two items (same pop bound)
+        constexpr bool PAIRS = EGM_WALK_PAIRS && !DEEP;
+        const uint32_t want = min(PAIRS ? 128u : 64u, sp), take = min(want, lim), bi = sp - take;
+        const uint32_t take_a = min(take, 64u), take_b = take - take_a;
         bounded += take < want ? 1u : 0u;
         iters += 1;
         popped += take;
-        Pend p;
-        p.act = lane < take;
+        Pend p, pb;
+        p.act = lane < take_a;
         p.it = L.stack[min(bi + lane, STK - 1)];   // unconditional: see issue()
+        if (PAIRS) {
+          pb.act = lane < take_b;
+          pb.it = L.stack[min(bi + 64 + lane, STK - 1)];
+        }
         sp = bi;
         const uint32_t tt = (p.it.y >> MT_SHIFT) & 0x7Fu;
         const uint32_t ti = L.tinfo[tt];
         p.D = ti & 0xFFFFFFu;
         p.d1 = p.D == 1 && ((ti >> 24) & TF_DOLLAR);   // TF_DOLLAR < 0x80: the fixed-stride bit is not read
         issue(tab, L.words + (tt & (S - 1)) * dmax, nullptr, 0, p);
+        uint32_t ttb = 0;
+        if (PAIRS) {
+          ttb = (pb.it.y >> MT_SHIFT) & 0x7Fu;
+          const uint32_t tib = L.tinfo[ttb];
+          pb.D = tib & 0xFFFFFFu;
+          pb.d1 = pb.D == 1 && ((tib >> 24) & TF_DOLLAR);
+          issue(tab, L.words + (ttb & (S - 1)) * dmax, nullptr, 0, pb);
+          lit_probes += popc(__ballot(pb.lit));
+          plus_reads += popc(__ballot(pb.plus));
+        }
         lit_probes += popc(__ballot(p.lit));
         plus_reads += popc(__ballot(p.plus));
         wave_sync();
         // ---- consume: children -> stack, emits -> stage ----
-        Out o;
-        finish(tab, mode, p, o);
-        created += o.created;
-        const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
-        const uint32_t m0 = popc(c0b), nc = m0 + popc(c1b);
-        if (sp + nc > STK) {   // guard only: the pop bound keeps sp + pushes <= STK
-          if (lane == 0) atomicOr(&w.stats->guard, GUARD_STACK);
-          break;
+        auto consume = [&](const Pend& q, uint32_t qt) -> bool {
+          Out o;
+          finish(tab, mode, q, o);
+          created += o.created;
+          const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
+          const uint32_t m0 = popc(c0b), nc = m0 + popc(c1b);
+          if (sp + nc > STK) {   // guard only: the pop bound keeps sp + pushes <= STK
+            if (lane == 0) atomicOr(&w.stats->guard, GUARD_STACK);
+            return false;
+          }
+          if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
+          if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;
+          sp += nc;
+          const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
+          const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
+          if (nstage + ne > WALK_STAGE) {
+            wave_sync();
+            flush_stage(L, nstage, t0, my_t, lane, w, sid, spc);
+            nstage = 0;
+          }
+          const uint8_t st = (uint8_t)qt;
+          if (o.e0) {
+            const uint32_t x = nstage + mbcnt(b0);
+            L.stage_fid[x] = o.f0;
+            L.stage_t[x] = st;
+          }
+          if (o.e1) {
+            const uint32_t x = nstage + n0 + mbcnt(b1);
+            L.stage_fid[x] = o.f1;
+            L.stage_t[x] = st;
+          }
+          if (o.e2) {
+            const uint32_t x = nstage + n1 + mbcnt(b2);
+            L.stage_fid[x] = o.f2;
+            L.stage_t[x] = st;
+          }
+          if (o.e3) {
+            const uint32_t x = nstage + n2 + mbcnt(b3);
+            L.stage_fid[x] = o.f3;
+            L.stage_t[x] = st;
+          }
+          nstage += ne;
+          return true;
+        };
+        if (!consume(p, tt)) break;
+        if (PAIRS && take_b) {
+          if (!consume(pb, ttb)) break;
         }
-        if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
-        if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;
-        sp += nc;
-        const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
-        const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
-        if (nstage + ne > WALK_STAGE) {
-          wave_sync();
-          flush_stage(L, nstage, t0, my_t, lane, w, sid, spc);
-          nstage = 0;
-        }
-        const uint8_t st = (uint8_t)tt;
-        if (o.e0) {
-          const uint32_t q = nstage + mbcnt(b0);
-          L.stage_fid[q] = o.f0;
-          L.stage_t[q] = st;
-        }
-        if (o.e1) {
-          const uint32_t q = nstage + n0 + mbcnt(b1);
-          L.stage_fid[q] = o.f1;
-          L.stage_t[q] = st;
-        }
-        if (o.e2) {
-          const uint32_t q = nstage + n1 + mbcnt(b2);
-          L.stage_fid[q] = o.f2;
-          L.stage_t[q] = st;
-        }
-        if (o.e3) {
-          const uint32_t q = nstage + n2 + mbcnt(b3);
-          L.stage_fid[q] = o.f3;
-          L.stage_t[q] = st;
-        }
-        nstage += ne;
         wave_sync();
       }
     }
@@ -1205,7 +1268,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
     }
     const bool dollar = (tf & TF_DOLLAR) != 0;
     const uint32_t w0 = uni(words[tb]);
-    const uint32_t rfl = root_flags(root, dollar, w0);
+    const uint32_t rfl = root_flags(root, dollar, w0 < WID_MAX ? sig_bit(w0) : 0u);
     const bool rem = (root.w & F_HASH) && !dollar;
     unsigned long long base = 0;
     uint32_t count = 0;
@@ -1924,6 +1987,9 @@ hipError_t launch_shard_merge(const uint32_t* cnt, uint32_t G, uint32_t n, const
 // the host never issues a D2H after waiting for the count.  16-B units with
 // nontemporal stores (write-combined PCIe writes), element tails separately.
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+#ifndef EGM_COPY_OUT_BLOCKS
+#define EGM_COPY_OUT_BLOCKS 256
+#endif
 
 __device__ __forceinline__ void seg_copy16(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t bytes,
                                            uint32_t elem, uint64_t gtid, uint64_t gsize) {
@@ -1953,7 +2019,11 @@ __global__ __launch_bounds__(256) void k_copy_out(const uint64_t* __restrict__ r
 
 hipError_t launch_copy_out(const uint64_t* row, uint32_t n, const uint32_t* ids, uint64_t ids_cap,
                            const uint8_t* flags, uint8_t* h_row, uint8_t* h_ids, uint8_t* h_fl, hipStream_t s) {
-  hipLaunchKernelGGL(k_copy_out, dim3(1024), dim3(256), 0, s, row, n, ids, ids_cap, flags, h_row, h_ids, h_fl);
+  // one 256-thread block per CU is enough for the PCIe link (tools/d2hbench: 54 GB/s at 256 blocks) and
+  // leaves the CUs' other wave slots to the next batch's match on the other stream (1 024 blocks held
+  // them all for the copy's ~4 ms: r4a/r4b host_e2e 146 M topics/s)
+  hipLaunchKernelGGL(k_copy_out, dim3(EGM_COPY_OUT_BLOCKS), dim3(256), 0, s, row, n, ids, ids_cap, flags, h_row, h_ids,
+                     h_fl);
   return hipGetLastError();
 }
 

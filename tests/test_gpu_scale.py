@@ -3,8 +3,9 @@ benchmarked but never checked).
 
 * C2 at full size — 10M wildcard filters x 10M topics, the bench's own
   workload: every topic's row total against the C++ oracle (in four parts, so
-  no single test is silent for minutes), 200K sampled rows id-exact, and
-  determinism of the whole batch through a per-row order-independent checksum.
+  no single test is silent for minutes), 200K sampled rows id-exact,
+  determinism of the whole batch through a per-row order-independent checksum,
+  and the prefix-partition layout at 8 logical ranks equal to the whole table.
 * C4 at its full size: 100M filters with the subscriber table, 1M topics,
   match + fan-out; the oracle is built as 10 disjoint filter shards of 10M
   (all row totals, sampled rows id-exact, every delivery row pointer,
@@ -95,52 +96,73 @@ class TestC2Full:
         vt, _ = o.visited_counts(sub.blob, sub.off, threads=THREADS)
         assert c2["gm"].match(sub.blob, sub.off, L.EGM_MODE_ROUTES).visited == vt
 
-    def test_c2_full_eight_logical_shards_merged(self, c2):
-        """BASELINE C2's sharded layout on one GPU: the
-        10M filters split 8 ways by word_hash(filter) mod 8 with global ids,
-        the whole 10M-topic batch matched against each shard, the shard CSRs
-        merged on the GPU by egm_shard_merge — equal to the whole-table
-        result (every row pointer; every row as a set through a per-row
-        order-independent checksum)."""
+    def test_c2_full_eight_prefix_partitions(self, c2):
+        """The prefix-partition layout of BASELINE C2 at 8 ranks on one GPU
+        (VERDICT r3 item 5): the 10M filters partitioned by their first two
+        words (egm_prefix_assign: 28 % replicated, the rest on one rank each),
+        the 10M-topic batch split into 8 per-rank batches, each routed by
+        egm_prefix_route, the all_to_all emulated by device copies of the
+        slots, every received slot matched in place by
+        egm_match_device_counted (count read on the device) against its
+        rank's partition — every topic matched on exactly one rank, with the
+        whole table's row (every row total; every row as a set through a
+        per-row order-independent checksum)."""
         import torch
-        from emqx_amd.dist import shard_of
+        from emqx_amd.dist import PrefixSlots, prefix_assign, topic_slice
         f, t, res = c2["f"], c2["t"], c2["res"]
         dev = torch.device("cuda:0")
         s = torch.cuda.current_stream().cuda_stream
+        G = 8
+        vr, fr = prefix_assign(f, G)
+        parts = [topic_slice(t.n, r, G) for r in range(G)]
+        ps = PrefixSlots.for_batch(G, max(hi - lo for lo, hi in parts),
+                                   max(int(t.off[hi]) - int(t.off[lo]) for lo, hi in parts))
+        dvr = torch.from_numpy(vr).to(dev)
         d_blob = torch.from_numpy(t.blob).to(dev)
-        d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
-        n, G = t.n, 8
-        sh = shard_of(f, G)
-        m = GpuMatcher(0, max_batch=n)
-        cnts, idss = [], []
+        sends = []
+        m = GpuMatcher(0, max_batch=ps.cap_topics)
+        for lo, hi in parts:   # each rank's batch: a slice of the blob, offsets rebased to 0
+            sub_off = torch.from_numpy((t.off[lo:hi + 1] - t.off[lo]).astype(np.uint32).view(np.int32)).to(dev)
+            send = torch.zeros(G * ps.slot_bytes, dtype=torch.uint8, device=dev)
+            m.prefix_route(d_blob.data_ptr() + int(t.off[lo]), sub_off.data_ptr(), hi - lo, dvr.data_ptr(), len(vr), G,
+                           ps.cap_topics, ps.cap_bytes, s, send.data_ptr())
+            sends.append(send)
+        torch.cuda.synchronize()
+        got_tot = np.full(t.n, -1, np.int64)
+        got_sum = np.zeros(t.n, np.uint64)
+        sizes = []
         try:
-            for g in range(G):
-                idx = np.nonzero(sh == g)[0].astype(np.uint32)
+            for q in range(G):
+                idx = np.nonzero((fr == q) | (fr == L.EGM_PREFIX_ALL))[0].astype(np.uint32)
+                sizes.append(len(idx))
                 part = f.subset(idx)
                 m.build(part.blob, part.off, idx)
-                row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-                ids = torch.zeros(12 * n, dtype=torch.int32, device=dev)
-                m.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES, s,
-                               row.data_ptr(), ids.data_ptr(), ids.numel())
-                torch.cuda.synchronize()
-                st = m.last_stats()
-                assert st["overflow"] == 0 and st["errors"] == 0, (g, st)
-                cnts.append((row[1:] - row[:-1]).to(torch.int32))
-                idss.append(ids[: int(row[-1].item())].clone())
-                del row, ids
+                del part
+                recv = torch.cat([sends[r][q * ps.slot_bytes:(q + 1) * ps.slot_bytes] for r in range(G)])
+                host = recv.cpu().numpy()
+                row = torch.zeros(ps.cap_topics + 1, dtype=torch.int64, device=dev)
+                ids = torch.zeros(ps.cap_topics * 96 + 4096, dtype=torch.int32, device=dev)
+                for r in range(G):
+                    base = recv.data_ptr() + r * ps.slot_bytes
+                    m.match_device_counted(base + ps.off_bytes, ps.cap_bytes, base + ps.off_offsets, ps.cap_topics,
+                                           base, L.EGM_MODE_ROUTES, s, row.data_ptr(), ids.data_ptr(), ids.numel())
+                    torch.cuda.synchronize()
+                    st = m.last_stats()
+                    assert st["overflow"] == 0 and st["errors"] == 0, (q, r, st)
+                    cnt, nb, ovf, tids, offs, data = ps.parse(host, r)
+                    assert ovf == 0
+                    rown = row.cpu().numpy().view(np.uint64)
+                    assert np.all(rown[cnt:] == rown[cnt])   # padding: empty rows
+                    gidx = parts[r][0] + tids.astype(np.int64)
+                    assert np.all(got_tot[gidx] < 0)          # matched on exactly one rank
+                    got_tot[gidx] = np.diff(rown[:cnt + 1]).astype(np.int64)
+                    got_sum[gidx] = row_checksums(rown[:cnt + 1], ids[:int(rown[cnt])].cpu().numpy().view(np.uint32))
         finally:
             m.close()
-        counts = torch.cat(cnts)
-        total = sum(int(x.numel()) for x in idss)
-        out_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-        out_ids = torch.zeros(total + 16, dtype=torch.int32, device=dev)
-        c2["gm"].shard_merge(G, n, counts.data_ptr(), [x.data_ptr() for x in idss], total, s, out_row.data_ptr(),
-                             out_ids.data_ptr(), out_ids.numel())
-        torch.cuda.synchronize()
-        row = out_row.cpu().numpy().view(np.uint64)
-        assert np.array_equal(row, res.row_ptr)
-        ids = out_ids[:total].cpu().numpy().view(np.uint32)
-        assert np.array_equal(row_checksums(row, ids), row_checksums(res.row_ptr, res.ids))
+        assert np.all(got_tot >= 0)
+        assert np.array_equal(got_tot, np.diff(res.row_ptr).astype(np.int64))
+        assert np.array_equal(got_sum, row_checksums(res.row_ptr, res.ids))
+        assert max(sizes) < 0.45 * f.n, sizes   # a partition, not a replica (37 % at 8 ranks)
 
     def test_c2_full_determinism(self, c2):
         t, res, gm = c2["t"], c2["res"], c2["gm"]

@@ -39,7 +39,7 @@ def main():
     for h in halves:   # warm up: size the buffers
         gm.wait(gm.submit(h.blob, h.off, mode), copy=False)
     out = {}
-    for depth in (1, 2):
+    for depth in (1, 2, 3):
         ids = 0
         t0 = time.perf_counter()
         inflight = []

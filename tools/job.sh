@@ -71,7 +71,15 @@ for step in "$@"; do
     sq)
       run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU -d "$R/gpurun_out/${TAG}_pmc_sq" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off
       run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off ;;
+    sq_*)   # SQ + TCC counter passes over the C2 bench on variant V
+      v=${step#sq_}
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "pmc_sq_$v" 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU -d "$R/gpurun_out/${TAG}_pmc_sq_$v" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "pmc_tcc_$v" 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc_$v" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "pmc_sq2_$v" 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_SMEM -d "$R/gpurun_out/${TAG}_pmc_sq2_$v" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
     host) run host 600 python tools/bench_host.py ;;
+    host_*)  # the host-visible path on variant V
+      v=${step#host_}
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 python tools/bench_host.py ;;
     s2) run s2 400 python $R/bench.py --steps 20 --warmup 3 --streams 2 --cpu-baseline off --host-e2e off --x-orders "a86,0" ;;
     cap128) EGM_FIX_CAP=128 run cap128 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86/128,a86/96,a86/128" ;;
     orders) run orders 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86,0,a86/128,a86" ;;
@@ -84,6 +92,8 @@ for step in "$@"; do
       run granule_tcc 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d "$R/gpurun_out/${TAG}_granule_tcc" -o run --output-format csv -- "$R/tools/granule" ;;
     walkmix)   # what bounds the walk: its memory mix with 0-600 VALU per round at 8-32 waves per CU (tools/walkmix.hip)
       run walkmix 300 "$R/tools/walkmix" ;;
+    walkmix2)  # the same with the walk's measured 68 L2 requests per iteration and its flush stores
+      run walkmix2 300 "$R/tools/walkmix" 2 ;;
     d2h)   # device <-> pinned host copy rates (tools/d2hbench.hip)
       run d2h 120 "$R/tools/d2hbench" ;;
     c4m) run c4m 400 python $R/bench.py --config c4 --filters 10000000 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;

@@ -37,7 +37,7 @@ __device__ __forceinline__ void valu(uint32_t& a, uint32_t& b, uint32_t& c, uint
   }
 }
 
-template <int NV, int LDS_BYTES>
+template <int NV, int LDS_BYTES, int SHARE = 4, bool STORES = false>
 __global__ __launch_bounds__(64) void k_mix(const uint4* __restrict__ t, uint32_t nlines, uint32_t hot_lines, int rounds,
                                             uint32_t* out) {
   __shared__ uint32_t pad[LDS_BYTES / 4];
@@ -46,8 +46,8 @@ __global__ __launch_bounds__(64) void k_mix(const uint4* __restrict__ t, uint32_
   uint32_t a = x, b = x ^ 1u, c = x ^ 2u, d = x ^ 3u;
   pad[lane] = x;
   for (int r = 0; r < rounds; ++r) {
-    // 4 lanes share a bucket line and a record line: 16 + 16 distinct lines per wave
-    const uint32_t kb = fmix(__shfl(x, (int)(lane & ~3u), 64) + (uint32_t)r * 0x9E3779B9u);
+    // SHARE lanes share a bucket line and a record line: 2 x 64 / SHARE distinct lines per wave
+    const uint32_t kb = fmix(__shfl(x, (int)(lane & ~(uint32_t)(SHARE - 1)), 64) + (uint32_t)r * 0x9E3779B9u);
     const uint32_t kr = fmix(kb ^ 0x5bd1e995u);
     const uint32_t lb = (kb & 1023u) < 358u ? (kb >> 10) % hot_lines : kb % nlines;
     const uint32_t lr = (kr & 1023u) < 358u ? (kr >> 10) % hot_lines : kr % nlines;
@@ -58,28 +58,35 @@ __global__ __launch_bounds__(64) void k_mix(const uint4* __restrict__ t, uint32_
     a += x;
     valu<NV>(a, b, c, d);
     x += (a ^ b ^ c ^ d) & 1u;
+    if (STORES && (lane & 7u) == 0) {   // ~8 line writes per round (the walk's flush stores: 8.6 per iteration)
+      uint32_t* o = out + 64 + ((uint64_t)fmix(x + lane) % (nlines / 16 - 8)) * 16;
+      o[0] = x;
+    }
   }
   if (x == 0x12345678u) out[0] = x + pad[(lane + 1) & 63];
 }
 
-template <int NV, int LDS_BYTES>
+template <int NV, int LDS_BYTES, int SHARE = 4, bool STORES = false>
 static void run(const uint4* t, uint32_t nlines, uint32_t hot_lines, int wpc, uint32_t* out) {
   const int blocks = 256 * wpc, rounds = 1500;
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  hipLaunchKernelGGL((k_mix<NV, LDS_BYTES>), dim3(blocks), dim3(64), 0, 0, t, nlines, hot_lines, 50, out);   // warm
+  hipLaunchKernelGGL((k_mix<NV, LDS_BYTES, SHARE, STORES>), dim3(blocks), dim3(64), 0, 0, t, nlines, hot_lines, 50, out);
   hipEventRecord(e0);
-  hipLaunchKernelGGL((k_mix<NV, LDS_BYTES>), dim3(blocks), dim3(64), 0, 0, t, nlines, hot_lines, rounds, out);
+  hipLaunchKernelGGL((k_mix<NV, LDS_BYTES, SHARE, STORES>), dim3(blocks), dim3(64), 0, 0, t, nlines, hot_lines, rounds,
+                     out);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0;
   hipEventElapsedTime(&ms, e0, e1);
   const double wr = (double)blocks * rounds;   // wave-rounds
-  const double req = wr * 32.0, miss = req * 0.65;
-  printf("{\"valu_per_round\": %d, \"lds_bytes_per_wave\": %d, \"waves_per_cu_target\": %d, \"ms\": %.3f, "
+  const double req = wr * 2.0 * 64 / SHARE, miss = req * 0.65;
+  printf("{\"lines_per_round\": %d, \"stores\": %d, \"valu_per_round\": %d, \"lds_bytes_per_wave\": %d, "
+         "\"waves_per_cu_target\": %d, \"ms\": %.3f, "
          "\"M_rounds_per_s\": %.1f, \"G_lines_per_s\": %.2f, \"G_misses_per_s\": %.2f, \"ms_for_7.32M_rounds\": %.2f}\n",
-         NV, LDS_BYTES, wpc, ms, wr / ms / 1e3, req / ms / 1e6, miss / ms / 1e6, 7.32e6 / (wr / ms));
+         2 * 64 / SHARE, (int)STORES, NV, LDS_BYTES, wpc, ms, wr / ms / 1e3, req / ms / 1e6, miss / ms / 1e6,
+         7.32e6 / (wr / ms));
   hipEventDestroy(e0);
   hipEventDestroy(e1);
 }
@@ -94,14 +101,26 @@ static void sweep(const uint4* t, uint32_t nlines, uint32_t hot, int wpc, uint32
   run<600, LDS_BYTES>(t, nlines, hot, wpc, out);
 }
 
-int main() {
+int main(int argc, char**) {
   const uint64_t big = 2800ull << 20;
   uint4* t = nullptr;
   uint32_t* out = nullptr;
-  if (hipMalloc(&t, big) != hipSuccess || hipMalloc(&out, 4) != hipSuccess) return 1;
+  if (hipMalloc(&t, big) != hipSuccess || hipMalloc(&out, (big / 16) + 4096) != hipSuccess) return 1;
   hipMemset(t, 1, big);
   hipDeviceSynchronize();
   const uint32_t nlines = (uint32_t)(big / 64), hot = (2u << 20) / 64;
+  if (argc > 1) {   // round 4, second probe: the walk's measured 68 L2 requests per iteration
+    // (498M per launch / 7.32M iterations) instead of the 32 distinct lines of the emulation,
+    // and its flush stores, at the walk's 16 waves per CU
+    run<0, 10240, 2>(t, nlines, hot, 16, out);
+    run<300, 10240, 2>(t, nlines, hot, 16, out);
+    run<0, 10240, 2, true>(t, nlines, hot, 16, out);
+    run<300, 10240, 2, true>(t, nlines, hot, 16, out);
+    run<300, 10240, 4, true>(t, nlines, hot, 16, out);
+    run<600, 10240, 2, true>(t, nlines, hot, 16, out);
+    hipDeviceSynchronize();
+    return 0;
+  }
   sweep<20480>(t, nlines, hot, 8, out);    // 8 waves per CU
   sweep<13312>(t, nlines, hot, 12, out);   // 12
   sweep<10240>(t, nlines, hot, 16, out);   // 16: the walk
