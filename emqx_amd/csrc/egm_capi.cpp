@@ -573,7 +573,7 @@ static uint64_t walk_sort_min_bytes() {
 static uint32_t fix_cap_ids() {
   const char* v = getenv("EGM_FIX_CAP");
   const int k = (v && *v) ? atoi(v) : 96;
-  return (uint32_t)std::min(std::max(k, 1), 4096);
+  return (uint32_t)std::min(std::max(k, 1), 1023);   // a chunk's blocks stay 16-bit addressable (64 x cap)
 }
 
 // The workspace for a batch on stream s: the one that last ran on s (stream

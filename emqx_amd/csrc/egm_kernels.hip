@@ -507,14 +507,14 @@ static_assert(light_dmax(WALK_STACK) >= DEEP_MIN, "the first pass must take the 
 static_assert(light_dmax(WALK_STACK_DEEP) >= 16, "stack too small");
 
 #ifndef EGM_FLUSH_V2
-#define EGM_FLUSH_V2 1   // round 4 flush (below); 0: round 3's multi-split flush (A/B)
-#endif
+#define EGM_FLUSH_V2 2   // 2: LDS-atomic ranks, stores in topic order (k_walk 9.13 ms at C2);
+#endif                   // 1: the same ranks, stores in arrival order (10.31); 0: round 3's multi-split (10.17)
 
 template <uint32_t STK>
 struct alignas(16) WaveLds {
   uint4 stack[STK];
   uint32_t stage_fid[WALK_STAGE];
-#if !EGM_FLUSH_V2
+#if EGM_FLUSH_V2 != 1
   uint16_t stage_rank[WALK_STAGE];
 #endif
   uint8_t stage_t[WALK_STAGE];       // topic in chunk of the emit
@@ -561,8 +561,80 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
   return r;
 }
 
-#if EGM_FLUSH_V2
-// Write the stage out (round 4).  One pass over the staged entries in arrival
+#if EGM_FLUSH_V2 == 2
+// Write the stage out, topic-ordered (round 4, the default).  The ranks come from
+// an LDS atomic on the topic's flush counter, as in the arrival-order flush,
+// and stay in registers; one scan of the per-topic counts gives each topic's
+// first slot, every entry moves to its slot (fid and its offset inside the
+// chunk's fixed blocks), and the stores then go out slot by slot, so
+// consecutive lanes write consecutive ids of a block (one L2 request per
+// line instead of one per entry).  Ids past a topic's fixed block are written
+// to the spill slab straight from registers (rare).
+template <class LDS>
+__device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t t0, uint32_t my_t, uint32_t lane,
+                                            const MatchWork& w, Slab& sid, Slab& spc) {
+  const uint32_t cap = w.fix_cap;
+  constexpr uint32_t NQ = (WALK_STAGE + 63) / 64;
+  uint32_t fv[NQ], pv[NQ];   // fid; topic | rank inside the flush << 8 (two VGPRs per entry)
+#pragma unroll
+  for (uint32_t r = 0; r < NQ; ++r) {
+    const uint32_t i = lane + 64 * r;
+    const bool act = i < nstage;
+    const uint32_t ic = act ? i : 0u;
+    const uint32_t tt = L.stage_t[ic];
+    fv[r] = L.stage_fid[ic];
+    pv[r] = act ? tt | (atomicAdd(&L.fcnt[tt], 1u) << 8) : 0xFFFFFFFFu;
+  }
+  wave_sync();
+  const uint32_t fl = L.fcnt[lane];   // the chunk's topic `lane`: ids in this flush
+  const uint32_t c0 = L.cnt[lane];    // ... and before it
+  const uint32_t nfix = c0 >= cap ? 0u : min(fl, cap - c0);
+  const uint32_t over = fl - nfix;    // ids past the fixed block: spilled
+  uint32_t tot, gtot;
+  const uint32_t gx = wave_excl_scan(nfix, lane, &gtot);
+  const uint32_t ex = wave_excl_scan(over, lane, &tot);
+  unsigned long long base = 0;
+  bool ok = true;
+  if (tot) {   // wave-uniform
+    uint32_t ptot;
+    const uint32_t pex = wave_excl_scan(over ? 1u : 0u, lane, &ptot);
+    base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
+    const unsigned long long pbase =
+        slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
+    ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
+    if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
+    if (over && ok) w.pieces[pbase + pex] = make_uint4(my_t, over, (uint32_t)(base + ex), c0 + nfix);
+  }
+  L.fcnt[lane] = gx | (ex << 16);   // first slot | spill start (both < WALK_STAGE)
+  wave_sync();
+#pragma unroll
+  for (uint32_t r = 0; r < NQ; ++r) {
+    if (pv[r] == 0xFFFFFFFFu) continue;
+    const uint32_t tt = pv[r] & 0xFFu, f = L.fcnt[tt], cb = L.cnt[tt], k = cb + (pv[r] >> 8);
+    if (k < cap) {
+      const uint32_t q = (f & 0xFFFFu) + (pv[r] >> 8);
+      L.stage_fid[q] = fv[r];
+      L.stage_rank[q] = (uint16_t)(tt * cap + k);   // < 64 x fix_cap <= 65472 (egm_capi.cpp fix_cap_ids)
+    } else if (ok) {
+      w.ids_tmp[base + (f >> 16) + (k - max(cb, cap))] = fv[r];
+    }
+  }
+  wave_sync();
+  const uint64_t blk = (uint64_t)t0 * cap;
+#pragma unroll 1
+  for (uint32_t q = lane; q < gtot; q += 64) {
+#ifdef EGM_AB_NO_ID_STORES   // measurement only (tools/build_variant.py): the walk without its id stores
+    if (L.stage_fid[q] != 0x7FFFFFF1u) continue;
+#endif
+    w.ids_fix[blk + L.stage_rank[q]] = L.stage_fid[q];
+  }
+  wave_sync();
+  L.cnt[lane] += fl;
+  L.fcnt[lane] = 0;
+  wave_sync();
+}
+#elif EGM_FLUSH_V2
+// Write the stage out in arrival order (round 4, A/B: EGM_FLUSH_V2=1).  One pass over the staged entries in arrival
 // order: an LDS atomic on the topic's flush counter ranks each entry inside
 // its topic, and the entry is stored at once into the topic's fixed block
 // (ids_fix, walk position x fix_cap) at cnt + rank — its place inside the
@@ -1988,7 +2060,7 @@ hipError_t launch_shard_merge(const uint32_t* cnt, uint32_t G, uint32_t n, const
 // nontemporal stores (write-combined PCIe writes), element tails separately.
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 #ifndef EGM_COPY_OUT_BLOCKS
-#define EGM_COPY_OUT_BLOCKS 256
+#define EGM_COPY_OUT_BLOCKS 64   // host path at C2: 64 -> 159M topics/s, 256 -> 141M, 1024 -> 140M (profiles/r4_host_ab.jsonl)
 #endif
 
 __device__ __forceinline__ void seg_copy16(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t bytes,

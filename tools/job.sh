@@ -12,6 +12,7 @@
 #   bench_sK   the C2 bench with K streams (bench_s1: no overlap of consecutive batches)
 #   bench_c1|bench_c3|bench_c4   the other configs under rocprofv3 --stats
 #   shard1     bench.py --mode shard at world 1 via torch.distributed.run
+#   prefix1    bench.py --mode prefix (root-word partitions, one all_to_all) at world 1
 #   pmc        FETCH_SIZE and WRITE_SIZE passes over the C2 bench (one counter per pass)
 #   sq         SQ wait/active counters + TCC hit/miss over the C2 bench
 #   host       host-visible path (egm_match_batch, pinned staging) bench
@@ -61,6 +62,7 @@ for step in "$@"; do
     shardfan) run shardfan 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --config c4 --filters 2000000 --topics 1000000 --mode shard --steps 5 --warmup 1 --cpu-baseline off ;;
     shardleg) run shardleg 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29535 bench.py --sharded-leg on --steps 5 --warmup 1 --cpu-baseline off --host-e2e off --pipelined off ;;
     slowd) run slowd 1100 python -u -m pytest tests -m "gpu and slow" -x -v --timeout 900 --timeout-method thread --durations=0 ;;
+    prefix1) run prefix1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29536 bench.py --mode prefix --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
     shard1) run shard1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --mode shard --steps 10 --warmup 2 --cpu-baseline off ;;
     pmc)
       run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
