@@ -562,7 +562,7 @@ def main():
         gm.build(f.blob, f.off)
     tstats = gm.stats()
     log(f"[rank {rank}] table built in {time.time() - t0:.1f}s: {tstats}")
-    sub_entries = leg.sub_entries if leg is not None else 0
+    sub_entries = getattr(leg, "sub_entries", 0)   # the shard leg's subscriber table; none for prefix
     if fanout and not shard:
         # filter id -> subscriber CSR (emqx_subscriber bag, shards flattened)
         t0 = time.time()

@@ -100,9 +100,13 @@ struct PipeSlot {
   PinBuf h_in, h_out, h_stats;
   DevBuf d_blob, d_off, d_row, d_ids, d_flags;
   // ev_in: staged input copied in; ev_match: matched (stream s); ev_done: the
-  // CSR written into h_out by the copy-out kernel (d2h stream)
+  // CSR in h_out (the copier's D2H copies, or the copy-out kernel)
   hipEvent_t ev_in = nullptr, ev_match = nullptr, ev_done = nullptr;
   uint64_t epoch = 0;
+  // launches of this slot / of them, how many the copier has enqueued the
+  // D2H of (ev_done is recorded for launch k once copied_gen == k; guarded by
+  // egm_ctx::cq_mu)
+  uint64_t launch_gen = 0, copied_gen = 0;
   ~PipeSlot() {
     if (ev_in) hipEventDestroy(ev_in);
     if (ev_match) hipEventDestroy(ev_match);
@@ -251,6 +255,19 @@ struct egm_ctx {
   std::vector<uint64_t> cancel_q;        // cancels that found the context busy (egm_match_cancel)
   hipStream_t copy_stream = nullptr;   // pipeline host->device copies
   hipStream_t d2h_stream = nullptr;    // pipeline device->host copies (PCIe is full duplex)
+  hipStream_t d2h_stream2 = nullptr;   // ... the second half of the ids
+  // The copier thread (round 4): it waits for each launched batch's match
+  // (ev_match; the stats, copied before it in stream order, hold the exact id
+  // total) and enqueues the result's D2H as DMA copies of exactly that size.
+  // A copy-out kernel storing to pinned memory instead (EGM_PIPE_COPY=kernel)
+  // stalls the next batch's memory-bound kernels behind the PCIe writes
+  // (k_tokenise 0.1 -> 1-2 ms beside it, profiles/r4_host_trace.json).
+  std::thread copier;
+  std::mutex cq_mu;                    // guards cq, cq_stop and every slot's launch/copied gens
+  std::condition_variable cq_cv;       // work for the copier
+  std::condition_variable copied_cv;   // a slot's D2H was enqueued
+  std::vector<std::pair<PipeSlot*, uint64_t>> cq;
+  bool cq_stop = false;
   // last fan-out (egm_last_fanout)
   const uint64_t* fan_drow = nullptr;
   uint32_t fan_topics = 0;
@@ -831,11 +848,25 @@ void egm_close(egm_ctx* c) {
     if (c->work_ev) hipEventDestroy(c->work_ev);
     c->work_ev = nullptr;
     if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
+  }
+  if (c->copier.joinable()) {   // outside the context lock: the copier never takes it
+    {
+      std::lock_guard<std::mutex> q(c->cq_mu);
+      c->cq_stop = true;
+    }
+    c->cq_cv.notify_all();
+    c->copier.join();
+  }
+  {
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    set_device(c);
     if (c->d2h_stream) hipStreamSynchronize(c->d2h_stream);
+    if (c->d2h_stream2) hipStreamSynchronize(c->d2h_stream2);
     c->pipe.clear();
     if (c->copy_stream) hipStreamDestroy(c->copy_stream);
     if (c->d2h_stream) hipStreamDestroy(c->d2h_stream);
-    c->copy_stream = c->d2h_stream = nullptr;
+    if (c->d2h_stream2) hipStreamDestroy(c->d2h_stream2);
+    c->copy_stream = c->d2h_stream = c->d2h_stream2 = nullptr;
   }
   hipStreamDestroy(c->stream);
   delete c;
@@ -1057,6 +1088,16 @@ static void par_copy(void* dst, const void* src, size_t bytes) {
   par_for(bytes, 4u << 20, [=](size_t lo, size_t hi) { memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, hi - lo); });
 }
 
+// EGM_PIPE_COPY=kernel: the round-4 copy-out kernel instead of the copier's DMA (A/B).
+static bool pipe_copy_kernel() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("EGM_PIPE_COPY");
+    v = (e && strcmp(e, "kernel") == 0) ? 1 : 0;
+  }
+  return v == 1;
+}
+
 // Enqueue one staged batch of slot S: H2D on the copy stream, the match on
 // the context stream once the input is in, then the batch's flags and
 // counters copied out in stream order (the next batch reuses the workspace).
@@ -1090,15 +1131,79 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
     return c->hip_fail(e, "pipe epilogue");
   }
   ws_done(W, s);
-  // the CSR straight into pinned memory, sized on the device, on the copy
-  // stream: it runs beside the next batch's match
-  uint8_t* h = (uint8_t*)S.h_out.p;
-  if ((e = hipStreamWaitEvent(c->d2h_stream, S.ev_match, 0)) != hipSuccess ||
-      (e = launch_copy_out(S.d_row.as<uint64_t>(), (uint32_t)n, S.d_ids.as<uint32_t>(), S.cap, S.d_flags.as<uint8_t>(),
-                           h + ol.o_row, h + ol.o_ids, h + ol.o_fl, c->d2h_stream)) != hipSuccess ||
-      (e = hipEventRecord(S.ev_done, c->d2h_stream)) != hipSuccess)
-    return c->hip_fail(e, "pipe copy-out");
+  if (pipe_copy_kernel()) {
+    // the CSR straight into pinned memory by a kernel, sized on the device
+    uint8_t* h = (uint8_t*)S.h_out.p;
+    if ((e = hipStreamWaitEvent(c->d2h_stream, S.ev_match, 0)) != hipSuccess ||
+        (e = launch_copy_out(S.d_row.as<uint64_t>(), (uint32_t)n, S.d_ids.as<uint32_t>(), S.cap,
+                             S.d_flags.as<uint8_t>(), h + ol.o_row, h + ol.o_ids, h + ol.o_fl, c->d2h_stream)) !=
+            hipSuccess ||
+        (e = hipEventRecord(S.ev_done, c->d2h_stream)) != hipSuccess)
+      return c->hip_fail(e, "pipe copy-out");
+    std::lock_guard<std::mutex> q(c->cq_mu);
+    S.copied_gen = ++S.launch_gen;
+    return EGM_OK;
+  }
+  {   // the copier enqueues the D2H once the match is done
+    std::lock_guard<std::mutex> q(c->cq_mu);
+    c->cq.emplace_back(&S, ++S.launch_gen);
+  }
+  c->cq_cv.notify_one();
   return EGM_OK;
+}
+
+// The copier thread's loop (egm_ctx::copier): in launch order, wait for a
+// batch's match, then enqueue its result's D2H — row_ptr and flags and the
+// first half of the ids on one DMA stream, the second half on another (one
+// stream alone measured 17-57 GB/s, two 56) — and record ev_done.  It never
+// takes the context lock; a slot it holds is not reused before copied_gen
+// reaches its launch (the waiter and the cancel path check it).
+static void copier_main(egm_ctx* c) {
+  hipSetDevice(c->device);
+  hipEvent_t join = nullptr;
+  hipEventCreateWithFlags(&join, hipEventDisableTiming);
+  for (;;) {
+    std::pair<PipeSlot*, uint64_t> it;
+    {
+      std::unique_lock<std::mutex> q(c->cq_mu);
+      c->cq_cv.wait(q, [&] { return c->cq_stop || !c->cq.empty(); });
+      if (c->cq.empty()) break;   // stopping, nothing left
+      it = c->cq.front();
+      c->cq.erase(c->cq.begin());
+    }
+    PipeSlot& S = *it.first;
+    hipError_t e = hipEventSynchronize(S.ev_match);
+    const MatchStats st = *(const MatchStats*)S.h_stats.p;   // copied before ev_match, in stream order
+    if (e == hipSuccess && !st.overflow && !st.guard) {
+      const uint64_t n = S.n, nids = std::min<uint64_t>(st.total_ids, S.cap), half = (nids / 2 + 3) & ~3ull;
+      const OutLayout ol = out_layout(n, S.cap);
+      uint8_t* h = (uint8_t*)S.h_out.p;
+      hipMemcpyAsync(h + ol.o_row, S.d_row.p, (n + 1) * 8, hipMemcpyDeviceToHost, c->d2h_stream);
+      if (n) hipMemcpyAsync(h + ol.o_fl, S.d_flags.p, n, hipMemcpyDeviceToHost, c->d2h_stream);
+      const uint64_t h1 = std::min(half, nids);
+      if (h1) hipMemcpyAsync(h + ol.o_ids, S.d_ids.p, h1 * 4, hipMemcpyDeviceToHost, c->d2h_stream);
+      if (nids > h1) {
+        hipMemcpyAsync(h + ol.o_ids + h1 * 4, (const uint8_t*)S.d_ids.p + h1 * 4, (nids - h1) * 4,
+                       hipMemcpyDeviceToHost, c->d2h_stream2);
+        hipEventRecord(join, c->d2h_stream2);
+        hipStreamWaitEvent(c->d2h_stream, join, 0);
+      }
+    }
+    // an overflowed or guarded batch copies nothing: the waiter reads the stats
+    hipEventRecord(S.ev_done, c->d2h_stream);
+    {
+      std::lock_guard<std::mutex> q(c->cq_mu);
+      S.copied_gen = it.second;
+    }
+    c->copied_cv.notify_all();
+  }
+  if (join) hipEventDestroy(join);
+}
+
+// Whether the slot's last launch has its D2H enqueued (ev_done recorded).
+static bool slot_copied(egm_ctx* c, PipeSlot& S) {
+  std::lock_guard<std::mutex> q(c->cq_mu);
+  return S.copied_gen == S.launch_gen;
 }
 
 // A free pipeline slot for a batch (index into c->pipe), or -1.  Slots whose
@@ -1121,7 +1226,7 @@ static long pipe_free_slot(egm_ctx* c) {
   drain_cancels(c);
   for (size_t k = 0; k < c->pipe.size(); ++k) {
     PipeSlot& S = *c->pipe[k];
-    if (S.busy && S.abandoned && !S.waiting && hipEventQuery(S.ev_done) == hipSuccess) {
+    if (S.busy && S.abandoned && !S.waiting && slot_copied(c, S) && hipEventQuery(S.ev_done) == hipSuccess) {
       S.busy = S.abandoned = false;   // a cancelled ticket whose batch is done
     }
     if (!S.busy && !S.held) return (long)k;
@@ -1155,6 +1260,9 @@ static int submit_locked(egm_ctx* c, std::unique_lock<std::recursive_mutex>& g, 
     return c->hip_fail(e, "copy stream");
   if (!c->d2h_stream && (e = hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking)) != hipSuccess)
     return c->hip_fail(e, "d2h stream");
+  if (!c->d2h_stream2 && (e = hipStreamCreateWithFlags(&c->d2h_stream2, hipStreamNonBlocking)) != hipSuccess)
+    return c->hip_fail(e, "d2h stream");
+  if (!c->copier.joinable()) c->copier = std::thread(copier_main, c);
   if (!sync) {
     size_t tickets = 0;
     for (auto& p : c->pipe)   // a cancelled ticket no longer counts (its slot comes back when its batch is done)
@@ -1260,6 +1368,10 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   MatchStats st{};
   for (int attempt = 0;; ++attempt) {
     g.unlock();
+    {   // the copier has enqueued this launch's D2H (ev_done recorded for it)
+      std::unique_lock<std::mutex> q(c->cq_mu);
+      c->copied_cv.wait(q, [&] { return S.copied_gen == S.launch_gen; });
+    }
     e = hipEventSynchronize(S.ev_done);
     g.lock();
     if (e != hipSuccess) return done(c->hip_fail(e, "pipe wait"));

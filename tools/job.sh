@@ -16,6 +16,7 @@
 #   pmc        FETCH_SIZE and WRITE_SIZE passes over the C2 bench (one counter per pass)
 #   sq         SQ wait/active counters + TCC hit/miss over the C2 bench
 #   host       host-visible path (egm_match_batch, pinned staging) bench
+#   host_trace the same under rocprofv3 --kernel-trace --memory-copy-trace (timeline)
 #   s2         the C2 bench with two streams (consecutive batches overlap), then sorted / input order
 #   orders     the C2 bench, then the walk-order A/B (sort key shapes) in the same process
 #   smoke      __graft_entry__.smoke()
@@ -79,6 +80,9 @@ for step in "$@"; do
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "pmc_tcc_$v" 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc_$v" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "pmc_sq2_$v" 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_SMEM -d "$R/gpurun_out/${TAG}_pmc_sq2_$v" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
     host) run host 600 python tools/bench_host.py ;;
+    host_k) EGM_PIPE_COPY=kernel run host_k 600 python tools/bench_host.py ;;   # A/B: the copy-out kernel
+    host_trace)   # the host path's timeline: kernels and copies (no counters)
+      run host_trace 600 rocprofv3 --kernel-trace --memory-copy-trace -d "$R/gpurun_out/${TAG}_host_trace" -o run --output-format csv -- python tools/bench_host.py --batches 10 ;;
     host_*)  # the host-visible path on variant V
       v=${step#host_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 python tools/bench_host.py ;;
