@@ -24,7 +24,7 @@ LIB = os.path.join(HERE, "libemqx_gpu_match.so")
 SYNTH = os.path.join(HERE, "libegm_synth.so")
 ORACLE = os.path.join(ROOT, "oracle", "liboracle_trie.so")
 
-HEADERS = [os.path.join(CSRC, f) for f in ("egm_common.h", "egm_table.h", "egm_kernels.h")] + [
+HEADERS = [os.path.join(CSRC, f) for f in ("egm_common.h", "egm_table.h", "egm_kernels.h", "egm_dma.h")] + [
     os.path.join(ROOT, "include", "emqx_gpu_match.h")]
 
 
@@ -59,7 +59,7 @@ def build_lib(verbose=False, force=False) -> str:
         _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result", "-Wno-unused-value",
               "-c", hip_src, "-o", o], verbose)
     objs.append(o)
-    for name in ("egm_table.cpp", "egm_bulk.cpp", "egm_capi.cpp", "egm_retain.cpp"):
+    for name in ("egm_table.cpp", "egm_bulk.cpp", "egm_capi.cpp", "egm_retain.cpp", "egm_dma.cpp"):
         src = os.path.join(CSRC, name)
         o = os.path.join(BUILD, name.replace(".cpp", ".o"))
         if force or _stale(o, [src] + HEADERS):
@@ -67,7 +67,8 @@ def build_lib(verbose=False, force=False) -> str:
                   f"-I{ROCM}/include", "-c", src, "-o", o], verbose)
         objs.append(o)
     if force or _stale(LIB, objs + [os.path.abspath(__file__)]):
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", LIB] + objs, verbose)
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", LIB] + objs +
+             [f"-L{ROCM}/lib", "-lhsa-runtime64"], verbose)
     return LIB
 
 

@@ -22,6 +22,7 @@
 
 #include "../../include/emqx_gpu_match.h"
 #include "egm_alloc.h"
+#include "egm_dma.h"
 #include "egm_kernels.h"
 #include "egm_table.h"
 
@@ -107,6 +108,7 @@ struct PipeSlot {
   // D2H of (ev_done is recorded for launch k once copied_gen == k; guarded by
   // egm_ctx::cq_mu)
   uint64_t launch_gen = 0, copied_gen = 0;
+  bool copy_failed = false;   // the copier's DMA reported an error (guarded by cq_mu)
   ~PipeSlot() {
     if (ev_in) hipEventDestroy(ev_in);
     if (ev_match) hipEventDestroy(ev_match);
@@ -1088,15 +1090,20 @@ static void par_copy(void* dst, const void* src, size_t bytes) {
   par_for(bytes, 4u << 20, [=](size_t lo, size_t hi) { memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, hi - lo); });
 }
 
-// EGM_PIPE_COPY=kernel: the round-4 copy-out kernel instead of the copier's DMA (A/B).
-static bool pipe_copy_kernel() {
+// How a pipeline result reaches pinned memory (EGM_PIPE_COPY, A/B):
+//   dma (default) — the copier thread, SDMA engines through the HSA runtime
+//   hip           — the copier thread, hipMemcpyAsync (a blit kernel here)
+//   kernel        — a copy-out kernel on the d2h stream, sized on the device
+enum { PIPE_DMA = 0, PIPE_HIP = 1, PIPE_KERNEL = 2 };
+static int pipe_copy_mode() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("EGM_PIPE_COPY");
-    v = (e && strcmp(e, "kernel") == 0) ? 1 : 0;
+    v = (e && strcmp(e, "kernel") == 0) ? PIPE_KERNEL : (e && strcmp(e, "hip") == 0) ? PIPE_HIP : PIPE_DMA;
   }
-  return v == 1;
+  return v;
 }
+static bool pipe_copy_kernel() { return pipe_copy_mode() == PIPE_KERNEL; }
 
 // Enqueue one staged batch of slot S: H2D on the copy stream, the match on
 // the context stream once the input is in, then the batch's flags and
@@ -1162,6 +1169,7 @@ static void copier_main(egm_ctx* c) {
   hipSetDevice(c->device);
   hipEvent_t join = nullptr;
   hipEventCreateWithFlags(&join, hipEventDisableTiming);
+  Dma* dma = pipe_copy_mode() == PIPE_DMA ? dma_open(c->device) : nullptr;   // null: hipMemcpyAsync
   for (;;) {
     std::pair<PipeSlot*, uint64_t> it;
     {
@@ -1172,9 +1180,20 @@ static void copier_main(egm_ctx* c) {
       c->cq.erase(c->cq.begin());
     }
     PipeSlot& S = *it.first;
-    hipError_t e = hipEventSynchronize(S.ev_match);
+    hipError_t e = hipEventSynchronize(S.ev_match);   // (a host-synchronised event: device writes released)
     const MatchStats st = *(const MatchStats*)S.h_stats.p;   // copied before ev_match, in stream order
-    if (e == hipSuccess && !st.overflow && !st.guard) {
+    bool failed = false;
+    if (e == hipSuccess && !st.overflow && !st.guard && dma) {
+      const uint64_t n = S.n, nids = std::min<uint64_t>(st.total_ids, S.cap), half = (nids / 2 + 3) & ~3ull;
+      const uint64_t h1 = std::min(half, nids);
+      const OutLayout ol = out_layout(n, S.cap);
+      uint8_t* h = (uint8_t*)S.h_out.p;
+      const DmaPart parts[4] = {{h + ol.o_ids, S.d_ids.p, h1 * 4},
+                                {h + ol.o_ids + h1 * 4, (const uint8_t*)S.d_ids.p + h1 * 4, (nids - h1) * 4},
+                                {h + ol.o_row, S.d_row.p, (n + 1) * 8},
+                                {h + ol.o_fl, S.d_flags.p, n}};
+      failed = !dma_copy_d2h(dma, parts, 4);
+    } else if (e == hipSuccess && !st.overflow && !st.guard) {
       const uint64_t n = S.n, nids = std::min<uint64_t>(st.total_ids, S.cap), half = (nids / 2 + 3) & ~3ull;
       const OutLayout ol = out_layout(n, S.cap);
       uint8_t* h = (uint8_t*)S.h_out.p;
@@ -1194,10 +1213,12 @@ static void copier_main(egm_ctx* c) {
     {
       std::lock_guard<std::mutex> q(c->cq_mu);
       S.copied_gen = it.second;
+      S.copy_failed = failed;
     }
     c->copied_cv.notify_all();
   }
   if (join) hipEventDestroy(join);
+  dma_close(dma);
 }
 
 // Whether the slot's last launch has its D2H enqueued (ev_done recorded).
@@ -1368,13 +1389,16 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   MatchStats st{};
   for (int attempt = 0;; ++attempt) {
     g.unlock();
-    {   // the copier has enqueued this launch's D2H (ev_done recorded for it)
+    bool copy_failed = false;
+    {   // the copier has copied this launch's result (DMA) or enqueued its D2H (ev_done recorded)
       std::unique_lock<std::mutex> q(c->cq_mu);
       c->copied_cv.wait(q, [&] { return S.copied_gen == S.launch_gen; });
+      copy_failed = S.copy_failed;
     }
     e = hipEventSynchronize(S.ev_done);
     g.lock();
     if (e != hipSuccess) return done(c->hip_fail(e, "pipe wait"));
+    if (copy_failed) return done(c->fail(EGM_E_DEVICE, "pipe result copy (SDMA) failed"));
     st = *(const MatchStats*)S.h_stats.p;
     if (st.guard) {   // a kernel invariant failed: a bug, never a capacity problem (no retry)
       c->last = st;

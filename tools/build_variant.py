@@ -22,10 +22,11 @@ os.makedirs(bdir, exist_ok=True)
 objs = [os.path.join(bdir, "egm_kernels.o")]
 B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
         "-Wno-unused-value", *flags, "-c", os.path.join(B.CSRC, "egm_kernels.hip"), "-o", objs[0]], True)
-for name in ("egm_table.cpp", "egm_bulk.cpp", "egm_capi.cpp", "egm_retain.cpp"):
+for name in ("egm_table.cpp", "egm_bulk.cpp", "egm_capi.cpp", "egm_retain.cpp", "egm_dma.cpp"):
     o = os.path.join(bdir, name.replace(".cpp", ".o"))
     B._run(["g++", "-O3", "-fPIC", "-std=c++17", "-pthread", "-D__HIP_PLATFORM_AMD__", f"-I{B.ROCM}/include", *flags,
             "-c", os.path.join(B.CSRC, name), "-o", o], True)
     objs.append(o)
-B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-pthread", "-o", out] + objs, True)
+B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-pthread", "-o", out] + objs +
+       [f"-L{B.ROCM}/lib", "-lhsa-runtime64"], True)
 print(out)
