@@ -270,6 +270,7 @@ struct egm_ctx {
   std::condition_variable copied_cv;   // a slot's D2H was enqueued
   std::vector<std::pair<PipeSlot*, uint64_t>> cq;
   bool cq_stop = false;
+  uint64_t pipe_cap_hint = 0;          // ids room a batch needed (overflow reruns): new slots start there
   // last fan-out (egm_last_fanout)
   const uint64_t* fan_drow = nullptr;
   uint32_t fan_topics = 0;
@@ -1105,6 +1106,20 @@ static int pipe_copy_mode() {
 }
 static bool pipe_copy_kernel() { return pipe_copy_mode() == PIPE_KERNEL; }
 
+// EGM_PIPE_TRACE=1: one stderr line per pipeline event with a ms clock
+// (diagnostics of the host pipeline's bubbles).
+static void ptrace(const char* what, const void* slot, uint64_t gen) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("EGM_PIPE_TRACE");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (v != 1) return;
+  static const auto t0 = std::chrono::steady_clock::now();
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  fprintf(stderr, "[pipe] %10.3f %-14s %p %llu\n", ms, what, slot, (unsigned long long)gen);
+}
+
 // Enqueue one staged batch of slot S: H2D on the copy stream, the match on
 // the context stream once the input is in, then the batch's flags and
 // counters copied out in stream order (the next batch reuses the workspace).
@@ -1180,7 +1195,9 @@ static void copier_main(egm_ctx* c) {
       c->cq.erase(c->cq.begin());
     }
     PipeSlot& S = *it.first;
+    ptrace("copier-take", &S, it.second);
     hipError_t e = hipEventSynchronize(S.ev_match);   // (a host-synchronised event: device writes released)
+    ptrace("match-done", &S, it.second);
     const MatchStats st = *(const MatchStats*)S.h_stats.p;   // copied before ev_match, in stream order
     bool failed = false;
     if (e == hipSuccess && !st.overflow && !st.guard && dma) {
@@ -1209,6 +1226,7 @@ static void copier_main(egm_ctx* c) {
       }
     }
     // an overflowed or guarded batch copies nothing: the waiter reads the stats
+    ptrace("copied", &S, it.second);
     hipEventRecord(S.ev_done, c->d2h_stream);
     {
       std::lock_guard<std::mutex> q(c->cq_mu);
@@ -1332,7 +1350,8 @@ static int submit_locked(egm_ctx* c, std::unique_lock<std::recursive_mutex>& g, 
   S.mode = mode;
   S.bytes = bytes;
   S.maxlen = maxlen.load();
-  S.cap = std::max<uint64_t>(std::max<uint64_t>((uint64_t)n * 4 + 1024, S.cap), c->out_ids.cap / 4);
+  S.cap = std::max<uint64_t>(std::max<uint64_t>((uint64_t)n * 4 + 1024, S.cap),
+                             std::max<uint64_t>(c->out_ids.cap / 4, c->pipe_cap_hint));
   if ((e = S.d_blob.ensure(bytes + 16)) != hipSuccess) return c->hip_fail(e, "pipe blob");
   if ((e = S.d_off.ensure(((uint64_t)n + 1) * 4)) != hipSuccess) return c->hip_fail(e, "pipe offsets");
   if ((bytes && (e = hipMemcpyAsync(S.d_blob.p, hin, bytes, hipMemcpyHostToDevice, c->copy_stream)) != hipSuccess) ||
@@ -1354,8 +1373,11 @@ static int submit_locked(egm_ctx* c, std::unique_lock<std::recursive_mutex>& g, 
 int egm_match_submit(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, int mode, uint64_t* ticket) {
   if (!c || !ticket || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES)) return EGM_E_INVAL;
   if (n && (!off || !valid_offsets(off, n) || (!blob && off[n] > off[0]))) return EGM_E_INVAL;
+  ptrace("submit-enter", nullptr, n);
   std::unique_lock<std::recursive_mutex> g(c->mu);
-  return submit_locked(c, g, blob, off, n, mode, false, ticket);
+  const int r = submit_locked(c, g, blob, off, n, mode, false, ticket);
+  ptrace("submit-exit", nullptr, *ticket);
+  return r;
 }
 
 // The slot of a live ticket (submitted, not yet waited for or cancelled), or null.
@@ -1387,6 +1409,7 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   };
   hipError_t e;
   MatchStats st{};
+  ptrace("wait-enter", &S, ticket);
   for (int attempt = 0;; ++attempt) {
     g.unlock();
     bool copy_failed = false;
@@ -1409,6 +1432,7 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
     if (attempt == 2) return done(c->fail(EGM_E_NOMEM, "ids capacity"));
     // the exact total is known even on overflow: rerun the staged batch once with room for it
     S.cap = st.total_ids + st.total_ids / 8 + 1024;
+    c->pipe_cap_hint = std::max(c->pipe_cap_hint, S.cap);
     const int r = pipe_launch(c, S);
     if (r) return done(r);
   }
@@ -1455,6 +1479,7 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   hdr->slot = ticket_slot(ticket);
   S.held = true;
   done(EGM_OK);
+  ptrace("wait-exit", &S, ticket);
   *out = res;
   if (res->n_error) {
     c->err = "some topics could not be walked (flag EGM_TF_ERROR)";

@@ -80,6 +80,7 @@ for step in "$@"; do
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "pmc_tcc_$v" 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc_$v" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "pmc_sq2_$v" 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_SMEM -d "$R/gpurun_out/${TAG}_pmc_sq2_$v" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
     host) run host 600 python tools/bench_host.py ;;
+    host_ptrace) EGM_PIPE_TRACE=1 run host_ptrace 600 python tools/bench_host.py ;;   # pipeline events on stderr
     host_hip) EGM_PIPE_COPY=hip run host_hip 600 python tools/bench_host.py ;;   # A/B: hipMemcpyAsync (blit kernel)
     host_k) EGM_PIPE_COPY=kernel run host_k 600 python tools/bench_host.py ;;   # A/B: the copy-out kernel
     host_trace)   # the host path's timeline: kernels and copies (no counters)
