@@ -219,6 +219,50 @@ def test_pipeline_submit_wait(gm):
     assert np.array_equal(again.row_ptr, want[3].row_ptr)
 
 
+def test_pipeline_deep_in_flight_exact(gm):
+    """Round 4's copier thread (results moved by SDMA copies sized from the
+    device's id total, egm_capi.cpp copier_main): 4-6 batches in flight on a
+    fresh context — its first batches overflow their slots' id room and are
+    rerun — of C2-shaped topics (~50 ids per topic), every result equal to the
+    one-by-one device match, itself checked against the C++ oracle on a sample."""
+    f, t = synth.config("c2", n_filters=300_000, n_topics=240_000)
+    m = GpuMatcher(0)
+    try:
+        m.build(f.blob, f.off)
+        parts = [t.subset(np.arange(k * 30_000, (k + 1) * 30_000)) for k in range(8)]
+        want = [m.match(p.blob, p.off, L.EGM_MODE_ROUTES) for p in parts]
+        assert int(want[0].row_ptr[-1]) > 15 * 30_000   # a sizeable result per batch (~21 ids per topic)
+        o = OracleTrie(True, L.EGM_MODE_ROUTES)
+        o.add(f.blob, f.off)
+        sub = parts[5].subset(np.arange(0, 3_000))
+        orow, oids = o.match(sub.blob, sub.off, threads=4)
+        w5 = m.match(sub.blob, sub.off, L.EGM_MODE_ROUTES)
+        assert np.array_equal(w5.row_ptr, orow)
+        assert np.array_equal(canonical(w5.row_ptr, w5.ids), canonical(orow, oids))
+        m2 = GpuMatcher(0)   # fresh pipeline slots: the first batches rerun with more id room
+        try:
+            m2.build(f.blob, f.off)
+            from collections import deque
+            for depth in (4, 6):
+                inflight, k = deque(), 0
+                for r in range(2 * len(parts)):
+                    j = r % len(parts)
+                    inflight.append((j, m2.submit(parts[j].blob, parts[j].off, L.EGM_MODE_ROUTES)))
+                    while len(inflight) >= depth or (r == 2 * len(parts) - 1 and inflight):
+                        jj, tk = inflight.popleft()
+                        got = m2.wait(tk)
+                        assert np.array_equal(got.row_ptr, want[jj].row_ptr), (depth, jj)
+                        assert np.array_equal(canonical(got.row_ptr, got.ids),
+                                              canonical(want[jj].row_ptr, want[jj].ids)), (depth, jj)
+                        assert np.array_equal(got.flags, want[jj].flags)
+                        k += 1
+                assert k == 2 * len(parts)
+        finally:
+            m2.close()
+    finally:
+        m.close()
+
+
 def test_pipeline_tickets_are_generational_and_cancellable(gm):
     """a ticket carries a generation (a stale or repeated ticket is
     refused, never answered with another batch's result) and can be given up
