@@ -270,7 +270,13 @@ struct egm_ctx {
   std::condition_variable copied_cv;   // a slot's D2H was enqueued
   std::vector<std::pair<PipeSlot*, uint64_t>> cq;
   bool cq_stop = false;
-  uint64_t pipe_cap_hint = 0;          // ids room a batch needed (overflow reruns): new slots start there
+  uint64_t pipe_cap_hint = 0;
+  // the last match launch's walk order, for a fan-out of the same rows (k_fan_count_ord)
+  struct {
+    const uint64_t* order = nullptr;   // null: that batch was walked in input order
+    const uint64_t* row = nullptr;
+    uint32_t n = 0, ws = 0;
+  } last_walk;          // ids room a batch needed (overflow reruns): new slots start there
   // last fan-out (egm_last_fanout)
   const uint64_t* fan_drow = nullptr;
   uint32_t fan_topics = 0;
@@ -710,7 +716,12 @@ static int run_match(egm_ctx* c, MatchWs& W, const Epoch& ep, const uint8_t* d_b
     evp[0] = c->take_event();
     evp[1] = c->take_event();
   }
-  hipError_t e = launch_match(ep.view, d_blob, d_off, n, mode, w, o, s, c->timing ? evp : nullptr);
+  bool walk_sorted = false;
+  hipError_t e = launch_match(ep.view, d_blob, d_off, n, mode, w, o, s, c->timing ? evp : nullptr, &walk_sorted);
+  c->last_walk.order = walk_sorted ? w.order : nullptr;
+  c->last_walk.row = d_row;
+  c->last_walk.n = n;
+  c->last_walk.ws = (uint32_t)(&W - c->ws);
   note_use(c, ep.slot, s);   // a later commit must not overwrite this slot before the walk is done
   if (c->timing) {
     c->ev_walk.push_back(evp[0]);
@@ -1582,9 +1593,15 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
     evp[1] = c->take_event();
   }
   c->work_begin(s);
+  // these rows are the last match's: count in its walk order (the workspace
+  // holding it is then protected until this fan-out has read it)
+  const bool ord = c->last_walk.order && c->last_walk.row == d_mrow && c->last_walk.n == n;
+  MatchWs* OW = ord ? &c->ws[c->last_walk.ws] : nullptr;
+  if (OW && OW->stream && OW->stream != s && OW->ev) hipStreamWaitEvent(s, OW->ev, 0);
   e = launch_fanout(st, d_mrow, d_mids, n, nids, d_drow, d_fid, d_sub, cap, c->f_dc.as<uint32_t>(),
                     c->f_ds0.as<uint64_t>(), dpos, c->f_wbase.as<uint64_t>(), c->f_tiles.as<uint64_t>(),
-                    c->f_ovf.as<unsigned int>(), s, c->timing ? evp : nullptr);
+                    c->f_ovf.as<unsigned int>(), s, c->timing ? evp : nullptr, ord ? c->last_walk.order : nullptr);
+  if (OW) ws_done(*OW, s);
   if (c->timing) {
     c->ev_fan.push_back(evp[0]);
     c->ev_fan.push_back(evp[1]);

@@ -8,9 +8,11 @@
 
 namespace egm {
 
+constexpr int DMA_MAX_PARTS = 8;
 struct Dma {
   hsa_agent_t gpu{}, cpu{};
-  hsa_signal_t sig{};
+  hsa_signal_t sig[DMA_MAX_PARTS]{};   // one per copy, each 1 -> 0 (a profiler's copy tracer expects that)
+  int nsig = 0;
 };
 
 namespace {
@@ -53,7 +55,10 @@ Dma* dma_open(int device) {
     d = new Dma();
     d->gpu = f.gpu;
     d->cpu = f.cpu;
-    if (hsa_signal_create(0, 0, nullptr, &d->sig) != HSA_STATUS_SUCCESS) {
+    for (; d->nsig < DMA_MAX_PARTS; ++d->nsig)
+      if (hsa_signal_create(0, 0, nullptr, &d->sig[d->nsig]) != HSA_STATUS_SUCCESS) break;
+    if (d->nsig < DMA_MAX_PARTS) {
+      for (int i = 0; i < d->nsig; ++i) hsa_signal_destroy(d->sig[i]);
       delete d;
       d = nullptr;
     }
@@ -64,28 +69,29 @@ Dma* dma_open(int device) {
 
 void dma_close(Dma* d) {
   if (!d) return;
-  hsa_signal_destroy(d->sig);
+  for (int i = 0; i < d->nsig; ++i) hsa_signal_destroy(d->sig[i]);
   delete d;
   hsa_shut_down();
 }
 
 bool dma_copy_d2h(Dma* d, const DmaPart* parts, int nparts) {
+  if (nparts > DMA_MAX_PARTS) return false;
   int k = 0;
-  for (int i = 0; i < nparts; ++i) k += parts[i].bytes ? 1 : 0;
-  if (!k) return true;
-  hsa_signal_store_screlease(d->sig, k);   // each copy decrements it once
-  int issued = 0;
-  for (int i = 0; i < nparts; ++i) {
+  bool ok = true;
+  for (int i = 0; i < nparts && ok; ++i) {
     if (!parts[i].bytes) continue;
-    if (hsa_amd_memory_async_copy(parts[i].dst, d->cpu, parts[i].src, d->gpu, parts[i].bytes, 0, nullptr, d->sig) !=
-        HSA_STATUS_SUCCESS)
+    hsa_signal_store_screlease(d->sig[k], 1);
+    if (hsa_amd_memory_async_copy(parts[i].dst, d->cpu, parts[i].src, d->gpu, parts[i].bytes, 0, nullptr, d->sig[k]) !=
+        HSA_STATUS_SUCCESS) {
+      ok = false;
       break;
-    ++issued;
+    }
+    ++k;
   }
-  if (issued < k) hsa_signal_subtract_screlease(d->sig, k - issued);   // the copies never issued
-  const hsa_signal_value_t v =
-      hsa_signal_wait_scacquire(d->sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
-  return issued == k && v == 0;
+  for (int j = 0; j < k; ++j)   // every issued copy is waited for, even after a failed issue
+    ok &= hsa_signal_wait_scacquire(d->sig[j], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                    HSA_WAIT_STATE_BLOCKED) == 0;
+  return ok;
 }
 
 }  // namespace egm

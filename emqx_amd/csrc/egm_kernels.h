@@ -135,7 +135,7 @@ inline uint64_t pieces_capacity(uint64_t ids, uint32_t n) {
 // Timing hooks: when ev != nullptr, ev[0]/ev[1] bracket the walk kernel.
 hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n,
                         int mode, const MatchWork& w, const MatchOut& out, hipStream_t s,
-                        hipEvent_t* ev_walk);
+                        hipEvent_t* ev_walk, bool* walk_sorted = nullptr);   // walk_sorted: w.order holds the batch's order
 
 // Fan-out (emqx_broker:dispatch/2, emqx_broker.erl:283-324): expand each
 // topic's filter ids through the filter -> subscriber CSR.
@@ -146,6 +146,9 @@ struct SubTable {
   const uint4* rp;                // [n_fid_slots] {row start lo, hi, count, 0} (launch_sub_pairs)
 };
 hipError_t launch_sub_pairs(const uint64_t* row, uint32_t n_slots, uint4* rp, hipStream_t s);
+// walk_order (optional): the batch's walk order (sort values, topic in the low
+// 32 bits, MatchWork::order) — the count then reads the subscriber records of
+// a walk chunk's topics together (their matched filters repeat: L2 hits).
 // Scratch: wsum u32[nids/64 + 1] (window totals), dsrc u64[nids] (packed row
 // start | count), wbase u64[nids/64 + 2] (scanned window totals), dpos
 // u64[nids + 1] (each entry's first delivery: the compact form's output).
@@ -153,7 +156,7 @@ hipError_t launch_fanout(const SubTable& st, const uint64_t* match_row, const ui
                          uint32_t n, uint64_t nids, uint64_t* deliv_row, uint32_t* deliv_fid,
                          uint32_t* deliv_sub, uint64_t deliv_cap, uint32_t* wsum, uint64_t* dsrc,
                          uint64_t* dpos, uint64_t* wbase, uint64_t* tile_sums, unsigned int* overflow, hipStream_t s,
-                         hipEvent_t* ev);
+                         hipEvent_t* ev, const uint64_t* walk_order = nullptr);
 
 // Filter-shard merge: G shard CSRs of one topic batch ->
 // one CSR, per topic shard 0's ids first.  cnt is [G][n]; src[g].ids holds

@@ -22,6 +22,7 @@
 
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 
@@ -1745,7 +1746,8 @@ constexpr uint32_t SORT_MIN_TOPICS = 16384;   // below this the sort's fixed cos
 
 hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t* off, uint32_t n,
                         int mode, const MatchWork& w_in, const MatchOut& out, hipStream_t s,
-                        hipEvent_t* ev_walk) {
+                        hipEvent_t* ev_walk, bool* walk_sorted) {
+  if (walk_sorted) *walk_sorted = false;
   hipError_t e = hipMemsetAsync(w_in.stats, 0, sizeof(MatchStats), s);
   if (e != hipSuccess) return e;
   if (n == 0) {
@@ -1770,6 +1772,7 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
     e = hipcub::DeviceRadixSort::SortPairs(w.sort_tmp, tb, w.skey, w.skey_out, w.sval, w.order, (int)n,
                                            32 - (int)kbits, 32, s);
     if (e != hipSuccess) return e;
+    if (walk_sorted) *walk_sorted = true;
     trace(s, "walk order sort");
   } else {
     w.order = nullptr;
@@ -1859,6 +1862,87 @@ __global__ __launch_bounds__(256) void k_fan_count(const uint32_t* __restrict__ 
   }
 }
 
+// The same count in walk order (round 4): a wave takes 64
+// consecutive topics of the batch's walk order — topics that share their
+// first levels, so their rows repeat the same matched filters — lays their
+// rows out as one run (wave scan, owner found by a 6-step LDS search as in
+// k_compact_fix) and reads each entry's subscriber record: the repeats are L2
+// hits instead of random misses over the 1.6 GB record table.  Entries are
+// written where they are (ds0 in input order); each window's total is
+// accumulated with one atomic per run of lanes in the same window (a
+// segmented wave sum), wsum zeroed beforehand.
+constexpr int FAN_ORD_WAVES = 4;
+__global__ __launch_bounds__(64 * FAN_ORD_WAVES) void k_fan_count_ord(const uint64_t* __restrict__ order, uint32_t n,
+                                                                      const uint64_t* __restrict__ mrow,
+                                                                      const uint32_t* __restrict__ mids, uint64_t nids,
+                                                                      SubTable st, uint32_t* __restrict__ wsum,
+                                                                      uint64_t* __restrict__ ds0) {
+  constexpr uint32_t U = 4;   // entries per lane in flight
+  __shared__ uint32_t s_ex[FAN_ORD_WAVES][64];
+  __shared__ uint64_t s_r0[FAN_ORD_WAVES][64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t ngroups = (n + 63) / 64;
+  for (uint32_t g = blockIdx.x * FAN_ORD_WAVES + wave; g < ngroups; g += gridDim.x * FAN_ORD_WAVES) {
+    const uint32_t p = g * 64 + lane;
+    uint64_t r0 = 0;
+    uint32_t c = 0;
+    if (p < n) {
+      const uint32_t t = (uint32_t)order[p];
+      if (t < n) {
+        r0 = mrow[t];
+        const uint64_t r1 = mrow[t + 1];
+        c = (r1 > r0 && r1 <= nids) ? (uint32_t)(r1 - r0) : 0u;
+      }
+    }
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan(c, lane, &tot);
+    s_ex[wave][lane] = ex;
+    s_r0[wave][lane] = r0;
+    wave_sync();
+    for (uint32_t q0 = 0; q0 < tot; q0 += 64 * U) {
+      uint64_t idx[U];
+      uint32_t f[U];
+      uint4 r[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t q = min(q0 + 64 * u + lane, tot - 1);
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t b = 32; b; b >>= 1)
+          if (s_ex[wave][k + b] <= q) k += b;
+        idx[u] = s_r0[wave][k] + (q - s_ex[wave][k]);
+        f[u] = mids[idx[u]];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) r[u] = st.rp[f[u] < st.n_fid_slots ? f[u] : 0u];   // unconditional
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const bool act = q0 + 64 * u + lane < tot;
+        const bool ok = act && f[u] < st.n_fid_slots;
+        const uint32_t cu = ok ? r[u].z : 0u;
+        if (act) ds0[idx[u]] = ok ? (((uint64_t)r[u].y << 32 | r[u].x) << FAN_CNT_BITS) | min(cu, FAN_CNT_SAT) : 0ull;
+        // segmented sum over runs of lanes in one window (lanes of one row are consecutive entries)
+        const uint32_t win = act ? (uint32_t)(idx[u] >> 6) : 0xFFFFFFFFu;
+        const uint32_t prev = __shfl_up(win, 1, 64);
+        const bool head = lane == 0 || prev != win;
+        const uint64_t heads = __ballot(head);
+        uint32_t incl = cu;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(incl, d, 64);
+          if (lane >= (uint32_t)d) incl += y;
+        }
+        const uint32_t start = 63u - (uint32_t)__builtin_clzll(heads & (~0ull >> (63 - lane)));   // this run's first lane
+        const uint32_t before = __shfl(incl, (int)(start ? start - 1 : 0), 64);
+        const bool last = lane == 63 || ((heads >> (lane + 1)) & 1ull);
+        const uint32_t run = incl - (start ? before : 0u);
+        if (last && win != 0xFFFFFFFFu && run) atomicAdd(&wsum[win], run);
+      }
+    }
+    wave_sync();
+  }
+}
+
 hipError_t launch_sub_pairs(const uint64_t* row, uint32_t n_slots, uint4* rp, hipStream_t s) {
   if (n_slots) hipLaunchKernelGGL(k_sub_pairs, dim3((n_slots + 255) / 256), dim3(256), 0, s, row, n_slots, rp);
   return hipGetLastError();
@@ -1945,15 +2029,30 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
   }
 }
 
+// EGM_FAN_ORDER=input: the count in input order even when the walk order is known (A/B).
+static bool fan_count_walk_order() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("EGM_FAN_ORDER");
+    v = (e && strcmp(e, "input") == 0) ? 0 : 1;
+  }
+  return v == 1;
+}
+
 hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_t* mids, uint32_t n,
                          uint64_t nids, uint64_t* drow, uint32_t* dfid, uint32_t* dsub, uint64_t cap,
                          uint32_t* wsum, uint64_t* ds0, uint64_t* dpos, uint64_t* wbase, uint64_t* tile_sums,
-                         unsigned int* overflow, hipStream_t s, hipEvent_t* ev) {
+                         unsigned int* overflow, hipStream_t s, hipEvent_t* ev, const uint64_t* walk_order) {
   hipError_t e = hipMemsetAsync(overflow, 0, 4, s);
   if (e != hipSuccess) return e;
   if (ev) hipEventRecord(ev[0], s);
   const uint64_t nwin = (nids + 63) / 64;
-  if (nids) {
+  if (nids && walk_order && fan_count_walk_order()) {
+    if ((e = hipMemsetAsync(wsum, 0, (nwin + 1) * 4, s)) != hipSuccess) return e;
+    const uint32_t g = std::min<uint32_t>((n + 64 * FAN_ORD_WAVES - 1) / (64 * FAN_ORD_WAVES), 16384);
+    hipLaunchKernelGGL(k_fan_count_ord, dim3(g), dim3(64 * FAN_ORD_WAVES), 0, s, walk_order, n, mrow, mids, nids, st,
+                       wsum, ds0);
+  } else if (nids) {
     const uint32_t g = (uint32_t)std::min<uint64_t>((nwin + 3) / 4 + 1, 8192);
     hipLaunchKernelGGL(k_fan_count, dim3(g), dim3(256), 0, s, mids, nids, st, wsum, ds0);
   }
