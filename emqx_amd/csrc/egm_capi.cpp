@@ -1552,6 +1552,7 @@ int egm_subs_build(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint
     if (row[i + 1] < row[i]) return EGM_E_INVAL;
   const uint64_t ns = row[n_slots];
   if (ns && !subs) return EGM_E_INVAL;
+  if (ns >= (1ull << 40)) return c->fail(EGM_E_INVAL, "subscriber table: at most 2^40 entries (40-bit row starts)");
   hipError_t e;
   hipStreamSynchronize(c->stream);
   if ((e = c->sub_row.ensure(((uint64_t)n_slots + 1) * 8)) != hipSuccess) return c->hip_fail(e, "sub_row");
@@ -1561,7 +1562,8 @@ int egm_subs_build(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint
   if (ns && (e = hipMemcpy(c->sub_ids.p, subs, ns * 4, hipMemcpyHostToDevice)) != hipSuccess)
     return c->hip_fail(e, "H2D subs");
   if ((e = c->sub_rp.ensure(((uint64_t)n_slots + 1) * 16)) != hipSuccess) return c->hip_fail(e, "sub_rp");
-  if ((e = launch_sub_pairs(c->sub_row.as<uint64_t>(), n_slots, c->sub_rp.as<uint4>(), c->stream)) != hipSuccess ||
+  if ((e = launch_sub_pairs(c->sub_row.as<uint64_t>(), c->sub_ids.as<uint32_t>(), n_slots, c->sub_rp.as<uint4>(),
+                            c->stream)) != hipSuccess ||
       (e = hipStreamSynchronize(c->stream)) != hipSuccess)
     return c->hip_fail(e, "sub pairs");
   c->n_fid_slots = n_slots;
@@ -1580,7 +1582,7 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   if (nids > mids_len) return c->fail(EGM_E_OVERFLOW, "match row total exceeds the id buffer (overflowed match batch)");
   const uint64_t nwin = (nids + 63) / 64;
   if ((e = c->f_dc.ensure((nwin + 1) * 4)) != hipSuccess) return c->hip_fail(e, "f_dc");   // window totals
-  if ((e = c->f_ds0.ensure((nids + 1) * 8)) != hipSuccess) return c->hip_fail(e, "f_ds0");
+  if ((e = c->f_ds0.ensure((nids + 1) * 16)) != hipSuccess) return c->hip_fail(e, "f_ds0");   // entry records
   if ((e = c->f_wbase.ensure((nwin + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_wbase");
   if (!d_entry_pos && (e = c->f_dpos.ensure((nids + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_dpos");
   uint64_t* dpos = d_entry_pos ? d_entry_pos : c->f_dpos.as<uint64_t>();   // the caller's, in the compact form
@@ -1599,7 +1601,7 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   MatchWs* OW = ord ? &c->ws[c->last_walk.ws] : nullptr;
   if (OW && OW->stream && OW->stream != s && OW->ev) hipStreamWaitEvent(s, OW->ev, 0);
   e = launch_fanout(st, d_mrow, d_mids, n, nids, d_drow, d_fid, d_sub, cap, c->f_dc.as<uint32_t>(),
-                    c->f_ds0.as<uint64_t>(), dpos, c->f_wbase.as<uint64_t>(), c->f_tiles.as<uint64_t>(),
+                    c->f_ds0.as<uint4>(), dpos, c->f_wbase.as<uint64_t>(), c->f_tiles.as<uint64_t>(),
                     c->f_ovf.as<unsigned int>(), s, c->timing ? evp : nullptr, ord ? c->last_walk.order : nullptr);
   if (OW) ws_done(*OW, s);
   if (c->timing) {

@@ -143,18 +143,19 @@ struct SubTable {
   const uint64_t* row;            // [n_fid_slots + 1] indexed by filter id
   const uint32_t* subs;           // subscriber ids; bit 31 set = shared group id
   uint32_t n_fid_slots;
-  const uint4* rp;                // [n_fid_slots] {row start lo, hi, count, 0} (launch_sub_pairs)
+  const uint4* rp;                // [n_fid_slots] subscriber records (launch_sub_pairs, egm_kernels.hip)
 };
-hipError_t launch_sub_pairs(const uint64_t* row, uint32_t n_slots, uint4* rp, hipStream_t s);
+hipError_t launch_sub_pairs(const uint64_t* row, const uint32_t* subs, uint32_t n_slots, uint4* rp, hipStream_t s);
 // walk_order (optional): the batch's walk order (sort values, topic in the low
 // 32 bits, MatchWork::order) — the count then reads the subscriber records of
 // a walk chunk's topics together (their matched filters repeat: L2 hits).
-// Scratch: wsum u32[nids/64 + 1] (window totals), dsrc u64[nids] (packed row
+// Scratch: wsum u32[nids/64 + 1] (window totals), dsrc 16 B [nids] (each entry's subscriber record:
+// packed row
 // start | count), wbase u64[nids/64 + 2] (scanned window totals), dpos
 // u64[nids + 1] (each entry's first delivery: the compact form's output).
 hipError_t launch_fanout(const SubTable& st, const uint64_t* match_row, const uint32_t* match_ids,
                          uint32_t n, uint64_t nids, uint64_t* deliv_row, uint32_t* deliv_fid,
-                         uint32_t* deliv_sub, uint64_t deliv_cap, uint32_t* wsum, uint64_t* dsrc,
+                         uint32_t* deliv_sub, uint64_t deliv_cap, uint32_t* wsum, uint4* dsrc,
                          uint64_t* dpos, uint64_t* wbase, uint64_t* tile_sums, unsigned int* overflow, hipStream_t s,
                          hipEvent_t* ev, const uint64_t* walk_order = nullptr);
 

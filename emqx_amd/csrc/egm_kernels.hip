@@ -1812,30 +1812,42 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
 // match entries, whose deliveries are contiguous in the output (the scan), and
 // its lanes write them in order — coalesced stores, and a 2 000-subscriber
 // filter is spread over 64 lanes instead of looping in one.
-// One aligned 16-B record per filter {row start lo, hi, subscriber count, 0}
-// (k_sub_pairs, at egm_subs_build): a matched id costs one line request
-// instead of two 8-B row-pointer reads; four ids per thread in flight.
-__global__ __launch_bounds__(256) void k_sub_pairs(const uint64_t* __restrict__ row, uint32_t n_slots,
-                                                   uint4* __restrict__ rp) {
+// One aligned 16-B record per filter (k_sub_pairs, at egm_subs_build):
+//   y = subscriber count (24 bits, saturated) << 8 | row start bits 32-39
+//   z, w = its first two subscriber ids (when it has them)
+//   x = row start bits 0-31, or — a row of at most 3 — its third subscriber
+// A matched id costs the count pass one line request, and — round 4 — the
+// fill reads no subscriber row at all for a filter of up to three
+// subscribers (C4: 92 % of filters; the record travels to the fill as the
+// entry's 16-B dsrc): the fill's random row reads were a 64-B line per
+// entry for ~14 B of subscribers.
+constexpr uint32_t FAN_CNT_BITS = 24;
+constexpr uint32_t FAN_CNT_SAT = (1u << FAN_CNT_BITS) - 1;   // saturated: the fill reads the exact count from row[]
+constexpr uint32_t FAN_INLINE_ALL = 3;   // a row this short is carried whole in its record
+__device__ __forceinline__ uint64_t rec_start(uint4 r) { return (uint64_t)r.x | ((uint64_t)(r.y & 0xFFu) << 32); }
+__device__ __forceinline__ uint32_t rec_count(uint4 r) { return r.y >> 8; }
+
+__global__ __launch_bounds__(256) void k_sub_pairs(const uint64_t* __restrict__ row, const uint32_t* __restrict__ subs,
+                                                   uint32_t n_slots, uint4* __restrict__ rp) {
   const uint32_t f = blockIdx.x * 256 + threadIdx.x;
   if (f < n_slots) {
-    const uint64_t r0 = row[f], r1 = row[f + 1];
-    rp[f] = make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)(r1 - r0), 0u);
+    const uint64_t r0 = row[f], r1 = row[f + 1], c = r1 - r0;
+    const uint32_t cs = (uint32_t)min(c, (uint64_t)FAN_CNT_SAT);
+    const uint32_t x = c <= FAN_INLINE_ALL ? (c > 2 ? subs[r0 + 2] : 0u) : (uint32_t)r0;
+    rp[f] = make_uint4(x, ((uint32_t)(r0 >> 32) & 0xFFu) | (cs << 8), c > 0 ? subs[r0] : 0u, c > 1 ? subs[r0 + 1] : 0u);
   }
 }
 
-// Round 4: the count kernel writes one packed record per
-// match entry {subscriber row start:40 | count:24} and one subscriber total per
-// window of 64 entries; the window totals are scanned (nids/64 of them), and
-// the fill derives each entry's delivery offset with a wave scan inside its
+// Round 4: the count kernel copies each match entry's
+// filter record (above) to ds0 and writes one subscriber total per window
+// of 64 entries; the window totals are scanned (nids/64 of them), and the
+// fill derives each entry's delivery offset with a wave scan inside its
 // window.  Round 3 wrote a count AND a start per entry and scanned all nids
 // counts into u64 offsets before the fill read them back (~8.8 GB of
 // intermediate traffic at C4, ~4.3 ms of scans).
-constexpr uint32_t FAN_CNT_BITS = 24;
-constexpr uint32_t FAN_CNT_SAT = (1u << FAN_CNT_BITS) - 1;   // saturated: the fill re-reads the row record
 __global__ __launch_bounds__(256) void k_fan_count(const uint32_t* __restrict__ mids, uint64_t nids,
                                                    SubTable st, uint32_t* __restrict__ wsum,
-                                                   uint64_t* __restrict__ ds0) {
+                                                   uint4* __restrict__ ds0) {
   constexpr uint32_t U = 4;   // windows per wave in flight
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t nwin = (nids + 63) / 64;
@@ -1851,9 +1863,9 @@ __global__ __launch_bounds__(256) void k_fan_count(const uint32_t* __restrict__ 
     for (uint32_t u = 0; u < U; ++u) {
       const uint64_t w = w0 + u * wstride, i = w * 64 + lane;
       const bool ok = i < nids && f[u] < st.n_fid_slots;
-      const uint32_t c = ok ? r[u].z : 0u;
-      if (i < nids)
-        ds0[i] = ok ? (((uint64_t)r[u].y << 32 | r[u].x) << FAN_CNT_BITS) | min(c, FAN_CNT_SAT) : 0ull;
+      const uint32_t cs = ok ? rec_count(r[u]) : 0u;
+      const uint32_t c = cs == FAN_CNT_SAT ? (uint32_t)min(st.row[f[u] + 1] - st.row[f[u]], (uint64_t)0xFFFFFFFFu) : cs;
+      if (i < nids) ds0[i] = ok ? r[u] : make_uint4(0, 0, 0, 0);
       uint32_t sum = c;
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
@@ -1876,7 +1888,7 @@ __global__ __launch_bounds__(64 * FAN_ORD_WAVES) void k_fan_count_ord(const uint
                                                                       const uint64_t* __restrict__ mrow,
                                                                       const uint32_t* __restrict__ mids, uint64_t nids,
                                                                       SubTable st, uint32_t* __restrict__ wsum,
-                                                                      uint64_t* __restrict__ ds0) {
+                                                                      uint4* __restrict__ ds0) {
   constexpr uint32_t U = 4;   // entries per lane in flight
   __shared__ uint32_t s_ex[FAN_ORD_WAVES][64];
   __shared__ uint64_t s_r0[FAN_ORD_WAVES][64];
@@ -1919,8 +1931,10 @@ __global__ __launch_bounds__(64 * FAN_ORD_WAVES) void k_fan_count_ord(const uint
       for (uint32_t u = 0; u < U; ++u) {
         const bool act = q0 + 64 * u + lane < tot;
         const bool ok = act && f[u] < st.n_fid_slots;
-        const uint32_t cu = ok ? r[u].z : 0u;
-        if (act) ds0[idx[u]] = ok ? (((uint64_t)r[u].y << 32 | r[u].x) << FAN_CNT_BITS) | min(cu, FAN_CNT_SAT) : 0ull;
+        const uint32_t cs = ok ? rec_count(r[u]) : 0u;
+        const uint32_t cu =
+            cs == FAN_CNT_SAT ? (uint32_t)min(st.row[f[u] + 1] - st.row[f[u]], (uint64_t)0xFFFFFFFFu) : cs;
+        if (act) ds0[idx[u]] = ok ? r[u] : make_uint4(0, 0, 0, 0);
         // segmented sum over runs of lanes in one window (lanes of one row are consecutive entries)
         const uint32_t win = act ? (uint32_t)(idx[u] >> 6) : 0xFFFFFFFFu;
         const uint32_t prev = __shfl_up(win, 1, 64);
@@ -1943,8 +1957,8 @@ __global__ __launch_bounds__(64 * FAN_ORD_WAVES) void k_fan_count_ord(const uint
   }
 }
 
-hipError_t launch_sub_pairs(const uint64_t* row, uint32_t n_slots, uint4* rp, hipStream_t s) {
-  if (n_slots) hipLaunchKernelGGL(k_sub_pairs, dim3((n_slots + 255) / 256), dim3(256), 0, s, row, n_slots, rp);
+hipError_t launch_sub_pairs(const uint64_t* row, const uint32_t* subs, uint32_t n_slots, uint4* rp, hipStream_t s) {
+  if (n_slots) hipLaunchKernelGGL(k_sub_pairs, dim3((n_slots + 255) / 256), dim3(256), 0, s, row, subs, n_slots, rp);
   return hipGetLastError();
 }
 
@@ -1960,11 +1974,13 @@ constexpr uint32_t FAN_BIG = 128;   // entries with this many subscribers are co
 // the entry offsets (dpos, the compact form's output and the rows' source)
 // come from the window's scanned total plus a wave scan of the entries'
 // counts; then small rows are written lane per delivery (owner found by a
-// 6-step LDS search) and big rows streamed by the whole wave.  An overflowed
-// batch (total > cap) still gets its offsets, so the caller learns the size.
+// 6-step LDS search; a row's first two subscribers come with its record, the
+// rest from the subscriber table) and big rows streamed by the whole wave.
+// An overflowed batch (total > cap) still gets its offsets, so the caller
+// learns the size.
 __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __restrict__ mids, uint64_t nids,
                                                              SubTable st, const uint64_t* __restrict__ wbase,
-                                                             const uint64_t* __restrict__ ds0,
+                                                             const uint4* __restrict__ ds0,
                                                              uint64_t* __restrict__ dpos,
                                                              uint32_t* __restrict__ dfid, uint32_t* __restrict__ dsub,
                                                              uint64_t cap, unsigned int* overflow) {
@@ -1972,15 +1988,17 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
   const bool ovf = wbase[nwin] > cap;
   if (ovf && blockIdx.x == 0 && threadIdx.x == 0) *overflow = 1u;
   __shared__ uint32_t s_pre[FAN_WAVES][64], s_off[FAN_WAVES][64], s_fid[FAN_WAVES][64], s_cnt[FAN_WAVES][64];
+  __shared__ uint32_t s_in0[FAN_WAVES][64], s_in1[FAN_WAVES][64], s_in2[FAN_WAVES][64];
   __shared__ uint64_t s_src[FAN_WAVES][64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (uint64_t w = (uint64_t)blockIdx.x * FAN_WAVES + wave; w < nwin; w += (uint64_t)gridDim.x * FAN_WAVES) {
     const uint64_t w0 = w * 64, i = w0 + lane, ic = min(i, nids - 1);
     const uint64_t base = wbase[w];
-    const uint64_t v = ds0[ic];
+    const uint4 v = ds0[ic];
     const uint32_t f = mids[ic];
-    uint32_t c = i < nids ? (uint32_t)(v & FAN_CNT_SAT) : 0u;
-    if (c == FAN_CNT_SAT) c = st.rp[f].z;   // a row of 2^24 or more subscribers (rare): its exact count
+    uint32_t c = i < nids ? rec_count(v) : 0u;
+    if (c == FAN_CNT_SAT)   // a row of 2^24 or more subscribers (rare): its exact count
+      c = (uint32_t)min(st.row[f + 1] - st.row[f], (uint64_t)0xFFFFFFFFu);
     uint32_t tot;
     const uint32_t off = wave_excl_scan(c, lane, &tot);
     if (i < nids) dpos[i] = base + off;
@@ -1993,7 +2011,10 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
     s_off[wave][lane] = off;
     s_fid[wave][lane] = f;
     s_cnt[wave][lane] = c;
-    s_src[wave][lane] = v >> FAN_CNT_BITS;
+    s_src[wave][lane] = rec_start(v);   // (meaningful only past FAN_INLINE_ALL subscribers)
+    s_in0[wave][lane] = v.z;
+    s_in1[wave][lane] = v.w;
+    s_in2[wave][lane] = v.x;
     wave_sync();
     // small entries: lane per delivery, the owning entry found by a 6-step search
     for (uint32_t q = lane; q < tot_s; q += 64) {
@@ -2006,7 +2027,11 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
       const uint32_t o = q - s_pre[wave][k];
       const uint64_t d = base + s_off[wave][k] + o;
       if (dfid) dfid[d] = s_fid[wave][k];   // null: the compact form (the entry offsets give the filter)
-      dsub[d] = st.subs[s_src[wave][k] + o];
+      const uint32_t inl = s_cnt[wave][k] <= FAN_INLINE_ALL ? FAN_INLINE_ALL : 2u;   // subscribers in the record
+      uint32_t sub;
+      if (o >= inl) sub = st.subs[s_src[wave][k] + o];   // only these lanes read the table
+      else sub = o == 0 ? s_in0[wave][k] : (o == 1 ? s_in1[wave][k] : s_in2[wave][k]);
+      dsub[d] = sub;
     }
     // big entries (C4: 2 000-subscriber filters): the wave streams the row, 4 per lane in flight
     for (uint64_t mb = __ballot(big); mb; mb &= mb - 1) {
@@ -2029,19 +2054,17 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
   }
 }
 
-// EGM_FAN_ORDER=input: the count in input order even when the walk order is known (A/B).
+// EGM_FAN_ORDER=walk: the count in the match's walk order when it is known
+// (A/B: no faster at C4, 5.79 vs 5.77 ms — a chunk's topics share few matched
+// filters there; profiles/r4_c4_fan_order_ab.jsonl).  Read at each launch.
 static bool fan_count_walk_order() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("EGM_FAN_ORDER");
-    v = (e && strcmp(e, "input") == 0) ? 0 : 1;
-  }
-  return v == 1;
+  const char* e = getenv("EGM_FAN_ORDER");
+  return e && strcmp(e, "walk") == 0;
 }
 
 hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_t* mids, uint32_t n,
                          uint64_t nids, uint64_t* drow, uint32_t* dfid, uint32_t* dsub, uint64_t cap,
-                         uint32_t* wsum, uint64_t* ds0, uint64_t* dpos, uint64_t* wbase, uint64_t* tile_sums,
+                         uint32_t* wsum, uint4* ds0, uint64_t* dpos, uint64_t* wbase, uint64_t* tile_sums,
                          unsigned int* overflow, hipStream_t s, hipEvent_t* ev, const uint64_t* walk_order) {
   hipError_t e = hipMemsetAsync(overflow, 0, 4, s);
   if (e != hipSuccess) return e;

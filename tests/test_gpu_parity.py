@@ -440,11 +440,12 @@ def test_fanout_device_exact_and_guarded(gm, monkeypatch, walk_sorted):
     """Device fan-out (the bench's C4 step) element-for-element against numpy,
     with 1% of filters at 2 000 subscribers (windows of one wave spanning
     thousands of deliveries); an overflowed match batch is refused, not read.
-    walk_sorted: the match sorts its batch (forced on this small table), so
-    the fan-out counts in the match's walk order (k_fan_count_ord)."""
+    walk_sorted: the match sorts its batch (forced on this small table) and
+    the fan-out counts in the match's walk order (k_fan_count_ord, A/B)."""
     import torch
     if walk_sorted:
         monkeypatch.setenv("EGM_WALK_SORT_MIN_BYTES", "0")
+        monkeypatch.setenv("EGM_FAN_ORDER", "walk")
     f, t = synth.config("c1", n_filters=50_000, n_topics=30_000)
     gm.build(f.blob, f.off)
     srow, subs = synth.subscribers(f.n, p_big=0.01, n_big=2000, p_share=0.1)
