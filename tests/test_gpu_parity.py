@@ -516,7 +516,10 @@ def test_full_size_c1_properties(gm):
     a = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
     b2 = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
     assert np.array_equal(a.row_ptr, b2.row_ptr)
-    assert np.array_equal(canonical(a.row_ptr, a.ids), canonical(b2.row_ptr, b2.ids))
+    # every row the same set in both runs: a per-row order-independent checksum
+    # (the whole-batch canonical sort of 180M ids took ~20 s of the suite's budget)
+    from tests.test_gpu_scale import row_checksums
+    assert np.array_equal(row_checksums(a.row_ptr, a.ids), row_checksums(b2.row_ptr, b2.ids))
     o = OracleTrie(True, 1)
     o.add(f.blob, f.off)
     rng = np.random.default_rng(5)
