@@ -48,6 +48,7 @@ run() {
 for step in "$@"; do
   case $step in
     tests) run tests 900 python -u -m pytest tests -m "gpu and not slow" -x -v --timeout 300 --timeout-method thread ;;
+    gpuall) run gpuall 1150 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread --durations=15 ;;   # the driver's whole GPU tier
     scale) run scale 1100 python -u -m pytest tests -m "gpu and slow" -x -v --timeout 600 --timeout-method thread ;;
     bench) run bench 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o run --output-format csv -- $B --steps 20 --warmup 5 --host-e2e off --pipelined off ;;
     drv) run drv 600 python $R/bench.py --gpus 1 --steps 20 --warmup 5 ;;
@@ -104,6 +105,7 @@ for step in "$@"; do
       run walkmix2 300 "$R/tools/walkmix" 2 ;;
     d2h)   # device <-> pinned host copy rates (tools/d2hbench.hip)
       run d2h 120 "$R/tools/d2hbench" ;;
+    bench_c4_in) EGM_FAN_ORDER=input run bench_c4_in 900 python $R/bench.py --config c4 --steps 10 --warmup 2 --host-e2e off --pipelined off --cpu-baseline off ;;   # A/B: fan-out count in input order
     c4m) run c4m 400 python $R/bench.py --config c4 --filters 10000000 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
     c4m_*)  # the same on variant V (tools/build_variant.py)
       v=${step#c4m_}
