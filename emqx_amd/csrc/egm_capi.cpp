@@ -242,13 +242,15 @@ struct egm_ctx {
   // waits for the last launch that used them (one event, recorded after each).
   hipEvent_t work_ev = nullptr;
   hipStream_t work_stream = nullptr;
+  bool work_used = false;   // (the null stream is a stream: work_stream may be 0 after a launch)
   void work_begin(hipStream_t s) {
-    if (work_stream && work_stream != s && work_ev) hipStreamWaitEvent(s, work_ev, 0);
+    if (work_used && work_stream != s && work_ev) hipStreamWaitEvent(s, work_ev, 0);
   }
   void work_end(hipStream_t s) {
     if (!work_ev && hipEventCreateWithFlags(&work_ev, hipEventDisableTiming) != hipSuccess) work_ev = nullptr;
     if (work_ev) hipEventRecord(work_ev, s);
     work_stream = s;
+    work_used = true;
   }
   // host pipeline (egm_match_submit / egm_match_wait)
   std::vector<std::unique_ptr<PipeSlot>> pipe;
@@ -615,7 +617,7 @@ static MatchWs& pick_ws(egm_ctx* c, hipStream_t s) {
     if (c->ws[i].used < c->ws[k].used) k = i;
   }
   MatchWs& W = c->ws[k];
-  if (W.stream && W.stream != s && W.ev) hipStreamWaitEvent(s, W.ev, 0);
+  if (W.used && W.stream != s && W.ev) hipStreamWaitEvent(s, W.ev, 0);   // (stream 0 is a stream too)
   c->cur_ws = k;
   W.used = ++c->ws_clock;
   return W;
@@ -986,7 +988,7 @@ int egm_match_device(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, con
   if (n && (!d_blob || !d_off || ((uintptr_t)d_blob & 3))) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipStream_t s = (hipStream_t)hip_stream;   // NULL: the HIP default (null) stream, as the caller's own work
   // a topic has at most (its bytes + 1) levels, and a legal one at most 65 536
   // (emqx_topic.erl:45, 99-100): bound the device batch's depth by its blob
   MatchWs& W = pick_ws(c, s);
@@ -1009,7 +1011,7 @@ int egm_match_device_counted(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_by
   if (n_max && (!d_blob || !d_off || ((uintptr_t)d_blob & 3))) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipStream_t s = (hipStream_t)hip_stream;   // NULL: the HIP default (null) stream, as the caller's own work
   MatchWs& W = pick_ws(c, s);
   int r = ensure_work(c, W, n_max, blob_bytes, ids_cap, std::min<uint64_t>(blob_bytes, 65535) + 1);
   if (r) return r;
@@ -1630,7 +1632,7 @@ int egm_fanout_device(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   if (!c || !d_mrow || !d_drow) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipStream_t s = (hipStream_t)hip_stream;   // NULL: the HIP default (null) stream, as the caller's own work
   return run_fanout(c, d_mrow, d_mids, mids_len, n, s, d_drow, d_fid, d_sub, cap, nullptr);
 }
 
@@ -1640,7 +1642,7 @@ int egm_fanout_device_compact(egm_ctx* c, const uint64_t* d_mrow, const uint32_t
   if (!c || !d_mrow || !d_drow || !d_entry_pos) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipStream_t s = (hipStream_t)hip_stream;   // NULL: the HIP default (null) stream, as the caller's own work
   return run_fanout(c, d_mrow, d_mids, mids_len, n, s, d_drow, nullptr, d_sub, cap, nullptr, d_entry_pos);
 }
 
@@ -1705,7 +1707,7 @@ int egm_shard_merge(egm_ctx* c, uint32_t n_shards, uint32_t n, const uint32_t* d
     if (!d_shard_ids[g] && total_ids) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipStream_t s = (hipStream_t)hip_stream;   // NULL: the HIP default (null) stream, as the caller's own work
   hipError_t e;
   const uint64_t nn = (uint64_t)n + 1;
   if ((e = c->m_srow.ensure(nn * n_shards * 8)) != hipSuccess) return c->hip_fail(e, "merge srow");
@@ -1866,7 +1868,7 @@ int egm_prefix_route(egm_ctx* c, const uint8_t* d_blob, const uint32_t* d_off, u
     return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipStream_t s = (hipStream_t)hip_stream;   // NULL: the HIP default (null) stream, as the caller's own work
   hipError_t e;
   if ((e = c->p_ctr.ensure(8 * PREFIX_RANKS_MAX)) != hipSuccess) return c->hip_fail(e, "prefix counters");
   if ((e = c->p_dst.ensure(8ull * std::max<uint32_t>(n, 1))) != hipSuccess) return c->hip_fail(e, "prefix routes");

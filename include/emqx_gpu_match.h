@@ -24,10 +24,12 @@
  * duration of the call; results are library-allocated and released with
  * egm_result_free().  One context = one HIP device; calls on a context are
  * serialised internally (a dirty-scheduler NIF may call from any thread).
- * The device entry points may be given any HIP stream: launches that share
- * the context's workspaces are ordered across streams by the library (a
- * launch on a new stream waits for the previous one), and a table commit
- * waits for every launch still reading the epoch it overwrites.
+ * The device entry points may be given any HIP stream — NULL is the HIP
+ * default (null) stream, ordered with the caller's own work there (e.g. a
+ * PyTorch default-stream tensor fill), never a stream of the library's own:
+ * launches that share the context's workspaces are ordered across streams by
+ * the library (a launch on a new stream waits for the previous one), and a
+ * table commit waits for every launch still reading the epoch it overwrites.
  * Table changes are all-or-nothing: a delta or build with an invalid id
  * leaves the staged table unchanged.
  */
@@ -171,7 +173,7 @@ int egm_match_cancel(egm_ctx* ctx, uint64_t ticket);
 /* Device-resident variant: d_blob (4-byte aligned, blob_bytes >= d_offsets[n])
    and d_offsets are device pointers (d_offsets[0] == 0); results stay in device buffers owned by the caller
    (d_row_ptr[n+1], d_ids[ids_cap], d_flags[n] may be NULL).  Asynchronous on
-   `hip_stream` (NULL = the context's stream).  After the stream completes,
+   `hip_stream` (NULL = the HIP default stream).  After the stream completes,
    d_row_ptr[n] holds the number of ids; egm_last_stats() reports overflow. */
 int egm_match_device(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_offsets,
                      uint32_t n_topics, int mode, void* hip_stream, uint64_t* d_row_ptr, uint32_t* d_ids,
@@ -252,7 +254,7 @@ int egm_last_fanout(egm_ctx* ctx, uint64_t* n_deliveries, uint32_t* overflow);
    d_counts: device [n_shards][n] per-topic counts; d_shard_ids: host array of
    n_shards (<= 16) device pointers (shard g's ids back to back, topic order);
    total_ids: the sum of all counts (EGM_E_OVERFLOW if > ids_cap).
-   Asynchronous on hip_stream (NULL = the context's stream). */
+   Asynchronous on hip_stream (NULL = the HIP default stream). */
 int egm_shard_merge(egm_ctx* ctx, uint32_t n_shards, uint32_t n_topics, const uint32_t* d_counts,
                     const uint32_t* const* d_shard_ids, uint64_t total_ids, void* hip_stream, uint64_t* d_row_ptr,
                     uint32_t* d_ids, uint64_t ids_cap);

@@ -461,7 +461,7 @@ def test_fanout_device_exact_and_guarded(gm, monkeypatch, walk_sorted):
     d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
     gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES, s,
                     d_row.data_ptr(), d_ids.data_ptr(), cap)
-    torch.cuda.synchronize()   # stream 0 means "the context's stream" at the C-ABI: wait for every stream
+    torch.cuda.synchronize()
     mrow = d_row.cpu().numpy().view(np.uint64)
     mids = d_ids.cpu().numpy().view(np.uint32)[: int(mrow[-1])]
     assert np.array_equal(mrow, host.row_ptr), (int(mrow[-1]), len(host.ids), gm.last_stats())

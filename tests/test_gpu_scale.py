@@ -128,6 +128,8 @@ class TestC2Full:
                            ps.cap_topics, ps.cap_bytes, s, send.data_ptr())
             sends.append(send)
         torch.cuda.synchronize()
+        # the slots as routed: any later change to a send buffer is a device-memory corruption
+        snap = [x.cpu().numpy() for x in sends]
         got_tot = np.full(t.n, -1, np.int64)
         got_sum = np.zeros(t.n, np.uint64)
         sizes = []
@@ -140,6 +142,13 @@ class TestC2Full:
                 del part
                 recv = torch.cat([sends[r][q * ps.slot_bytes:(q + 1) * ps.slot_bytes] for r in range(G)])
                 host = recv.cpu().numpy()
+                for r in range(G):
+                    a = snap[r][q * ps.slot_bytes:(q + 1) * ps.slot_bytes]
+                    b = host[r * ps.slot_bytes:(r + 1) * ps.slot_bytes]
+                    if not np.array_equal(a, b):
+                        d = np.nonzero(a != b)[0]
+                        raise AssertionError(("send buffer changed after routing", q, r, len(d), d[:8].tolist(),
+                                              a[d[:8]].tolist(), b[d[:8]].tolist()))
                 row = torch.zeros(ps.cap_topics + 1, dtype=torch.int64, device=dev)
                 ids = torch.zeros(ps.cap_topics * 96 + 4096, dtype=torch.int32, device=dev)
                 for r in range(G):
@@ -154,7 +163,12 @@ class TestC2Full:
                     rown = row.cpu().numpy().view(np.uint64)
                     assert np.all(rown[cnt:] == rown[cnt])   # padding: empty rows
                     gidx = parts[r][0] + tids.astype(np.int64)
-                    assert np.all(got_tot[gidx] < 0)          # matched on exactly one rank
+                    seen = np.nonzero(got_tot[gidx] >= 0)[0]
+                    assert len(seen) == 0, ("topic matched on two ranks", q, r, cnt, nb, len(tids), len(seen),
+                                            seen[:5].tolist(), tids[seen[:5]].tolist(),
+                                            int(tids.min()) if len(tids) else None,
+                                            int(tids.max()) if len(tids) else None,
+                                            parts[r], int(len(np.unique(tids))))   # matched on exactly one rank
                     got_tot[gidx] = np.diff(rown[:cnt + 1]).astype(np.int64)
                     got_sum[gidx] = row_checksums(rown[:cnt + 1], ids[:int(rown[cnt])].cpu().numpy().view(np.uint32))
         finally:
