@@ -118,6 +118,9 @@ for step in "$@"; do
     tests_*)   # the fast GPU tests on variant V
       v=${step#tests_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 900 python -u -m pytest tests -m "gpu and not slow" -x -v --timeout 300 --timeout-method thread ;;
+    abx_*)   # A/B variant, second sample (own log/prof names)
+      v=${step#abx_}
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "abx_$v" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_profx_$v" -o run --output-format csv -- $B --steps 10 --warmup 2 --cpu-baseline off --host-e2e off ;;
     ab_*)   # A/B variant built by tools/build_variant.py: C2 bench under rocprof stats
       v=${step#ab_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$v" -o run --output-format csv -- $B --steps 10 --warmup 2 --cpu-baseline off --host-e2e off ;;
