@@ -562,6 +562,9 @@ __device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, 
   return r;
 }
 
+#ifndef EGM_FLUSH_NT
+#define EGM_FLUSH_NT 1   // flush stores with the nontemporal hint (A/B: profiles/r4_walk_ab.jsonl, nts)
+#endif
 #if EGM_FLUSH_V2 == 2
 // Write the stage out, topic-ordered (round 4, the default).  The ranks come from
 // an LDS atomic on the topic's flush counter, as in the arrival-order flush,
@@ -627,7 +630,11 @@ __device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t t0
 #ifdef EGM_AB_NO_ID_STORES   // measurement only (tools/build_variant.py): the walk without its id stores
     if (L.stage_fid[q] != 0x7FFFFFF1u) continue;
 #endif
+#if EGM_FLUSH_NT   // streaming stores: the id blocks do not displace table lines from L2 (9.78 -> 9.62 ms)
+    __builtin_nontemporal_store(L.stage_fid[q], &w.ids_fix[blk + L.stage_rank[q]]);
+#else
     w.ids_fix[blk + L.stage_rank[q]] = L.stage_fid[q];
+#endif
   }
   wave_sync();
   L.cnt[lane] += fl;
