@@ -111,6 +111,9 @@ for step in "$@"; do
     c4m_*)  # the same on variant V (tools/build_variant.py)
       v=${step#c4m_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 400 python $R/bench.py --config c4 --filters 10000000 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
+    c4_*)   # full C4 (100M filters, match + fan-out) on variant V
+      v=${step#c4_}
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 900 python $R/bench.py --config c4 --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
     c3_*)   # C3 on variant V (tools/build_variant.py)
       v=${step#c3_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 python $R/bench.py --config c3 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
