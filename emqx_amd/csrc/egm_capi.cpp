@@ -580,11 +580,14 @@ static int commit_locked(egm_ctx* c, uint64_t* epoch) {
 
 // Walk order: the sort key's bits per level as hex nibbles,
 // level 0 in the lowest; 0 walks in input order.  EGM_WALK_KEY is a tuning
-// knob for A/B runs (read at every batch); the default is the measured best.
+// knob for A/B runs (read at every batch); the default is the measured best:
+// 6/8/10/8 bits over four levels (round 4 with the v3 flush, one process:
+// 11.94-11.97 ms per C2 step against 12.03-12.06 for round 3's 6/8/10;
+// profiles/r4_walk_key_ab.jsonl).
 static uint32_t walk_key_shape() {
   const char* v = getenv("EGM_WALK_KEY");
-  const uint32_t shape = (v && *v) ? (uint32_t)strtoul(v, nullptr, 16) & 0xFFFFu : 0xa86u;   // KEY_LEVELS nibbles
-  return walk_key_bits(shape) <= 32 ? shape : 0xa86u;
+  const uint32_t shape = (v && *v) ? (uint32_t)strtoul(v, nullptr, 16) & 0xFFFFu : 0x8a86u;   // KEY_LEVELS nibbles
+  return walk_key_bits(shape) <= 32 ? shape : 0x8a86u;
 }
 
 // EGM_WALK_SORT_MIN_BYTES: tables smaller than this are walked in input order.
