@@ -49,6 +49,7 @@ for step in "$@"; do
   case $step in
     tests) run tests 900 python -u -m pytest tests -m "gpu and not slow" -x -v --timeout 300 --timeout-method thread ;;
     prefixdiag) run prefixdiag 1150 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread -k "not slow or eight_prefix" ;;
+    slowrest) run slowrest 900 python -u -m pytest tests -m "gpu and slow" -x -q --timeout 600 --timeout-method thread -k "not TestC2Full" ;;
     c2full) run c2full 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -k TestC2Full ;;
     gpuall) run gpuall 1150 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread --durations=15 ;;   # the driver's whole GPU tier
     scale) run scale 1100 python -u -m pytest tests -m "gpu and slow" -x -v --timeout 600 --timeout-method thread ;;
