@@ -37,7 +37,8 @@
 %% destructor cancels it (egm_match_cancel) and the slot is reclaimed.
 %%
 %% Not compiled in this repository's CI (no ERTS in the build image);
-%% emqx_amd/gpu_batch.py mirrors this logic and is tested.
+%% emqx_amd/gpu_batch.py mirrors this logic and is tested, and
+%% tests/test_erl_lint.py checks this module against the reference's erl_opts.
 %%--------------------------------------------------------------------
 -module(emqx_gpu_batch).
 -behaviour(gen_server).
@@ -132,7 +133,7 @@ next(St = #st{waiters = W, depth = D, queue = Q}) ->
 
 %% Submit one committed batch and start its (monitored) waiter.  The overlay
 %% is read before the submit (emqx_gpu_routes, step 2).
-submit(Items, St = #st{ctx = Ctx, waiters = W}) ->
+submit(Items, St) ->
     Topics = [T || {_From, T} <- Items],
     case emqx_gpu_routes:overlay() of
         {ok, Ov} -> submit(Items, Topics, Ov, St);

@@ -55,7 +55,9 @@
 -module(emqx_gpu_routes).
 -behaviour(gen_server).
 
--include("emqx.hrl").   %% ?ROUTE_TAB (apps/emqx/include/emqx.hrl)
+%% The route table's name.  emqx_router defines it privately
+%% (apps/emqx/src/emqx_router.erl:70), not in apps/emqx/include/emqx.hrl.
+-define(ROUTE_TAB, emqx_route).
 
 -export([start_link/1, flush/0, with_pending/2, overlay/0]).
 -export([init/1, handle_call/3, handle_cast/2, handle_info/2, terminate/2]).
