@@ -333,7 +333,7 @@ class PrefixLeg:
         import torch
         import torch.distributed as dist
         from emqx_amd import _lib as L
-        from emqx_amd.dist import PrefixExchange, PrefixSlots, gpu_match_slot, gpu_route, prefix_assign
+        from emqx_amd.dist import PrefixSlots, prefix_assign
         self.gm, self.rank, self.world, self.dev, self.sp, self.mode = gm, rank, world, dev, stream, mode
         vr, fr = prefix_assign(f, world)
         idx = np.nonzero((fr == rank) | (fr == L.EGM_PREFIX_ALL))[0].astype(np.uint32)
@@ -342,52 +342,60 @@ class PrefixLeg:
         gm.build(sub.blob, sub.off, idx)
         self.n_filters = len(idx)
         del sub, fr
-        self.n = t.n
+        self.n, self.nbytes = t.n, len(t.blob)
         # the slots are the layout's (equal all_to_all splits): sized from the largest batch of any rank
         mx = torch.tensor([t.n, len(t.blob)], dtype=torch.int64, device=dev)
         if have_pg:
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        self.ps = ps = PrefixSlots.for_batch(world, int(mx[0].item()), int(mx[1].item()), slack)
+        ps = PrefixSlots.for_batch(world, int(mx[0].item()), int(mx[1].item()), slack)
         self.d_blob = torch.from_numpy(t.blob).to(dev)
         self.d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
         self.d_vr = torch.from_numpy(vr).to(dev)
-        self.send = torch.zeros(world * ps.slot_bytes, dtype=torch.uint8, device=dev)
-        self.rows = [torch.zeros(ps.cap_topics + 1, dtype=torch.int64, device=dev) for _ in range(world)]
-        self.cap = 64 * ps.cap_topics + 4096
-        self.idss = [torch.zeros(self.cap, dtype=torch.int32, device=dev) for _ in range(world)]
-        self._make()
+        self.ids_per_topic = 64
+        self._make(ps)
 
-    def _make(self):
-        from emqx_amd.dist import PrefixExchange, gpu_match_slot, gpu_route
-        route = gpu_route(self.gm, self.ps, self.d_vr, self.sp, self.send)
-        match = gpu_match_slot(self.gm, self.ps, self.mode, self.sp, self.rows, self.idss)
-        self.ex = PrefixExchange(self.rank, self.world, self.dev, self.ps, route, match)
+    def _make(self, ps):
+        from emqx_amd.dist import PrefixExchange, gpu_prefix_stages
+        self.ex = PrefixExchange(self.rank, self.world, self.dev, ps,
+                                 gpu_prefix_stages(self.gm, self.d_vr, self.mode, self.sp, self.ids_per_topic))
+
+    @property
+    def ps(self):
+        return self.ex.ps
+
+    @property
+    def rows(self):
+        return self.ex.match_slot.rows
+
+    @property
+    def cap(self):
+        return self.ex.match_slot.ids[0].numel()
 
     def step(self):
-        return self.ex.step(self.d_blob, self.d_off, self.n)
+        """One step that always completes (PrefixExchange.run: an overflowed
+        slot is redone with grown slots; one 24-byte all-reduce per step)."""
+        return self.ex.run(self.d_blob, self.d_off, self.n, self.nbytes)
 
     def size(self):
         """Untimed steps until every received slot's ids fit (grown from the
-        device totals); a slot overflow means the slack is too small."""
+        device totals) and the slot layout has settled."""
         import torch
         for _ in range(4):
             self.step()
             torch.cuda.synchronize(self.dev)
-            if self.ex.overflowed():
-                raise RuntimeError("prefix leg: a destination slot overflowed (raise the slack)")
             need = max(int(r[self.ps.cap_topics].item()) for r in self.rows)
             if need <= self.cap:
                 return
-            self.cap = int(need * 1.25) + 1024
-            self.idss = [torch.zeros(self.cap, dtype=torch.int32, device=self.dev) for _ in range(self.world)]
-            self._make()
+            self.ids_per_topic = int(need * 1.25 / max(self.ps.cap_topics, 1)) + 1
+            self._make(self.ps)
         raise RuntimeError("prefix leg: buffers did not settle")
 
     def merged_ids(self):
         return None
 
     def check(self):
-        """After the timed steps (the caller has synced): no slot overflow, ids fit."""
+        """After the timed steps (the caller has synced): no slot overflow left
+        unredone, ids fit."""
         assert not self.ex.overflowed(), "prefix slot overflow"
         ids = [int(r[self.ps.cap_topics].item()) for r in self.rows]
         assert max(ids) <= self.cap, (ids, self.cap)
@@ -398,17 +406,12 @@ class PrefixLeg:
         totals (levels, states created, ids, topics received) for the byte model."""
         import torch
         st = {"levels": 0, "visited": 0, "ids": 0, "topics": 0}
-        self.ex.route(self.d_blob, self.d_off, self.n)
-        if self.world > 1:
-            import torch.distributed as dist
-            dist.all_to_all_single(self.ex.recv, self.send)
-            recv = self.ex.recv
-        else:
-            recv = self.send
+        recv = self.ex.exchange(self.ex.route(self.d_blob, self.d_off, self.n))
         torch.cuda.synchronize(self.dev)
         host = recv.cpu().numpy()
         for g in range(self.world):
             cnt, nb, ovf, tids, offs, data = self.ps.parse(host, g)
+            assert not ovf
             self.ex.match_slot(recv, g)
             ls = self.gm.last_stats()
             st["levels"] += int(np.count_nonzero(data == ord("/"))) + cnt
@@ -826,7 +829,7 @@ def main():
             "xgmi_model": (shard_cost_model(n, nbytes, world, merged_ids) if shard else
                            prefix_cost_model(n, nbytes, world, leg.ps) if prefix else None),
             "partition": ({"filters_on_rank": leg.n_filters, "replicated_filters": leg.replicated,
-                           "topics_matched_on_rank0": n_walked} if prefix else None),
+                           "topics_matched_on_rank0": n_walked, "slot_reruns": leg.ex.reruns} if prefix else None),
             "host_e2e": host,
             "cpu_baseline": cpu,
         }
@@ -988,6 +991,7 @@ def prefix_leg(args, f, t, rank, world, dev, mode, have_pg):
         return {"value": t.n * world * args.steps / el, "unit": "topics/s", "ms_per_step": el / args.steps * 1e3,
                 "scaling": "weak", "layout": LAYOUTS["prefix"], "filters_per_rank_max": max_filters,
                 "replicated_filters": leg.replicated, "filters_total": f.n, "ids_on_rank0": ids,
+                "slot_reruns": leg.ex.reruns,
                 "xgmi_model": prefix_cost_model(t.n, len(t.blob), world, leg.ps)}
     finally:
         gm2.close()

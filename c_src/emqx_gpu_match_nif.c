@@ -286,14 +286,18 @@ static ERL_NIF_TERM nif_wait(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
 /* cancel(Ctx, Ticket) -> ok | {error, _}: give the batch up without its rows.
    A normal (not dirty) NIF: egm_match_cancel never blocks — while a build or
    commit holds the context it queues the cancel — so this call and the ticket
-   destructor (run on whatever scheduler collects the ticket) return at once. */
+   destructor (run on whatever scheduler collects the ticket) return at once.
+   Always ok for a ticket of this context: egm_match_cancel answers EGM_OK for
+   a queued (unvalidated) cancel and EGM_E_STATE for a stale ticket only when
+   the context happened to be free, so that difference is lock contention,
+   not a result (include/emqx_gpu_match.h). */
 static ERL_NIF_TERM nif_cancel(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   egm_res_t* r;
   egm_ticket_t* t;
   if (argc != 2 || !get_ctx(env, argv[0], &r) || !get_ticket(env, argv[1], r, &t)) return enif_make_badarg(env);
   t->live = 0;
   int rc = egm_match_cancel(r->ctx, t->ticket);
-  return rc ? error_tuple(env, r->ctx, rc) : ATOM_OK;
+  return (rc == EGM_OK || rc == EGM_E_STATE) ? ATOM_OK : error_tuple(env, r->ctx, rc);
 }
 
 /* subs_build(Ctx, [[Sub]]) -> ok | {error, _}: list position = filter id; a

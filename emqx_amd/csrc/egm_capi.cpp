@@ -1215,7 +1215,7 @@ static void copier_main(egm_ctx* c) {
     hipError_t e = hipEventSynchronize(S.ev_match);   // (a host-synchronised event: device writes released)
     ptrace("match-done", &S, it.second);
     const MatchStats st = *(const MatchStats*)S.h_stats.p;   // copied before ev_match, in stream order
-    bool failed = false;
+    bool failed = e != hipSuccess;   // the match itself failed: nothing is copied, the waiter reports EGM_E_DEVICE
     if (e == hipSuccess && !st.overflow && !st.guard && dma) {
       const uint64_t n = S.n, nids = std::min<uint64_t>(st.total_ids, S.cap), half = (nids / 2 + 3) & ~3ull;
       const uint64_t h1 = std::min(half, nids);
@@ -1604,7 +1604,7 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   // holding it is then protected until this fan-out has read it)
   const bool ord = c->last_walk.order && c->last_walk.row == d_mrow && c->last_walk.n == n;
   MatchWs* OW = ord ? &c->ws[c->last_walk.ws] : nullptr;
-  if (OW && OW->stream && OW->stream != s && OW->ev) hipStreamWaitEvent(s, OW->ev, 0);
+  if (OW && OW->used && OW->stream != s && OW->ev) hipStreamWaitEvent(s, OW->ev, 0);   // (stream 0 is a stream too)
   e = launch_fanout(st, d_mrow, d_mids, n, nids, d_drow, d_fid, d_sub, cap, c->f_dc.as<uint32_t>(),
                     c->f_ds0.as<uint4>(), dpos, c->f_wbase.as<uint64_t>(), c->f_tiles.as<uint64_t>(),
                     c->f_ovf.as<unsigned int>(), s, c->timing ? evp : nullptr, ord ? c->last_walk.order : nullptr);
@@ -1867,13 +1867,13 @@ int egm_prefix_route(egm_ctx* c, const uint8_t* d_blob, const uint32_t* d_off, u
                      uint32_t n_vparts, uint32_t n_ranks, uint32_t cap_topics, uint64_t cap_bytes, void* hip_stream,
                      uint8_t* d_send) {
   if (!c || !d_vpart_rank || !d_send || n_vparts == 0 || n_ranks == 0 || n_ranks > PREFIX_RANKS_MAX ||
-      (n && (!d_blob || !d_off)) || cap_bytes >= (1ull << 32))
+      (n && (!d_blob || !d_off)) || cap_bytes >= (1ull << 32) || n >= PFX_TOPICS_MAX || cap_topics >= PFX_TOPICS_MAX)
     return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
   hipStream_t s = (hipStream_t)hip_stream;   // NULL: the HIP default (null) stream, as the caller's own work
   hipError_t e;
-  if ((e = c->p_ctr.ensure(8 * PREFIX_RANKS_MAX)) != hipSuccess) return c->hip_fail(e, "prefix counters");
+  if ((e = c->p_ctr.ensure(2 * 8 * PREFIX_RANKS_MAX)) != hipSuccess) return c->hip_fail(e, "prefix counters");
   if ((e = c->p_dst.ensure(8ull * std::max<uint32_t>(n, 1))) != hipSuccess) return c->hip_fail(e, "prefix routes");
   c->work_begin(s);
   const PrefixSlots ps{n_ranks, cap_topics, cap_bytes};

@@ -82,7 +82,8 @@ struct MatchWork {                // per-batch device workspace
   void* sort_tmp;                 // radix sort scratch
   size_t sort_tmp_bytes;
   uint32_t key_shape;             // key bits per level, nibble l = level l (0: walk in input order)
-  const uint32_t* n_live;         // device count of real topics (null: all n); the rest are skipped padding
+  const uint32_t* n_live;         // device slot header {count, bytes, overflow, 0} (null: all n live); topics
+                                  // past count are skipped padding, and an overflowed header has none live
 };
 
 constexpr uint32_t KEY_LEVELS = 4;           // levels hashed into the walk-order key
@@ -92,7 +93,8 @@ struct WalkOrderOut {                        // what k_tokenise writes for the s
   uint64_t* val;
   uint32_t* wfix;
   uint32_t shape;
-  const uint32_t* n_live;                    // topics at or past *n_live are padding: TF_SKIP (null: none)
+  const uint32_t* n_live;                    // slot header {count, bytes, overflow, 0}: topics at or past count
+                                             // are padding (TF_SKIP), every topic if overflow != 0 (null: none)
 };
 
 constexpr uint32_t GUARD_STACK = 4u;         // a push would have overrun a work stack (the pop bound makes it impossible)
@@ -184,7 +186,11 @@ hipError_t launch_copy_out(const uint64_t* row, uint32_t n, const uint32_t* ids,
 //   [PO, PO + 4(Ct+1)) offsets into the slot's bytes (entries past count = bytes)
 //   [PB, PB + Cb)    topic bytes
 // Overflow (a destination got more than Ct topics or Cb bytes) is flagged in
-// the header; the slot is then incomplete and the step must be redone.
+// the header; the slot then holds a consistent prefix of its topics (count,
+// bytes and offsets describe exactly the topics placed) and the step must be
+// redone with larger capacities.  A batch holds fewer than 2^30 topics
+// (PFX_TOPICS_MAX: the packed route counter) and a slot fewer than 2^32 bytes.
+constexpr uint32_t PFX_TOPICS_MAX = 1u << 30;
 struct PrefixSlots {
   uint32_t n_ranks, cap_topics;
   uint64_t cap_bytes;

@@ -259,7 +259,8 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
   const uint32_t blk0 = blockIdx.x * TOK_BLOCK;
   if (blk0 >= n) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uint32_t n_live = wo.n_live ? min(*wo.n_live, n) : n;   // topics past it: padding (TF_SKIP)
+  // topics past the slot's count are padding (TF_SKIP); an overflowed slot is not matched at all
+  const uint32_t n_live = wo.n_live ? (wo.n_live[2] ? 0u : min(wo.n_live[0], n)) : n;
   const uint32_t tend = min(blk0 + (uint32_t)TOK_BLOCK, n);
   uint32_t S = TOK_BLOCK;
   for (uint32_t t0 = blk0; t0 < tend;) {
@@ -2240,16 +2241,28 @@ hipError_t launch_copy_out(const uint64_t* row, uint32_t n, const uint32_t* ids,
 // counters would serialise), so a topic's index and byte offset in its slot
 // come from one counter and stay in step.  k_prefix_copy then moves the
 // bytes, a quarter-wave per topic; k_prefix_finish writes the headers.
+//
+// Capacity: a topic is placed iff pos < cap_topics and bpos + len <= cap_bytes.
+// pos and bpos come from one packed counter, so they grow together and the
+// placed topics of a slot are exactly its positions [0, placed): the header's
+// count, bytes and offsets describe them (and only them) even when the slot
+// overflowed.  `placed` is the max over placed topics of the packed
+// {pos + 1, bpos + len}, one LDS atomicMax per topic and one global per block
+// and destination.
 constexpr uint32_t PREFIX_MAX_RANKS = 16;
-constexpr unsigned long long PFX_BYTES_MASK = (1ull << 40) - 1;
+constexpr uint32_t PFX_BYTES_BITS = 34;   // packed counter: topics << 34 | bytes (a batch < 2^30 topics, < 2^32 B)
+constexpr unsigned long long PFX_BYTES_MASK = (1ull << PFX_BYTES_BITS) - 1;
 
 __global__ __launch_bounds__(256) void k_prefix_route(const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off,
                                                       uint32_t n, const uint8_t* __restrict__ vpart_rank,
                                                       uint32_t n_vparts, PrefixSlots ps, uint8_t* __restrict__ send,
                                                       unsigned long long* __restrict__ ctr, uint64_t* __restrict__ dst) {
-  __shared__ unsigned long long lctr[PREFIX_MAX_RANKS], lbase[PREFIX_MAX_RANKS];
+  __shared__ unsigned long long lctr[PREFIX_MAX_RANKS], lbase[PREFIX_MAX_RANKS], lacc[PREFIX_MAX_RANKS];
   const uint32_t tid = threadIdx.x, G = ps.n_ranks;
-  if (tid < G) lctr[tid] = 0;
+  if (tid < G) {
+    lctr[tid] = 0;
+    lacc[tid] = 0;
+  }
   __syncthreads();
   const uint32_t t = blockIdx.x * 256 + tid;
   uint32_t r = 0, len = 0;
@@ -2258,22 +2271,25 @@ __global__ __launch_bounds__(256) void k_prefix_route(const uint8_t* __restrict_
     const uint32_t a = off[t];
     len = off[t + 1] - a;
     r = vpart_rank[prefix_vpart(blob + a, len, n_vparts)];
-    loc = atomicAdd(&lctr[r], (1ull << 40) | len);
+    loc = atomicAdd(&lctr[r], (1ull << PFX_BYTES_BITS) | len);
   }
   __syncthreads();
   if (tid < G) lbase[tid] = lctr[tid] ? atomicAdd(&ctr[tid], lctr[tid]) : 0ull;
   __syncthreads();
   if (t < n) {
-    const unsigned long long pos = (lbase[r] >> 40) + (loc >> 40);
+    const unsigned long long pos = (lbase[r] >> PFX_BYTES_BITS) + (loc >> PFX_BYTES_BITS);
     const unsigned long long bpos = (lbase[r] & PFX_BYTES_MASK) + (loc & PFX_BYTES_MASK);
     const bool ok = pos < ps.cap_topics && bpos + len <= ps.cap_bytes;
-    dst[t] = ok ? ((uint64_t)r | (pos << 8) | (bpos << 32)) : ~0ull;   // ~0: dropped (the header says overflow)
+    dst[t] = ok ? ((uint64_t)r | (bpos << 8)) : ~0ull;   // ~0: not placed (the header says overflow)
     if (ok) {
       uint8_t* slot = send + (uint64_t)r * ps.slot_bytes();
       ((uint32_t*)(slot + 16))[pos] = t;
       ((uint32_t*)(slot + ps.off_offsets()))[pos] = (uint32_t)bpos;
+      atomicMax(&lacc[r], ((pos + 1) << PFX_BYTES_BITS) | (bpos + len));
     }
   }
+  __syncthreads();
+  if (tid < G && lacc[tid]) atomicMax(&ctr[PREFIX_MAX_RANKS + tid], lacc[tid]);
 }
 
 // A quarter-wave (16 lanes) per topic copies its bytes into its slot.
@@ -2285,27 +2301,27 @@ __global__ __launch_bounds__(256) void k_prefix_copy(const uint8_t* __restrict__
     const uint64_t d = dst[t];
     if (d == ~0ull) continue;
     const uint32_t a = off[t], len = off[t + 1] - a;
-    uint8_t* out = send + (uint64_t)(d & 0xFF) * ps.slot_bytes() + ps.off_bytes() + (d >> 32);
+    uint8_t* out = send + (uint64_t)(d & 0xFF) * ps.slot_bytes() + ps.off_bytes() + (d >> 8);
     for (uint32_t i = l16; i < len; i += 16) out[i] = blob[a + i];
   }
 }
 
-// Headers, and the offsets past each slot's count (= its bytes: empty padding
-// topics, skipped by egm_match_device_counted through the count).
+// Headers, and the offsets past each slot's placed topics (= its placed
+// bytes: empty padding topics, skipped by egm_match_device_counted through
+// the count).  ctr[r] = every topic routed to r; ctr[PREFIX_MAX_RANKS + r] =
+// the placed prefix.
 __global__ __launch_bounds__(256) void k_prefix_finish(PrefixSlots ps, uint8_t* __restrict__ send,
                                                        const unsigned long long* __restrict__ ctr) {
   const uint32_t r = blockIdx.y;
   uint8_t* slot = send + (uint64_t)r * ps.slot_bytes();
-  const unsigned long long c = ctr[r];
-  const uint64_t nt = c >> 40, nb = c & PFX_BYTES_MASK;
-  const bool ovf = nt > ps.cap_topics || nb > ps.cap_bytes;
-  const uint32_t cnt = (uint32_t)min<uint64_t>(nt, ps.cap_topics);
-  const uint32_t bytes = (uint32_t)min<uint64_t>(nb, ps.cap_bytes);
+  const uint64_t routed = ctr[r] >> PFX_BYTES_BITS, acc = ctr[PREFIX_MAX_RANKS + r];
+  const uint32_t cnt = (uint32_t)(acc >> PFX_BYTES_BITS);
+  const uint32_t bytes = (uint32_t)(acc & PFX_BYTES_MASK);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     uint32_t* h = (uint32_t*)slot;
     h[0] = cnt;
     h[1] = bytes;
-    h[2] = ovf ? 1u : 0u;
+    h[2] = routed > cnt ? 1u : 0u;
     h[3] = 0;
   }
   uint32_t* po = (uint32_t*)(slot + ps.off_offsets());
@@ -2317,7 +2333,8 @@ hipError_t launch_prefix_route(const uint8_t* blob, const uint32_t* off, uint32_
                                uint32_t n_vparts, const PrefixSlots& ps, uint8_t* send, unsigned long long* ctr,
                                uint64_t* dst, hipStream_t s) {
   if (ps.n_ranks == 0 || ps.n_ranks > PREFIX_MAX_RANKS || n_vparts == 0) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * ps.n_ranks, s);
+  if (n >= PFX_TOPICS_MAX || ps.cap_topics >= PFX_TOPICS_MAX || ps.cap_bytes >= (1ull << 32)) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(ctr, 0, sizeof(unsigned long long) * 2 * PREFIX_MAX_RANKS, s);
   if (e != hipSuccess) return e;
   if (n) {
     hipLaunchKernelGGL(k_prefix_route, dim3((n + 255) / 256), dim3(256), 0, s, blob, off, n, vpart_rank, n_vparts, ps,

@@ -14,9 +14,10 @@ Two layouts, both over ``torch.distributed`` (backend "nccl" = RCCL on ROCm,
   batch to the key owners (``egm_prefix_route``, HIP) and ONE
   ``all_to_all_single`` exchanges the fixed-size slots; each rank matches the
   slots it received against its partition (``egm_match_device_counted``, the
-  topic count read on the device).  No broadcast, no gather, no host sync per
-  step; results stay on the owner rank (where, in a broker, the owner's
-  subscribers are dispatched).  ``PrefixExchange``.
+  topic count read on the device).  No broadcast, no gather; results stay on
+  the owner rank (where, in a broker, the owner's subscribers are
+  dispatched).  ``PrefixExchange.run`` adds one 24-byte all-reduce per step so
+  that a slot overflowed by key skew is redone with grown slots.
 * **shard** (round 3, kept for comparison): filters are split by
   ``word_hash(filter) mod G`` (egm_common.h filter_shard) with global filter
   ids; rank 0's topic batch is broadcast, every rank matches it against its
@@ -275,7 +276,10 @@ def prefix_key(topic: bytes) -> bytes:
 def prefix_route_reference(blob: np.ndarray, off: np.ndarray, vpart_rank: np.ndarray, ps: PrefixSlots) -> np.ndarray:
     """Host restatement of egm_prefix_route (the gloo path and the GPU test's
     checker): the same slots, topics in input order within a slot (the kernel
-    may order them differently: per-topic content is what is compared)."""
+    may order them differently: per-topic content is what is compared).  A
+    slot past its capacity keeps the topics placed before the capacity ran out
+    (a topic is placed iff its position < cap_topics and its bytes end within
+    cap_bytes — in slot order that is a prefix) and flags overflow."""
     lib = L.load()
     G, V = ps.n_ranks, len(vpart_rank)
     out = np.zeros(G * ps.slot_bytes, dtype=np.uint8)
@@ -289,17 +293,19 @@ def prefix_route_reference(blob: np.ndarray, off: np.ndarray, vpart_rank: np.nda
     for r in range(G):
         base = r * ps.slot_bytes
         items = per[r]
-        nbytes = sum(len(x) for _, x in items)
-        ovf = len(items) > ps.cap_topics or nbytes > ps.cap_bytes
-        if ovf:   # what the kernel keeps is unspecified then: only the flag is compared
-            out[base:base + 16] = np.array([min(len(items), ps.cap_topics), min(nbytes, ps.cap_bytes), 1, 0],
-                                           dtype=np.uint32).view(np.uint8)
-            continue
+        placed, nbytes = 0, 0
+        for _, x in items:
+            if placed >= ps.cap_topics or nbytes + len(x) > ps.cap_bytes:
+                break
+            placed += 1
+            nbytes += len(x)
+        ovf = placed < len(items)
+        items = items[:placed]
         tids = np.array([t for t, _ in items], dtype=np.uint32)
         lens = np.array([len(x) for _, x in items], dtype=np.uint64)
         offs = np.full(ps.cap_topics + 1, nbytes, dtype=np.uint32)
         offs[:len(items)] = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint32) if len(items) else []
-        out[base:base + 16] = np.array([len(items), nbytes, 0, 0], dtype=np.uint32).view(np.uint8)
+        out[base:base + 16] = np.array([len(items), nbytes, int(ovf), 0], dtype=np.uint32).view(np.uint8)
         out[base + ps.off_tids:base + ps.off_tids + 4 * len(items)] = tids.view(np.uint8)
         out[base + ps.off_offsets:base + ps.off_offsets + 4 * (ps.cap_topics + 1)] = offs.view(np.uint8)
         data = b"".join(x for _, x in items)
@@ -310,6 +316,23 @@ def prefix_route_reference(blob: np.ndarray, off: np.ndarray, vpart_rank: np.nda
 SlotMatch = Callable[["object", int], object]
 
 
+class TorchComm:
+    """The prefix exchange's two collectives over torch.distributed (RCCL
+    over xGMI on the GPU, gloo on the CPU)."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def all_to_all(self, recv, send):
+        import torch.distributed as dist
+        dist.all_to_all_single(recv, send, group=self.group)
+
+    def all_max(self, t):
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t
+
+
 class PrefixExchange:
     """One step of the prefix-partition layout on every rank (torch.distributed):
 
@@ -317,36 +340,73 @@ class PrefixExchange:
       2. all_to_all_single of the equal-size slots               [RCCL over xGMI]
       3. match each received slot against this rank's partition [egm_match_device_counted]
 
-    ``route(blob, off, n) -> send`` (uint8 tensor of n_ranks * slot_bytes) and
-    ``match_slot(recv, g) -> result`` are injected: the GPU path in production
-    (``gpu_route`` / ``gpu_match_slot``), numpy + the oracle in the gloo tests.
-    A slot's topic count is read from its header on the device; an overflowed
-    slot (header flag) makes the step invalid — ``overflow_flag`` accumulates
-    the received flags on the device, and the caller checks it when it syncs
-    anyway (no host sync per step)."""
+    ``make(ps) -> (route, match_slot)`` builds the two injected stages for a
+    slot layout: ``route(blob, off, n) -> send`` (uint8 tensor of n_ranks *
+    slot_bytes) and ``match_slot(recv, g) -> result`` — the GPU path in
+    production (``gpu_route`` / ``gpu_match_slot``), numpy + the oracle in the
+    gloo tests.  ``comm`` carries the collectives (``TorchComm`` by default).
 
-    def __init__(self, rank: int, world: int, device, ps: PrefixSlots, route, match_slot: SlotMatch, group=None):
+    ``step`` never syncs the host: a slot's topic count is read from its
+    header on the device, an overflowed slot (header flag) is matched as empty,
+    and ``overflow_flag`` accumulates the received flags on the device for the
+    caller to check where it syncs anyway.  ``run`` is the step that always
+    completes: one small all-reduce decides whether any rank received an
+    overflowed slot, and if so every rank regrows its slots to hold the
+    largest rank's whole batch — which no key skew can overflow, even every
+    topic sharing one prefix — and redoes the step.  The grown layout is kept
+    (a skewed workload stays skewed).  The reference has no such step: it
+    replicates its tables (apps/emqx/src/emqx_trie.erl:53, emqx_router.erl:71)."""
+
+    def __init__(self, rank: int, world: int, device, ps: PrefixSlots, make, comm=None):
         import torch
-        self.rank, self.world, self.device, self.ps = rank, world, device, ps
-        self.route, self.match_slot, self.group = route, match_slot, group
-        self.recv = torch.empty(world * ps.slot_bytes, dtype=torch.uint8, device=device)
+        self.rank, self.world, self.device = rank, world, device
+        self.make = make
+        self.comm = comm if comm is not None else TorchComm()
         self.overflow_flag = torch.zeros(1, dtype=torch.int64, device=device)
+        self.last_flag = torch.zeros(1, dtype=torch.int64, device=device)
+        self.reruns = 0
+        self._layout(ps)
+
+    def _layout(self, ps: PrefixSlots):
+        import torch
+        self.ps = ps
+        self.route, self.match_slot = self.make(ps)
+        self.recv = torch.empty(self.world * ps.slot_bytes, dtype=torch.uint8, device=self.device)
+
+    def exchange(self, send):
+        if self.world > 1:
+            self.comm.all_to_all(self.recv, send)                                # 2. exchange
+            return self.recv
+        return send
 
     def step(self, blob, off, n: int):
         import torch
-        import torch.distributed as dist
-        send = self.route(blob, off, n)                                          # 1. route
-        if self.world > 1:
-            dist.all_to_all_single(self.recv, send, group=self.group)           # 2. exchange
-            recv = self.recv
-        else:
-            recv = send
+        recv = self.exchange(self.route(blob, off, n))                           # 1. route, 2.
         hdr = recv.view(self.world, self.ps.slot_bytes)[:, :16].view(torch.int32)
-        self.overflow_flag += hdr[:, 2].to(torch.int64).sum()                    # stays on the device
+        self.last_flag = hdr[:, 2].to(torch.int64).sum().reshape(1)             # stays on the device
+        self.overflow_flag += self.last_flag
         return [self.match_slot(recv, g) for g in range(self.world)]             # 3. match
 
+    def run(self, blob, off, n: int, n_bytes: int):
+        """step(), redone with grown slots if any rank's received slot
+        overflowed (one all-reduce of 3 int64 per step: a host sync)."""
+        import torch
+        out = self.step(blob, off, n)
+        info = torch.cat([self.last_flag, torch.tensor([n, n_bytes], dtype=torch.int64, device=self.device)])
+        if self.world > 1:
+            info = self.comm.all_max(info)
+        flag, mn, mb = (int(x) for x in info.tolist())
+        if flag == 0:
+            return out
+        self.overflow_flag -= self.last_flag                                    # handled here
+        self.reruns += 1
+        self._layout(PrefixSlots(self.world, max(mn, 1), max(mb, 16)))
+        out = self.step(blob, off, n)
+        return out
+
     def overflowed(self) -> bool:
-        """Any overflow so far (a host sync: call it where the caller syncs anyway)."""
+        """Any overflow in a step not redone by run() (a host sync: call it
+        where the caller syncs anyway)."""
         return bool(self.overflow_flag.item())
 
 
@@ -377,6 +437,27 @@ def gpu_match_slot(gm, ps: PrefixSlots, mode: int, stream: int, rows: list, ids:
         return rows[g], ids[g], tids
 
     return match_slot
+
+
+def gpu_prefix_stages(gm, d_vpart_rank, mode: int, stream: int, ids_per_topic: int = 64):
+    """make(ps) for PrefixExchange on the GPU: a send buffer, per-slot row and
+    id buffers sized for ps (ids_per_topic per slot topic + 4096), and the
+    route / match stages over them.  The buffers stay reachable as attributes
+    of the returned route function (`route.send`, `match.rows`, `match.ids`)."""
+    import torch
+
+    def make(ps: PrefixSlots):
+        dev = d_vpart_rank.device
+        send = torch.zeros(ps.n_ranks * ps.slot_bytes, dtype=torch.uint8, device=dev)
+        rows = [torch.zeros(ps.cap_topics + 1, dtype=torch.int64, device=dev) for _ in range(ps.n_ranks)]
+        ids = [torch.zeros(ids_per_topic * ps.cap_topics + 4096, dtype=torch.int32, device=dev)
+               for _ in range(ps.n_ranks)]
+        route = gpu_route(gm, ps, d_vpart_rank, stream, send)
+        match = gpu_match_slot(gm, ps, mode, stream, rows, ids)
+        route.send, match.rows, match.ids = send, rows, ids
+        return route, match
+
+    return make
 
 
 def topic_slice(n: int, rank: int, world: int) -> Tuple[int, int]:

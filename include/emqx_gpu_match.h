@@ -160,7 +160,13 @@ int egm_match_batch(egm_ctx* ctx, const uint8_t* topics_blob, const uint32_t* to
    never blocks: while another call holds the context (a bulk build or a
    commit can for seconds) the cancel is queued and applied by the next
    pipeline call, so it may run on a normal Erlang scheduler or in a resource
-   destructor; a queued cancel of a stale ticket is dropped.
+   destructor; a queued cancel of a stale ticket is dropped.  Return value:
+   EGM_OK when the cancel was applied OR queued (a queued cancel is not
+   validated: EGM_OK then says nothing about the ticket), EGM_E_STATE only
+   when the context was free and the ticket is unknown, stale or already
+   waited.  Callers must not branch on the difference (the NIF's cancel/2
+   returns ok in both cases).  A queued cancel keeps its slot busy until the
+   next submit, wait or cancel drains the queue.
    egm_match_batch is submit + wait on a slot of its own: concurrent callers
    never see "pipeline full" (extra slots up to 16, then they queue for one).
    A walk guard trip (a kernel invariant failed, egm_last_guard) makes wait
@@ -178,12 +184,15 @@ int egm_match_cancel(egm_ctx* ctx, uint64_t ticket);
 int egm_match_device(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_offsets,
                      uint32_t n_topics, int mode, void* hip_stream, uint64_t* d_row_ptr, uint32_t* d_ids,
                      uint64_t ids_cap, uint8_t* d_flags);
-/* egm_match_device over a batch whose topic count is on the device: the
-   first *d_n (<= n_max) topics are matched, the rest (padding; their offsets
-   must still be valid, e.g. empty topics at the end) get empty rows without a
-   walk.  For batches whose size only the device knows — the received slots of
-   the prefix partition exchange (egm_prefix_route) — so the host never waits
-   for a count.  d_row_ptr[n_max] holds the number of ids. */
+/* egm_match_device over a batch whose topic count is on the device: d_n is a
+   device slot header {count, bytes, overflow, 0} (u32 x 4, egm_prefix_route's
+   layout).  The first count (<= n_max) topics are matched, the rest (padding;
+   their offsets must still be valid, e.g. empty topics at the end) get empty
+   rows without a walk; a header with overflow != 0 is matched as an empty
+   batch (every row empty: the step must be redone, its partial slot is never
+   walked).  For batches whose size only the device knows — the received slots
+   of the prefix partition exchange (egm_prefix_route) — so the host never
+   waits for a count.  d_row_ptr[n_max] holds the number of ids. */
 int egm_match_device_counted(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_offsets,
                              uint32_t n_max, const uint32_t* d_n, int mode, void* hip_stream, uint64_t* d_row_ptr,
                              uint32_t* d_ids, uint64_t ids_cap);
@@ -277,8 +286,12 @@ int egm_shard_merge(egm_ctx* ctx, uint32_t n_shards, uint32_t n_topics, const ui
      [0,16) {count, bytes, overflow, 0}; [16, 16+4*cap_topics) source topic
      index of each slot topic; then offsets u32[cap_topics+1] (entries past
      count = bytes); then the topic bytes (cap_bytes), all 16-B aligned.
-   A slot past its capacity sets overflow (its content is then incomplete:
-   redo the step with larger capacities). */
+   A slot past its capacity sets overflow: it then holds the topics placed
+   before the capacity ran out, and count, bytes and offsets describe exactly
+   those (a consistent, incomplete slot; egm_match_device_counted matches it as
+   empty); redo the step with larger capacities (dist.PrefixExchange.run does).
+   n_topics and cap_topics < 2^30, cap_bytes < 2^32, n_ranks <= 16, else
+   EGM_E_INVAL. */
 #define EGM_PREFIX_ALL 0xFFFFFFFFu
 int egm_prefix_assign(const uint8_t* blob, const uint32_t* offsets, uint32_t n, uint32_t n_vparts, uint32_t n_ranks,
                       uint8_t* vpart_rank, uint32_t* filter_rank);

@@ -148,19 +148,40 @@ def test_shard_fanout_world2():
 
 
 # ---- prefix partition (SURVEY §8e "partition by root word")
-def _prefix_worker(rank, world, port, q):
-    """PrefixExchange over gloo: every rank routes ITS OWN batch (host
+def _prefix_case(skew: bool):
+    """The C0 sets; with skew, every topic's first two words are replaced by
+    the most common literal two-word prefix of the filters, so every topic
+    routes to one rank (the typical tenant/site/... MQTT tree)."""
+    f, t = synth.config("c0", n_filters=3000, n_topics=4000)
+    if not skew:
+        return f, t
+    from collections import Counter
+    pre = Counter(tuple(x.split(b"/")[:2]) for x in f.to_list()
+                  if x.count(b"/") >= 2 and b"+" not in x.split(b"/")[:2] and b"#" not in x.split(b"/")[:2])
+    (w0, w1), _ = pre.most_common(1)[0]
+    topics = []
+    for x in t.to_list():
+        w = x.split(b"/")
+        topics.append(b"/".join([w0, w1] + w[2:]))
+    blob, off = pack_strings(topics)
+    return f, synth.StringSet(blob, off)
+
+
+def _prefix_worker(rank, world, port, q, skew):
+    """PrefixExchange.run over gloo: every rank routes ITS OWN batch (host
     restatement of egm_prefix_route), one all_to_all exchanges the slots, and
     each rank matches what it received against its partition (replicated
-    filters + its own keys; the C++ oracle stands in for the GPU matcher).
-    The (source rank, topic, ids) triples are gathered to rank 0 only to be
-    checked."""
+    filters + its own keys; the C++ oracle stands in for the GPU matcher, and
+    like egm_match_device_counted it matches an overflowed slot as empty).
+    With skew every topic goes to one rank: the first step overflows that
+    slot and run() redoes it with grown slots.  The (source rank, topic, ids)
+    triples are gathered to rank 0 only to be checked."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from emqx_amd.dist import PrefixExchange, PrefixSlots, prefix_assign, prefix_route_reference
     from emqx_amd import _lib as L
-    f, t = synth.config("c0", n_filters=3000, n_topics=4000)
+    f, t = _prefix_case(skew)
     vr, fr = prefix_assign(f, world, n_vparts=256)
     idx = np.nonzero((fr == rank) | (fr == L.EGM_PREFIX_ALL))[0]
     fl = f.to_list()
@@ -170,52 +191,67 @@ def _prefix_worker(rank, world, port, q):
     lo, hi = topic_slice(t.n, rank, world)
     mine = t.subset(np.arange(lo, hi))
     # the slot capacities are the layout's, the same on every rank (equal all_to_all splits)
-    ps = PrefixSlots.for_batch(world, -(-t.n // world), int(t.off[-1]) // world + 4096, slack=2.0)
+    # (skew: the layout's default slack without for_batch's additive margin,
+    # which one rank's whole load overflows at this small size)
+    if skew:
+        ps = PrefixSlots(world, int(1.25 * t.n / world / world) + 16, int(1.25 * int(t.off[-1]) / world / world) + 1024)
+    else:
+        ps = PrefixSlots.for_batch(world, -(-t.n // world), int(t.off[-1]) // world + 4096, slack=2.0)
 
-    def route(tb, to, n):
-        return torch.from_numpy(prefix_route_reference(tb.numpy(), to.numpy().view(np.uint32), vr, ps))
+    def make(ps):
+        def route(tb, to, n):
+            return torch.from_numpy(prefix_route_reference(tb.numpy(), to.numpy().view(np.uint32), vr, ps))
 
-    def match_slot(recv, g):
-        cnt, nb, ovf, tids, offs, data = ps.parse(recv.numpy(), g)
-        assert not ovf
-        row, ids = o.match(np.ascontiguousarray(data), np.ascontiguousarray(offs), threads=1)
-        return [(g, int(tids[k]), sorted(ids[row[k]:row[k + 1]].tolist())) for k in range(cnt)]
+        def match_slot(recv, g):
+            cnt, nb, ovf, tids, offs, data = ps.parse(recv.numpy(), g)
+            if ovf:
+                return []
+            row, ids = o.match(np.ascontiguousarray(data), np.ascontiguousarray(offs), threads=1)
+            return [(g, int(tids[k]), sorted(ids[row[k]:row[k + 1]].tolist())) for k in range(cnt)]
 
-    ex = PrefixExchange(rank, world, torch.device("cpu"), ps, route, match_slot)
-    out = ex.step(torch.from_numpy(mine.blob.copy()), torch.from_numpy(mine.off.view(np.int32).copy()), mine.n)
+        return route, match_slot
+
+    ex = PrefixExchange(rank, world, torch.device("cpu"), ps, make)
+    out = ex.run(torch.from_numpy(mine.blob.copy()), torch.from_numpy(mine.off.view(np.int32).copy()), mine.n,
+                 len(mine.blob))
     assert not ex.overflowed()
     got = [x for part in out for x in part]
     allg = [None] * world if rank == 0 else None
-    dist.gather_object((rank, len(idx), got), allg, dst=0)
+    dist.gather_object((rank, len(idx), ex.reruns, got), allg, dst=0)
     if rank == 0:
         q.put(allg)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_prefix_exchange_gloo(world):
+@pytest.mark.parametrize("world,skew", [(2, False), (3, False), (2, True), (3, True)])
+def test_prefix_exchange_gloo(world, skew):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_prefix_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_prefix_worker, args=(r, world, port, q, skew)) for r in range(world)]
     for p in procs:
         p.start()
     allg = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    f, t = synth.config("c0", n_filters=3000, n_topics=4000)
+    f, t = _prefix_case(skew)
     o = OracleTrie(True, 0)
     o.add(f.blob, f.off)
     wrow, wids = o.match(t.blob, t.off)
-    seen = {}
-    for _rank, n_filters, got in allg:
+    seen, owners = {}, set()
+    for rank, n_filters, reruns, got in allg:
         assert n_filters < f.n          # a partition, not the whole table
+        assert reruns == (1 if skew else 0)
         for src, tid, ids in got:
             lo, _ = topic_slice(t.n, src, world)
             assert (lo + tid) not in seen   # every topic matched on exactly one rank
             seen[lo + tid] = ids
+            owners.add(rank)
     assert len(seen) == t.n
+    if skew:
+        assert len(owners) == 1         # every topic went to one rank
+    assert sum(1 for i in range(t.n) if wrow[i + 1] > wrow[i]) > t.n // 10
     for i in range(t.n):
         assert seen[i] == sorted(wids[wrow[i]:wrow[i + 1]].tolist()), i

@@ -194,14 +194,38 @@ def test_prefix_route_kernel_vs_reference(gm):
             assert set(pairs) == set(int(x) for x in wt)
             total += gc
         assert total == t.n
-    # capacities too small: overflow flagged in the header
-    small = PrefixSlots(2, 100, 1 << 16)
+    # capacities too small: overflow flagged in the header, and the slot holds
+    # a consistent prefix of its topics (count, bytes and offsets describe
+    # exactly the topics placed) that egm_match_device_counted matches as
+    # empty, without a fault (a byte overflow with topic room left
+    # used to leave unwritten offsets below the header count)
     vr, _ = _prefix_setup(f, 2)
-    send = torch.zeros(2 * small.slot_bytes, dtype=torch.uint8, device=dev)
-    gm.prefix_route(blob.data_ptr(), off.data_ptr(), t.n, torch.from_numpy(vr).to(dev).data_ptr(), len(vr), 2,
-                    small.cap_topics, small.cap_bytes, 0, send.data_ptr())
-    torch.cuda.synchronize()
-    assert all(small.parse(send.cpu().numpy(), r)[2] == 1 for r in range(2))
+    dvr = torch.from_numpy(vr).to(dev)
+    gm.build(f.blob, f.off)
+    for small in (PrefixSlots(2, 100, 1 << 16), PrefixSlots(2, t.n, 1 << 16), PrefixSlots(2, t.n, 40_000)):
+        send = torch.full((2 * small.slot_bytes,), 0xAB, dtype=torch.uint8, device=dev)   # stale bytes
+        gm.prefix_route(blob.data_ptr(), off.data_ptr(), t.n, dvr.data_ptr(), len(vr), 2,
+                        small.cap_topics, small.cap_bytes, 0, send.data_ptr())
+        torch.cuda.synchronize()
+        host = send.cpu().numpy()
+        for r in range(2):
+            gc, gb, go, gt, goff, gdata = small.parse(host, r)
+            assert go == 1 and gc <= small.cap_topics and gb <= small.cap_bytes
+            full = host[r * small.slot_bytes + small.off_offsets:][:4 * (small.cap_topics + 1)].view(np.uint32)
+            assert full[0] == 0 and np.all(np.diff(full[:gc + 1].astype(np.int64)) >= 0) and full[gc] == gb
+            assert np.all(full[gc:] == gb)
+            pairs = {int(gt[k]): bytes(gdata[int(goff[k]):int(goff[k + 1])]) for k in range(gc)}
+            assert len(pairs) == gc and all(pairs[k] == tl[k] for k in pairs)
+            base = send.data_ptr() + r * small.slot_bytes
+            row = torch.full((small.cap_topics + 1,), -1, dtype=torch.int64, device=dev)
+            ids = torch.zeros(4096, dtype=torch.int32, device=dev)
+            gm.match_device_counted(base + small.off_bytes, small.cap_bytes, base + small.off_offsets,
+                                    small.cap_topics, base, L.EGM_MODE_ROUTES, 0, row.data_ptr(), ids.data_ptr(),
+                                    ids.numel())
+            torch.cuda.synchronize()
+            st = gm.last_stats()
+            assert st["overflow"] == 0 and st["errors"] == 0 and st["n_ids"] == 0
+            assert int(row.abs().sum().item()) == 0     # every row empty: an overflowed slot is not walked
 
 
 def _prefix_logical(f, t, world, mode=L.EGM_MODE_ROUTES):
@@ -278,3 +302,150 @@ def test_prefix_partitions_equal_whole_table(gm, world):
     assert np.array_equal(canonical(row, ids), canonical(want.row_ptr, want.ids))
     if world > 1:
         assert max(sizes) < f.n
+
+
+# ---- PrefixExchange.run on logical ranks (threads, one context each) --------
+class _ThreadComm:
+    """all_to_all / all_max between `world` threads of one process on one GPU
+    (the collectives PrefixExchange takes from torch.distributed), so the
+    exchange's own code — including its rerun — runs at world 2 and 4 on the
+    single GPU of a test box.  Barriers time out instead of hanging."""
+
+    def __init__(self, world):
+        import threading
+        self.world = world
+        self.bar = threading.Barrier(world, timeout=180)
+        self.box = [None] * world
+
+    def rank(self, r):
+        hub = self
+
+        class _C:
+            def all_to_all(self, recv, send):
+                import torch
+                torch.cuda.synchronize()
+                hub.box[r] = send
+                hub.bar.wait()
+                S = recv.numel() // hub.world
+                for q in range(hub.world):
+                    recv[q * S:(q + 1) * S].copy_(hub.box[q][r * S:(r + 1) * S])
+                torch.cuda.synchronize()
+                hub.bar.wait()
+
+            def all_max(self, t):
+                import torch
+                torch.cuda.synchronize()
+                hub.box[r] = t.clone()
+                hub.bar.wait()
+                out = torch.stack(hub.box).max(0).values
+                hub.bar.wait()
+                return out
+
+        return _C()
+
+
+def _skew_topics(f, t):
+    """Every topic's first two words replaced by the most common literal
+    two-word prefix of the filters: the whole batch routes to one rank."""
+    from collections import Counter
+    heads = [x.split(b"/")[:2] for x in f.to_list() if x.count(b"/") >= 2]
+    pre = Counter(tuple(h) for h in heads if b"+" not in h and b"#" not in h)
+    (w0, w1), _ = pre.most_common(1)[0]
+    blob, off = pack_strings([b"/".join([w0, w1] + x.split(b"/")[2:]) for x in t.to_list()])
+    return synth.StringSet(blob, off)
+
+
+@pytest.mark.parametrize("case,world", [("skew", 2), ("skew", 4), ("bytes", 2), ("plain", 2)])
+def test_prefix_exchange_run_logical_ranks(gm, case, world):
+    """dist.PrefixExchange.run on `world` logical ranks (threads, a context
+    and a table partition each, _ThreadComm for the collectives):
+    * skew — every topic shares one a/b prefix, so one slot per sender
+      overflows at the layout's default slack; run() redoes the step with
+      grown slots on every rank;
+    * bytes — the first layout has room for every topic but too few bytes,
+      so the first step's slots overflow by bytes (matched as empty, no
+      fault) and the rerun completes;
+    * plain — no overflow, no rerun.
+    Every topic is matched on exactly one rank and the rows equal the whole
+    table's (ROUTES mode)."""
+    import threading
+    import torch
+    from emqx_amd.dist import PrefixExchange, PrefixSlots, gpu_prefix_stages, topic_slice
+    dev = torch.device("cuda:0")
+    f, t = synth.config("c2", n_filters=200_000, n_topics=100_000)
+    if case == "skew":
+        t = _skew_topics(f, t)
+    vr, fr = _prefix_setup(f, world)
+    fl = f.to_list()
+    parts = [t.subset(np.arange(*topic_slice(t.n, r, world))) for r in range(world)]
+    mt, mb = max(p.n for p in parts), max(len(p.blob) for p in parts)
+    if case == "bytes":
+        ps0 = PrefixSlots(world, mt, mb // (4 * world))
+    else:
+        ps0 = PrefixSlots(world, int(mt * 1.25 / world) + 16, int(mb * 1.25 / world) + 1024)
+    hub = _ThreadComm(world)
+    results, errors = [None] * world, []
+
+    def rank_main(r):
+        try:
+            idx = np.nonzero((fr == r) | (fr == L.EGM_PREFIX_ALL))[0]
+            g = GpuMatcher(0, max_batch=mt)
+            try:
+                blob, off = pack_strings([fl[i] for i in idx])
+                g.build(blob, off, idx.astype(np.uint32))
+                dvr = torch.from_numpy(vr).to(dev)
+                p = parts[r]
+                b = torch.from_numpy(p.blob.copy()).to(dev)
+                o = torch.from_numpy(p.off.view(np.int32).copy()).to(dev)
+                ex = PrefixExchange(r, world, dev, ps0, gpu_prefix_stages(g, dvr, L.EGM_MODE_ROUTES, 0, 128),
+                                    comm=hub.rank(r))
+                out = ex.run(b, o, p.n, len(p.blob))
+                torch.cuda.synchronize()
+                assert not ex.overflowed()
+                st = g.last_stats()
+                assert st["errors"] == 0
+                got = []
+                for src, (row, ids, tids) in enumerate(out):
+                    rown = row.cpu().numpy()
+                    got.append((src, rown, ids.cpu().numpy().view(np.uint32), tids.cpu().numpy().view(np.uint32)))
+                recv = (ex.recv if world > 1 else ex.route.send).cpu().numpy()
+                counts = [ex.ps.parse(recv, src)[0] for src in range(world)]
+                results[r] = (ex.reruns, got, counts, len(idx))
+            finally:
+                g.close()
+        except BaseException as e:   # noqa: BLE001 - reported below, barrier released
+            errors.append((r, repr(e)))
+            hub.bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=600)
+    assert not errors, errors
+    rows_by_topic = [None] * t.n
+    owners = set()
+    for r in range(world):
+        reruns, got, counts, nf = results[r]
+        assert reruns == (0 if case == "plain" else 1), (r, reruns)
+        if world > 1:
+            assert nf < f.n
+        for (src, rown, idn, tids), cnt in zip(got, counts):
+            assert np.all(rown[cnt:] == rown[cnt])      # padding topics: empty rows
+            lo = topic_slice(t.n, src, world)[0]
+            for k in range(cnt):
+                i = lo + int(tids[k])
+                assert rows_by_topic[i] is None         # matched on exactly one rank
+                rows_by_topic[i] = idn[rown[k]:rown[k + 1]]
+                owners.add(r)
+    assert all(x is not None for x in rows_by_topic)
+    if case == "skew":
+        assert len(owners) == 1
+    row = np.zeros(t.n + 1, np.uint64)
+    row[1:] = np.cumsum([len(x) for x in rows_by_topic])
+    ids = np.concatenate(rows_by_topic)
+    gm.build(f.blob, f.off)
+    want = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
+    assert int(want.row_ptr[-1]) > t.n                # matches exist
+    assert np.array_equal(row, want.row_ptr)
+    assert np.array_equal(canonical(row, ids), canonical(want.row_ptr, want.ids))
