@@ -478,9 +478,13 @@ def main():
                          "would save the walk")
     ap.add_argument("--x-orders", default="",
                     help="experiment: after the timed steps, time the same steps under each walk order "
-                         "'shape[/cap],...' (EGM_WALK_KEY: key bits per level as hex nibbles, level 0 lowest, 0 = "
-                         "input order; EGM_FIX_CAP: ids per fixed block) and check "
+                         "'shape[/flush],...' (EGM_WALK_KEY: key bits per level as hex nibbles, level 0 lowest, 0 = "
+                         "input order; EGM_FLUSH_AT: staged emits per flush record) and check "
                          "that every order gives the same rows (stderr)")
+    ap.add_argument("--rows", default="walk", choices=["walk", "input"],
+                    help="result rows in the walk's order with the row -> topic map (egm_match_device_ordered, "
+                         "the default) or in input order (egm_match_device); the other form is timed beside it "
+                         "(`rows_other`)")
     ap.add_argument("--pipelined", default="on", choices=["on", "off"],
                     help="after the timed steps, time them again in the other stream setting: one stream "
                          "(`serial`) after two, two streams (`pipelined`) after --streams 1 (replicate mode, "
@@ -590,6 +594,8 @@ def main():
     bufs["rows"] = [torch.zeros(n + 1, dtype=torch.int64, device=dev) for _ in range(nbuf)]
     bufs["idss"] = [torch.zeros(bufs["cap"], dtype=torch.int32, device=dev) for _ in range(nbuf)]
     bufs["row"], bufs["ids"] = bufs["rows"][0], bufs["idss"][0]
+    bufs["walk_rows"] = args.rows == "walk" and leg is None
+    bufs["tops"] = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(nbuf)]
 
     compact = args.fanout_form == "compact"
     fcap = max(8 * n, 1 << 20) if fanout else 0
@@ -606,8 +612,12 @@ def main():
         bufs["k"] += 1
         s_i = streams[i].cuda_stream
         row, ids = bufs["rows"][i], bufs["idss"][i]
-        gm.match_device(d_blob.data_ptr(), nbytes, d_off.data_ptr(), n, mode, s_i, row.data_ptr(), ids.data_ptr(),
-                        bufs["cap"])
+        if bufs["walk_rows"]:   # rows in walk order + the row -> topic map
+            gm.match_device_ordered(d_blob.data_ptr(), nbytes, d_off.data_ptr(), n, mode, s_i, row.data_ptr(),
+                                    bufs["tops"][i].data_ptr(), ids.data_ptr(), bufs["cap"])
+        else:
+            gm.match_device(d_blob.data_ptr(), nbytes, d_off.data_ptr(), n, mode, s_i, row.data_ptr(),
+                            ids.data_ptr(), bufs["cap"])
         if fan_on:
             fan = gm.fanout_device_compact if compact else gm.fanout_device
             fan(row.data_ptr(), ids.data_ptr(), bufs["cap"], n, s_i, d_drow.data_ptr(), d_fid.data_ptr(),
@@ -749,6 +759,28 @@ def main():
                      "note": "same steps, consecutive batches alternating over two HIP streams (separate "
                              "workspaces and output buffers)"}
         bufs["ns"], bufs["k"] = nstreams, 0
+    rows_other = None
+    if leg is None and not fanout:
+        # the same steps with the other row form (input order <-> walk order), reported beside `value`
+        bufs["walk_rows"], bufs["k"] = not bufs["walk_rows"], 0
+        for _ in range(2):
+            run_local()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run_local()
+        torch.cuda.synchronize(dev)
+        pe = time.perf_counter() - t0
+        if have_pg:
+            e = torch.tensor([pe], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            pe = float(e.item())
+        st2 = gm.last_stats()
+        assert st2["overflow"] == 0 and st2["errors"] == 0, st2
+        rows_other = {"rows": "walk" if bufs["walk_rows"] else "input", "streams": bufs["ns"],
+                      "value": n * world * args.steps / pe, "ms_per_step": pe / args.steps * 1e3,
+                      "api": "egm_match_device_ordered" if bufs["walk_rows"] else "egm_match_device"}
+        bufs["walk_rows"], bufs["k"] = not bufs["walk_rows"], 0
     merged_ids = leg.merged_ids() if leg is not None else None
     if args.x_orders and leg is None:
         order_experiment(args, gm, run_local, bufs, dev, n)
@@ -795,7 +827,9 @@ def main():
                        "topics_per_step": units_per_step, "topics_per_gpu": n,
                        "filters_on_rank0": tstats["filters"],
                        "match": "emqx_router:match_routes" if args.match == "routes" else "emqx_trie:match",
-                       "parallelism": f"{args.mode}{world}", "streams": nstreams, "table": tstats},
+                       "parallelism": f"{args.mode}{world}", "streams": nstreams, "table": tstats,
+                       "rows": ("walk order + row -> topic map (egm_match_device_ordered)" if bufs["walk_rows"]
+                                else "input order (egm_match_device)")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic[0]["traffic_bytes_per_launch"] if traffic else None,
@@ -825,6 +859,7 @@ def main():
                        if fanout else None),
             "pipelined": pipelined,
             "serial": serial,
+            "rows_other": rows_other,
             "sharded": None,
             "xgmi_model": (shard_cost_model(n, nbytes, world, merged_ids) if shard else
                            prefix_cost_model(n, nbytes, world, leg.ps) if prefix else None),
@@ -1004,24 +1039,30 @@ def order_experiment(args, gm, run_local, bufs, dev, n):
     import torch
 
     def rows_sig():
+        # per input topic: (ids, sum of ids) — walk-order rows mapped through the topic map
         row, ids = bufs["rows"][0], bufs["idss"][0]
         tot = int(row[n].item())
         cs = torch.cumsum(ids[:tot].to(torch.int64), 0)
         cs = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), cs])
-        return row.clone(), cs[row]
+        cnt, sm = row[1:] - row[:-1], cs[row[1:]] - cs[row[:-1]]
+        if bufs["walk_rows"]:
+            top = bufs["tops"][0].to(torch.int64)
+            cnt = torch.zeros_like(cnt).scatter_(0, top, cnt)
+            sm = torch.zeros_like(sm).scatter_(0, top, sm)
+        return cnt, sm
 
-    saved = {k: os.environ.get(k) for k in ("EGM_WALK_KEY", "EGM_FIX_CAP")}
+    saved = {k: os.environ.get(k) for k in ("EGM_WALK_KEY", "EGM_FLUSH_AT")}
     bufs["k"] = 0
     run_local()
     torch.cuda.synchronize(dev)
     ref_row, ref_sig = rows_sig()
     for spec in args.x_orders.split(","):
-        shape, _, cap = spec.partition("/")
+        shape, _, fl = spec.partition("/")
         os.environ["EGM_WALK_KEY"] = shape
-        if cap:
-            os.environ["EGM_FIX_CAP"] = cap
+        if fl:
+            os.environ["EGM_FLUSH_AT"] = fl
         else:
-            os.environ.pop("EGM_FIX_CAP", None)
+            os.environ.pop("EGM_FLUSH_AT", None)
         for _ in range(2):
             bufs["k"] = 0
             run_local()

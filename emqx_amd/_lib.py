@@ -100,6 +100,7 @@ SIGNATURES = {
     "egm_match_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(C.POINTER(egm_result))]),
     "egm_match_cancel": (C.c_int, [_P, C.c_uint64]),
     "egm_match_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, _P, _P, C.c_uint64, _P]),
+    "egm_match_device_ordered": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, _P, _P, _P, C.c_uint64]),
     "egm_match_device_counted": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, _P, C.c_int, _P, _P, _P,
                                            C.c_uint64]),
     "egm_last_stats": (C.c_int, [_P, _u64p, _u64p, _u32p, _u32p, _u32p]),

@@ -148,9 +148,9 @@ inline uint32_t ticket_gen(uint64_t t) { return (uint32_t)(t >> 16); }
 struct MatchWs {
   DevBuf wid, lv, tfl, cnt, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats;
   DevBuf skey, skey_out, sval, order, wfix, sort_tmp;   // walk-order sort
-  DevBuf inv, ids_fix;                                   // fixed per-topic id blocks (k_compact_fix)
-  uint32_t fix_cap = 0;   // walk-order sort (egm_kernels.hip walk_key)
-  uint64_t pieces_cap = 0, ids_tmp_cap = 0;
+  DevBuf rec, chunks;                                    // flush records and their per-chunk chains (k_rec_rows)
+  uint64_t pieces_cap = 0, ids_tmp_cap = 0, rec_cap = 0;
+  uint32_t rec_grain = REC_GRAIN, flush_lim = 0;
   uint32_t heavy_cap = 0;        // stack items per heavy wave
   hipEvent_t ev = nullptr;       // recorded after its last batch
   hipStream_t stream = nullptr;  // stream of its last batch
@@ -599,13 +599,18 @@ static uint64_t walk_sort_min_bytes() {
   return (v && *v) ? strtoull(v, nullptr, 10) : (1ull << 30);
 }
 
-// EGM_FIX_CAP: ids per topic in its fixed block (the rest spill as pieces);
-// 96 keeps 98.5 % of C2's ids (50 per topic on average) out of the spill.
-static uint32_t fix_cap_ids() {
-  const char* v = getenv("EGM_FIX_CAP");
-  const int k = (v && *v) ? atoi(v) : 96;
-  return (uint32_t)std::min(std::max(k, 1), 1023);   // a chunk's blocks stay 16-bit addressable (64 x cap)
+// Test and A/B knobs of the flush records: EGM_FLUSH_AT — staged emits that
+// trigger a flush (1..WALK_STAGE, default WALK_STAGE: small values make many
+// short records per chunk); EGM_REC_SEG — u32 per record segment (default
+// REC_GRAIN; small values make chunks' record chains jump between segments).
+static uint32_t env_u32(const char* name, uint32_t dflt, uint32_t lo, uint32_t hi) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  const long long k = atoll(v);
+  return (uint32_t)std::min<long long>(std::max<long long>(k, lo), hi);
 }
+static uint32_t flush_lim() { return env_u32("EGM_FLUSH_AT", walk_stage(), 1, walk_stage()); }
+static uint32_t rec_grain() { return env_u32("EGM_REC_SEG", REC_GRAIN, 64, 1u << 24); }
 
 // The workspace for a batch on stream s: the one that last ran on s (stream
 // order protects it), else the least recently used one, ordered after its
@@ -636,18 +641,19 @@ static int ensure_work(egm_ctx* c, MatchWs& W, uint32_t n, uint64_t blob_bytes, 
   if ((e = W.lv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "lv");
   if ((e = W.tfl.ensure(nn)) != hipSuccess) return c->hip_fail(e, "tfl");
   if ((e = W.cnt.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "cnt");
-  if ((e = W.inv.ensure(nn * 4)) != hipSuccess) return c->hip_fail(e, "walk positions");
-  {
-    const uint32_t cap = fix_cap_ids();
-    if ((e = W.ids_fix.ensure(nn * cap * 4)) != hipSuccess) return c->hip_fail(e, "fixed id blocks");
-    W.fix_cap = cap;
-  }
-  // ids in flush order and their pieces, plus the slack of per-wave slabs
-  const uint64_t tcap = ids_tmp_capacity(ids_cap, n);
+  // flush records: sized for the worst case of the batch's id capacity
+  W.flush_lim = flush_lim();
+  W.rec_grain = rec_grain();
+  const uint64_t rcap = rec_capacity(ids_cap, n, W.flush_lim, W.rec_grain);
+  if ((e = W.rec.ensure(rcap * 4)) != hipSuccess) return c->hip_fail(e, "flush records");
+  W.rec_cap = W.rec.cap / 4;
+  if ((e = W.chunks.ensure(((uint64_t)n / WALK_CHUNK + 2) * 16)) != hipSuccess) return c->hip_fail(e, "chunk records");
+  // heavy topics: their ids (count then fill, one piece per topic)
+  const uint64_t tcap = ids_cap + 4096;
   if (tcap >= 0xFFFFFFF0ull) return c->fail(EGM_E_INVAL, "batch too large: > 4G matched ids (split it)");
   if ((e = W.ids_tmp.ensure(tcap * 4)) != hipSuccess) return c->hip_fail(e, "ids_tmp");
   W.ids_tmp_cap = W.ids_tmp.cap / 4;
-  if ((e = W.pieces.ensure(pieces_capacity(ids_cap, n) * 16)) != hipSuccess) return c->hip_fail(e, "pieces");
+  if ((e = W.pieces.ensure(((uint64_t)n + 4096) * 16)) != hipSuccess) return c->hip_fail(e, "pieces");
   W.pieces_cap = std::min<uint64_t>(W.pieces.cap / 16, 0xFFFFFFF0ull);
   if ((e = W.deferred.ensure((n / WALK_CHUNK + 2) * 4 * 2)) != hipSuccess) return c->hip_fail(e, "deferred");
   const uint32_t hcap = heavy_stack_items(max_levels);
@@ -677,9 +683,11 @@ static MatchWork work_view(egm_ctx* c, MatchWs& W) {
   w.lv = W.lv.as<uint32_t>();
   w.tfl = W.tfl.as<uint8_t>();
   w.cnt = W.cnt.as<uint32_t>();
-  w.inv = W.inv.as<uint32_t>();
-  w.ids_fix = W.ids_fix.as<uint32_t>();
-  w.fix_cap = W.fix_cap;
+  w.rec = W.rec.as<uint32_t>();
+  w.rec_cap = W.rec_cap;
+  w.rec_grain = W.rec_grain;
+  w.flush_lim = W.flush_lim;
+  w.chunks = W.chunks.as<uint4>();
   w.ids_tmp = W.ids_tmp.as<uint32_t>();
   w.ids_cap = W.ids_tmp_cap;   // ids_tmp entries (the output capacity is MatchOut's)
   w.pieces = W.pieces.as<uint4>();
@@ -711,11 +719,11 @@ static MatchWork work_view(egm_ctx* c, MatchWs& W) {
 
 static int run_match(egm_ctx* c, MatchWs& W, const Epoch& ep, const uint8_t* d_blob, const uint32_t* d_off,
                      uint32_t n, int mode, hipStream_t s, uint64_t* d_row, uint32_t* d_ids, uint64_t ids_cap,
-                     const uint32_t* d_n_live = nullptr) {
+                     const uint32_t* d_n_live = nullptr, uint32_t* d_topic = nullptr) {
   MatchWork w = work_view(c, W);
   w.n_live = d_n_live;
   if (ep.bytes < walk_sort_min_bytes()) w.key_shape = 0;   // the table fits the caches: the order buys nothing
-  MatchOut o{d_row, d_ids, ids_cap};
+  MatchOut o{d_row, d_ids, ids_cap, d_topic};
   hipEvent_t evp[2] = {nullptr, nullptr};
   if (c->timing) {
     evp[0] = c->take_event();
@@ -723,7 +731,7 @@ static int run_match(egm_ctx* c, MatchWs& W, const Epoch& ep, const uint8_t* d_b
   }
   bool walk_sorted = false;
   hipError_t e = launch_match(ep.view, d_blob, d_off, n, mode, w, o, s, c->timing ? evp : nullptr, &walk_sorted);
-  c->last_walk.order = walk_sorted ? w.order : nullptr;
+  c->last_walk.order = (walk_sorted && !d_topic) ? w.order : nullptr;   // (walk-order rows: already in that order)
   c->last_walk.row = d_row;
   c->last_walk.n = n;
   c->last_walk.ws = (uint32_t)(&W - c->ws);
@@ -1003,6 +1011,23 @@ int egm_match_device(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, con
     hipError_t e = hipMemcpyAsync(d_flags, W.tfl.p, n, hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) r = c->hip_fail(e, "flags copy");
   }
+  ws_done(W, s);
+  return r;
+}
+
+int egm_match_device_ordered(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_off,
+                             uint32_t n, int mode, void* hip_stream, uint64_t* d_row, uint32_t* d_topic,
+                             uint32_t* d_ids, uint64_t ids_cap) {
+  if (!c || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES) || !d_row || (n && !d_topic)) return EGM_E_INVAL;
+  if (n && (!d_blob || !d_off || ((uintptr_t)d_blob & 3))) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  hipStream_t s = (hipStream_t)hip_stream;   // NULL: the HIP default (null) stream, as the caller's own work
+  MatchWs& W = pick_ws(c, s);
+  int r = ensure_work(c, W, n, blob_bytes, ids_cap, std::min<uint64_t>(blob_bytes, 65535) + 1);
+  if (r) return r;
+  std::shared_ptr<Epoch> ep = c->cur;
+  r = run_match(c, W, *ep, d_blob, d_off, n, mode, s, d_row, d_ids, ids_cap, nullptr, d_topic ? d_topic : nullptr);
   ws_done(W, s);
   return r;
 }

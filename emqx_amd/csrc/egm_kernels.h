@@ -39,28 +39,46 @@ struct MatchStats {               // device-side counters, zeroed per batch
   unsigned long long plus_reads;  // walk pops that read a '+' child's record (instrumentation)
   unsigned int n_deep;            // chunks handed to the deep pass of the walk (more than DEEP_MIN levels)
   unsigned int pad2_;
+  unsigned long long rec_cursor;  // flush-record slab u32 reserved (per-wave segments, incl. slack)
 };
 
-// A piece is one flush's run of a topic's spilled ids in ids_tmp:
-// {topic, count, ids_tmp offset, offset inside the topic's CSR row}, so the
-// compaction places every run without atomics (count 0: an unused slot).
-// Each wave reserves its output space in slabs (one device-scope atomic per
-// slab): a single shared counter bumped per flush serialises across the 8
-// XCDs at the memory side.
-constexpr uint32_t SLAB_IDS = 4096;
-constexpr uint32_t SLAB_PIECES = 256;
+// Flush records (round 5).  The walk stages a chunk's emits in LDS and writes
+// each full stage out as ONE contiguous record appended to the wave's segment
+// of the record slab, so its stores are whole lines:
+//   [0, 4)        header {n_entries | REC_TAG, 0, 0, 0}
+//   [4, 36)       64 x u16: the entries of each of the chunk's topics
+//   [36, 36 + n)  the entries' filter ids, grouped by topic (topic 0's first)
+//   padded to a multiple of 4 u32 (16 B).
+// A wave reserves segments of rec_grain u32 (one device-scope atomic each:
+// a counter bumped per flush would serialise across the 8 XCDs) and always
+// keeps REC_HDR u32 free at a segment's end: when the next record does not
+// fit it writes a jump {REC_JUMP, 0, target lo, target hi} there, so a chunk's
+// records are a chain from its first one (ChunkRec).  k_rec_rows then moves
+// each chunk's ids into the rows, whose starts the scan of the counts gives.
+constexpr uint32_t REC_HDR = 4;
+constexpr uint32_t REC_IDS = REC_HDR + 32;        // u32 before the ids
+constexpr uint32_t REC_TAG = 0x5EC0u << 16;
+constexpr uint32_t REC_JUMP = 0x4A4Du << 16;
+constexpr uint32_t REC_GRAIN = 16384;             // default u32 per segment (EGM_REC_SEG)
+__host__ __device__ constexpr uint32_t rec_size(uint32_t n_entries) { return (REC_IDS + n_entries + 3u) & ~3u; }
+// Per chunk (uint4): {first record lo, first record hi, records, flags}.
+constexpr uint32_t CHUNK_WALKED = 1u;             // walked by k_walk (either pass): its records hold its ids
+constexpr uint32_t CHUNK_HEAVY = 2u;              // deferred to k_heavy: its ids are in pieces
 
 struct MatchWork {                // per-batch device workspace
   uint32_t* wid;                  // [blob_bytes + n] word ids, topic t at off[t] + t
   uint32_t* lv;                   // [n] levels
   uint8_t* tfl;                   // [n] TF_* flags
-  uint32_t* cnt;                  // [n] number of ids of topic t
-  uint32_t* inv;                  // [n] walk position of topic t = its fixed block (NONE: a heavy topic, no block)
-  uint32_t* ids_fix;              // [n * fix_cap] each walked topic's first fix_cap ids, by walk position
-  uint32_t fix_cap;               // ids per fixed block (the rest spill into ids_tmp as pieces)
-  uint32_t* ids_tmp;              // [ids_cap] ids in flush order
+  uint32_t* cnt;                  // [n] ids of each result row (row = walk position if walk_rows, else topic)
+  uint32_t walk_rows;             // rows in walk order (MatchOut::topic set): row k = the k-th topic walked
+  uint32_t* rec;                  // [rec_cap] flush records (u32), per-wave segments
+  uint64_t rec_cap;
+  uint32_t rec_grain;             // u32 per record segment
+  uint32_t flush_lim;             // staged emits that trigger a flush (<= WALK_STAGE; smaller: tests)
+  uint4* chunks;                  // [n / CHUNK + 1] ChunkRec per chunk
+  uint32_t* ids_tmp;              // [ids_cap] ids of heavy topics (one piece each)
   uint64_t ids_cap;
-  uint4* pieces;                  // [pieces_cap]
+  uint4* pieces;                  // [pieces_cap] {row, count, ids_tmp offset, 0}
   uint64_t pieces_cap;
   uint32_t* deferred;             // [n / CHUNK + 1] chunk ids for the heavy kernel
   uint32_t* deep;                 // [n / CHUNK + 1] chunk ids for the walk's deep pass
@@ -113,6 +131,8 @@ struct MatchOut {                 // CSR result (device)
   uint64_t* row_ptr;              // [n + 1]
   uint32_t* ids;                  // [ids_cap]
   uint64_t ids_cap;
+  uint32_t* topic;                // [n] or null.  Set: rows in walk order, topic[k] = the input topic of row k
+                                  // (null: row t = input topic t)
 };
 
 // launch sizing shared with the host (egm_capi.cpp)
@@ -124,14 +144,18 @@ int walk_grid_blocks(uint32_t n_topics);
 size_t scan_tiles(uint32_t n);
 // items of HBM stack per heavy wave for topics of up to max_levels levels
 uint32_t heavy_stack_items(uint64_t max_levels);
-// ids_tmp / pieces capacity a batch needs beyond its matched ids: slab tails
-inline uint64_t ids_tmp_capacity(uint64_t ids, uint32_t n) {
-  return ids + ids / 4 + (uint64_t)(walk_grid_blocks(n) + 256) * SLAB_IDS;
-}
-inline uint64_t pieces_capacity(uint64_t ids, uint32_t n) {
-  uint64_t p = 2ull * n + 4096;
-  if (ids / 2 > p) p = ids / 2;
-  return p + (uint64_t)(walk_grid_blocks(n) + 256) * SLAB_PIECES;
+int deep_grid_blocks(uint32_t n_topics);
+uint32_t walk_stage();   // WALK_STAGE: the most emits a flush record holds
+// Record slab u32 for a batch of up to `ids` matched ids: every record carries
+// REC_IDS + 3 u32 beyond its entries and holds at least flush_lim - 256 + 1 of
+// them (a flush is due once the next step could overfill the stage; the last
+// record of a chunk can be shorter: one per chunk), plus every wave's segment
+// tail.
+inline uint64_t rec_capacity(uint64_t ids, uint32_t n, uint32_t flush_lim, uint32_t grain) {
+  const uint64_t per = flush_lim > 256 ? flush_lim - 256 : 1;
+  const uint64_t chunks = (uint64_t)n / WALK_CHUNK + 2;
+  const uint64_t waves = (uint64_t)walk_grid_blocks(n) + (uint64_t)deep_grid_blocks(n);
+  return ids + ids * (REC_IDS + 3 + per - 1) / per + chunks * (REC_IDS + 3 + REC_HDR) + waves * (grain + REC_HDR);
 }
 
 // Timing hooks: when ev != nullptr, ev[0]/ev[1] bracket the walk kernel.

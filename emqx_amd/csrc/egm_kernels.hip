@@ -482,7 +482,7 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #define EGM_WALK_DEEP_MIN 12   // a chunk with a deeper topic is walked by the deep pass
 #endif
 #ifndef EGM_WALK_STAGE
-#define EGM_WALK_STAGE 320   // staged emits per flush (7 B each; >= 4 emits x 64 lanes)
+#define EGM_WALK_STAGE 320   // staged emits per flush record (5 B each in LDS; >= 4 emits x 64 lanes)
 #endif
 #ifndef EGM_WALK_PAIRS
 #define EGM_WALK_PAIRS 0     // A/B: the first pass pops two items per lane per iteration
@@ -504,27 +504,20 @@ __host__ __device__ constexpr uint32_t light_dmax(uint32_t stack) {
 }
 static_assert(WALK_CHUNK == 64, "one topic per lane in the chunk prologue");
 static_assert(WALK_STAGE >= 256, "a step stages up to 4 emits x 64 lanes");
-static_assert(WALK_STAGE <= 0xFFFF, "flush slots and spill starts are packed as 16-bit halves");
+static_assert(WALK_STAGE <= 0xFFFF, "a record's entry count and per-topic counts are 16-bit");
 static_assert(light_dmax(WALK_STACK) >= DEEP_MIN, "the first pass must take the chunks it does not hand on");
 static_assert(light_dmax(WALK_STACK_DEEP) >= 16, "stack too small");
-
-#ifndef EGM_FLUSH_V2
-#define EGM_FLUSH_V2 2   // 2: LDS-atomic ranks, stores in topic order (k_walk 9.13 ms at C2);
-#endif                   // 1: the same ranks, stores in arrival order (10.31); 0: round 3's multi-split (10.17)
 
 template <uint32_t STK>
 struct alignas(16) WaveLds {
   uint4 stack[STK];
   uint32_t stage_fid[WALK_STAGE];
-#if EGM_FLUSH_V2 != 1
-  uint16_t stage_rank[WALK_STAGE];
-#endif
   uint8_t stage_t[WALK_STAGE];       // topic in chunk of the emit
   uint32_t words[WALK_WORDS + 1];    // the sub-chunk's word ids, [topic][level] (+1: a leaf's
                                      // unclamped next-word read, never used)
   uint32_t tinfo[WALK_CHUNK];        // D | tflags << 24 | words at the fixed stride << 31
   uint32_t cnt[WALK_CHUNK];          // ids per topic, whole chunk
-  uint32_t fcnt[WALK_CHUNK];         // ids per topic in the current stage / start inside the flush
+  uint32_t fcnt[WALK_CHUNK];         // ids per topic in the current stage / its first slot in the record
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
@@ -534,53 +527,39 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | (uint64_t)uni((uint32_t)v);
 }
 
-// An unused pieces-slab slot: count 0, skipped by k_compact.
-__device__ __forceinline__ uint4 empty_piece() { return make_uint4(0, 0, 0, 0); }
-
-// Per-wave output slab (uniform across the wave).
-struct Slab {
-  unsigned long long cur, end;
+// The wave's current record segment (u32 offsets into MatchWork::rec) and
+// the current chunk's record chain (all wave-uniform).
+struct RecCursor {
+  unsigned long long cur, end;     // free space [cur, end - REC_HDR) of the segment ({0, 0}: none yet)
+  unsigned long long first;        // the chunk's first record
+  uint32_t nrec;                   // the chunk's records so far
 };
 
-// Take `need` entries from the wave's slab, reserving a new slab of at least
-// `grain` entries (one device-scope atomic) when the current one is short.
-// The unused tail of an abandoned pieces slab is marked empty (count 0).
-__device__ __forceinline__ unsigned long long slab_take(Slab& s, uint32_t need, uint32_t grain,
-                                                        unsigned long long* counter, uint32_t lane,
-                                                        uint4* tail_fill, unsigned long long tail_cap) {
-  if (s.cur + need > s.end) {
-    if (tail_fill)
-      for (unsigned long long i = s.cur + lane; i < s.end && i < tail_cap; i += 64) tail_fill[i] = empty_piece();
-    const unsigned long long sz = need > grain ? need : grain;
-    unsigned long long b = 0;
-    if (lane == 0) b = atomicAdd(counter, sz);
-    b = uni64(__shfl(b, 0, 64));   // wave-uniform: keep it in SGPRs
-    s.cur = b;
-    s.end = b + sz;
-  }
-  const unsigned long long r = s.cur;
-  s.cur += need;
-  return r;
+#ifndef EGM_FLUSH_NT
+#define EGM_FLUSH_NT 1   // flush stores with the nontemporal hint: the records do not displace table lines from L2
+#endif
+__device__ __forceinline__ void st_u32(uint32_t* p, uint32_t v) {
+#if EGM_FLUSH_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
 }
 
-#ifndef EGM_FLUSH_NT
-#define EGM_FLUSH_NT 1   // flush stores with the nontemporal hint (A/B: profiles/r4_walk_ab.jsonl, nts)
-#endif
-#if EGM_FLUSH_V2 == 2
-// Write the stage out, topic-ordered (round 4, the default).  The ranks come from
-// an LDS atomic on the topic's flush counter, as in the arrival-order flush,
-// and stay in registers; one scan of the per-topic counts gives each topic's
-// first slot, every entry moves to its slot (fid and its offset inside the
-// chunk's fixed blocks), and the stores then go out slot by slot, so
-// consecutive lanes write consecutive ids of a block (one L2 request per
-// line instead of one per entry).  Ids past a topic's fixed block are written
-// to the spill slab straight from registers (rare).
+// Write the stage out as one flush record (round 5).  Each staged entry is
+// ranked inside its topic by an LDS atomic on the topic's flush counter
+// (ranks stay in registers); one wave scan of the 64 per-topic counts gives
+// each topic's first slot, the entries move to their slots in the stage, and
+// the record — header, the 64 counts as u16, the ids grouped by topic — goes
+// out as one contiguous run of whole lines, lane l writing u32 l, l + 64, ...
+// of it.  (Rounds 2-4 wrote each topic's entries into a fixed block of 96 ids
+// by walk position: ~5 ids per topic per flush, a partial line in each of ~64
+// blocks, 4.10 GB written per C2 walk for 1.99 GB of ids.)
 template <class LDS>
-__device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t t0, uint32_t my_t, uint32_t lane,
-                                            const MatchWork& w, Slab& sid, Slab& spc) {
-  const uint32_t cap = w.fix_cap;
+__device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t lane, const MatchWork& w,
+                                            RecCursor& rc) {
   constexpr uint32_t NQ = (WALK_STAGE + 63) / 64;
-  uint32_t fv[NQ], pv[NQ];   // fid; topic | rank inside the flush << 8 (two VGPRs per entry)
+  uint32_t fv[NQ], pv[NQ];   // fid; topic | rank inside the flush << 8
 #pragma unroll
   for (uint32_t r = 0; r < NQ; ++r) {
     const uint32_t i = lane + 64 * r;
@@ -591,212 +570,55 @@ __device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t t0
     pv[r] = act ? tt | (atomicAdd(&L.fcnt[tt], 1u) << 8) : 0xFFFFFFFFu;
   }
   wave_sync();
-  const uint32_t fl = L.fcnt[lane];   // the chunk's topic `lane`: ids in this flush
-  const uint32_t c0 = L.cnt[lane];    // ... and before it
-  const uint32_t nfix = c0 >= cap ? 0u : min(fl, cap - c0);
-  const uint32_t over = fl - nfix;    // ids past the fixed block: spilled
-  uint32_t tot, gtot;
-  const uint32_t gx = wave_excl_scan(nfix, lane, &gtot);
-  const uint32_t ex = wave_excl_scan(over, lane, &tot);
-  unsigned long long base = 0;
-  bool ok = true;
-  if (tot) {   // wave-uniform
-    uint32_t ptot;
-    const uint32_t pex = wave_excl_scan(over ? 1u : 0u, lane, &ptot);
-    base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
-    const unsigned long long pbase =
-        slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
-    ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
-    if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
-    if (over && ok) w.pieces[pbase + pex] = make_uint4(my_t, over, (uint32_t)(base + ex), c0 + nfix);
+  const uint32_t fl = L.fcnt[lane];   // the chunk's topic `lane`: its entries in this flush
+  uint32_t tot;
+  const uint32_t gx = wave_excl_scan(fl, lane, &tot);
+  L.fcnt[lane] = gx;
+  // reserve the record: a new segment when the current one cannot hold it and a jump
+  const uint32_t size = rec_size(nstage);
+  if (rc.cur + size + REC_HDR > rc.end) {   // wave-uniform
+    const unsigned long long grain = max((unsigned long long)w.rec_grain, (unsigned long long)(size + REC_HDR));
+    unsigned long long b = 0;
+    if (lane == 0) b = atomicAdd(&w.stats->rec_cursor, grain);
+    b = uni64(__shfl(b, 0, 64));
+    if (rc.end && rc.cur + REC_HDR <= w.rec_cap && lane < REC_HDR)   // the old segment's tail: jump to the new one
+      st_u32(w.rec + rc.cur + lane, lane == 0 ? REC_JUMP : lane == 2 ? (uint32_t)b : lane == 3 ? (uint32_t)(b >> 32) : 0u);
+    rc.cur = b;
+    rc.end = b + grain;
   }
-  L.fcnt[lane] = gx | (ex << 16);   // first slot | spill start (both < WALK_STAGE)
-  wave_sync();
-#pragma unroll
-  for (uint32_t r = 0; r < NQ; ++r) {
-    if (pv[r] == 0xFFFFFFFFu) continue;
-    const uint32_t tt = pv[r] & 0xFFu, f = L.fcnt[tt], cb = L.cnt[tt], k = cb + (pv[r] >> 8);
-    if (k < cap) {
-      const uint32_t q = (f & 0xFFFFu) + (pv[r] >> 8);
-      L.stage_fid[q] = fv[r];
-      L.stage_rank[q] = (uint16_t)(tt * cap + k);   // < 64 x fix_cap <= 65472 (egm_capi.cpp fix_cap_ids)
-    } else if (ok) {
-      w.ids_tmp[base + (f >> 16) + (k - max(cb, cap))] = fv[r];
-    }
-  }
-  wave_sync();
-  const uint64_t blk = (uint64_t)t0 * cap;
-#pragma unroll 1
-  for (uint32_t q = lane; q < gtot; q += 64) {
-#ifdef EGM_AB_NO_ID_STORES   // measurement only (tools/build_variant.py): the walk without its id stores
-    if (L.stage_fid[q] != 0x7FFFFFF1u) continue;
-#endif
-#if EGM_FLUSH_NT   // streaming stores: the id blocks do not displace table lines from L2 (9.78 -> 9.62 ms)
-    __builtin_nontemporal_store(L.stage_fid[q], &w.ids_fix[blk + L.stage_rank[q]]);
-#else
-    w.ids_fix[blk + L.stage_rank[q]] = L.stage_fid[q];
-#endif
-  }
-  wave_sync();
-  L.cnt[lane] += fl;
-  L.fcnt[lane] = 0;
-  wave_sync();
-}
-#elif EGM_FLUSH_V2
-// Write the stage out in arrival order (round 4, A/B: EGM_FLUSH_V2=1).  One pass over the staged entries in arrival
-// order: an LDS atomic on the topic's flush counter ranks each entry inside
-// its topic, and the entry is stored at once into the topic's fixed block
-// (ids_fix, walk position x fix_cap) at cnt + rank — its place inside the
-// block is free (a row is a set).  Two dependent LDS round trips per 64
-// entries.  Entries past a topic's fixed block (1.5 % of C2's ids) are
-// compacted to the front of the stage and, only when there are any, written
-// to the wave's ids slab as one piece per topic {topic, count, ids_tmp offset,
-// offset inside the topic's CSR row}, so neither compaction needs atomics.
-// Round 3's flush ranked entries with a 6-ballot multi-split, scanned three
-// times and stored in topic order after inverting slot -> entry: ~600
-// instructions and ~15 dependent LDS round trips per flush, once every ~4.7
-// walk iterations at C2.
-template <class LDS>
-__device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t t0, uint32_t my_t, uint32_t lane,
-                                            const MatchWork& w, Slab& sid, Slab& spc) {
-  const uint32_t cap = w.fix_cap;
-  uint32_t nsp = 0;   // wave-uniform: entries past their topic's fixed block
-#pragma unroll 1
-  for (uint32_t q0 = 0; q0 < nstage; q0 += 64) {
-    const uint32_t q = q0 + lane;
-    const bool act = q < nstage;
-    const uint32_t qc = act ? q : 0u;
-    const uint32_t tt = L.stage_t[qc], fid = L.stage_fid[qc];
-    uint32_t k = 0;
-    if (act) k = atomicAdd(&L.fcnt[tt], 1u) + L.cnt[tt];
-    const bool fix = act && k < cap;
-#ifndef EGM_AB_NO_ID_STORES   // measurement only (tools/build_variant.py): the walk without its id stores
-    if (fix) w.ids_fix[(uint64_t)(t0 + tt) * cap + k] = fid;
-#endif
-    const uint64_t sb = __ballot(act && !fix);
-    if (sb) {   // rare; every lane has read its entry (the writes land at or below the reading lane's slot)
-      wave_sync();
-      if (act && !fix) {
-        const uint32_t p = nsp + mbcnt(sb);
-        L.stage_fid[p] = fid;
-        L.stage_t[p] = (uint8_t)tt;
-      }
-      nsp += popc(sb);
-    }
-  }
-  wave_sync();
-  const uint32_t fl = L.fcnt[lane];   // the chunk's topic `lane`: ids in this flush
-  if (nsp) {
-    const uint32_t c0 = L.cnt[lane];
-    const uint32_t nfix = c0 >= cap ? 0u : min(fl, cap - c0);
-    const uint32_t over = fl - nfix;    // ids past the fixed block: spilled
-    uint32_t tot, ptot;
-    const uint32_t ex = wave_excl_scan(over, lane, &tot);
-    const uint32_t pex = wave_excl_scan(over ? 1u : 0u, lane, &ptot);
-    const unsigned long long base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
-    const unsigned long long pbase = slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
-    const bool ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
-    if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
-    if (over && ok) w.pieces[pbase + pex] = make_uint4(my_t, over, (uint32_t)(base + ex), c0 + nfix);
-    L.fcnt[lane] = ex;   // the topic's spill cursor inside this flush's run
-    wave_sync();
-#pragma unroll 1
-    for (uint32_t q = lane; q < nsp; q += 64) {
-      const uint32_t tt = L.stage_t[q], fid = L.stage_fid[q];
-      const uint32_t pos = atomicAdd(&L.fcnt[tt], 1u);
-      if (ok) w.ids_tmp[base + pos] = fid;
-    }
-    wave_sync();
-  }
-  L.cnt[lane] += fl;
-  L.fcnt[lane] = 0;
-  wave_sync();
-}
-#else
-// Write the stage out.  Entries are ranked within their topic by a
-// conflict-free multi-split (lanes holding the same topic find each other
-// with 6 ballots; one LDS add per topic per 64 entries).  A topic's first
-// fix_cap ids go straight to its fixed block in ids_fix (walk position x
-// fix_cap; a chunk's blocks are one contiguous region); the rest spill into
-// the wave's ids slab grouped by topic, one piece
-// {topic, count, ids_tmp offset, offset inside the topic's CSR row} per topic
-// that spills, so neither compaction needs atomics.
-template <class LDS>
-__device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t t0, uint32_t my_t, uint32_t lane,
-                                            const MatchWork& w, Slab& sid, Slab& spc) {
-#pragma unroll 1
-  for (uint32_t i0 = 0; i0 < nstage; i0 += 64) {
-    const uint32_t i = i0 + lane;
-    const bool act = i < nstage;
-    const uint32_t tt = act ? L.stage_t[i] : 0u;
-    uint64_t m = __ballot(act);
-#pragma unroll
-    for (uint32_t b = 0; b < 6; ++b) {
-      const bool bit = (tt >> b) & 1u;
-      const uint64_t bb = __ballot(bit);
-      m &= bit ? bb : ~bb;
-    }
-    const uint32_t leader = act ? (uint32_t)__builtin_ctzll(m) : lane;
-    uint32_t old = 0;
-    if (act && lane == leader) old = atomicAdd(&L.fcnt[tt], popc(m));
-    old = __shfl(old, (int)leader, 64);
-    if (act) L.stage_rank[i] = (uint16_t)(old + mbcnt(m));
-  }
-  wave_sync();
-  const uint32_t cap = w.fix_cap;
-  const uint32_t fl = L.fcnt[lane];   // the chunk's topic `lane`: ids in this flush
-  const uint32_t c0 = L.cnt[lane];    // ... and before it
-  const uint32_t nfix = c0 >= cap ? 0u : min(fl, cap - c0);
-  const uint32_t over = fl - nfix;    // ids past the fixed block: spilled
-  uint32_t tot, ptot;
-  const uint32_t ex = wave_excl_scan(over, lane, &tot);
-  const uint32_t pex = wave_excl_scan(over ? 1u : 0u, lane, &ptot);
-  unsigned long long base = 0;
-  bool ok = true;
-  if (tot) {   // wave-uniform
-    base = slab_take(sid, tot, SLAB_IDS, &w.stats->cursor, lane, nullptr, 0);
-    const unsigned long long pbase =
-        slab_take(spc, ptot, SLAB_PIECES, &w.stats->pieces, lane, w.pieces, w.pieces_cap);
-    ok = base + tot <= w.ids_cap && pbase + ptot <= w.pieces_cap;
-    if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
-    if (over && ok) w.pieces[pbase + pex] = make_uint4(my_t, over, (uint32_t)(base + ex), c0 + nfix);
-  }
-  // Stores go out in topic order: slot q of the flush (topics in lane order,
-  // each topic's entries by rank) -> its entry, so consecutive lanes write
-  // consecutive ids of a block instead of one line per lane.
-  uint32_t gtot;
-  const uint32_t gx = wave_excl_scan(fl, lane, &gtot);
-  L.fcnt[lane] = ex | (gx << 16);   // spill start | first slot (both < WALK_STAGE)
-  wave_sync();
-  constexpr uint32_t NQ = (WALK_STAGE + 63) / 64;
-  uint32_t qv[NQ];
-#pragma unroll
-  for (uint32_t r = 0; r < NQ; ++r) {
-    const uint32_t i = lane + 64 * r;
-    qv[r] = i < nstage ? (L.fcnt[L.stage_t[i]] >> 16) + L.stage_rank[i] : 0u;
-  }
+  const unsigned long long base = rc.cur;
+  rc.cur += size;
+  if (rc.nrec == 0) rc.first = base;
+  rc.nrec += 1;
+  const bool ok = base + size <= w.rec_cap;
+  if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
   wave_sync();
 #pragma unroll
   for (uint32_t r = 0; r < NQ; ++r)
-    if (lane + 64 * r < nstage) L.stage_rank[qv[r]] = (uint16_t)(lane + 64 * r);   // now: slot -> entry
+    if (pv[r] != 0xFFFFFFFFu) L.stage_fid[L.fcnt[pv[r] & 0xFFu] + (pv[r] >> 8)] = fv[r];
   wave_sync();
+  if (ok) {
+    // u32 j of the record: j < 4 the header, 4 <= j < 36 the counts of topics 2(j-4) and 2(j-4)+1, then the ids
+    const uint32_t k2 = (lane >= REC_HDR && lane < REC_IDS) ? 2u * (lane - REC_HDR) : 0u;
+    const uint32_t lo = (uint32_t)__shfl(fl, (int)k2, 64), hi = (uint32_t)__shfl(fl, (int)k2 + 1, 64);
+    uint32_t* out = w.rec + base;
 #pragma unroll 1
-  for (uint32_t q = lane; q < nstage; q += 64) {
-    const uint32_t i = L.stage_rank[q], tt = L.stage_t[i], f = L.fcnt[tt], cb = L.cnt[tt];
-    const uint32_t k = cb + (q - (f >> 16));
+    for (uint32_t j = lane; j < size; j += 64) {
+      uint32_t v;
+      if (j < REC_HDR) v = j == 0 ? (nstage | REC_TAG) : 0u;
+      else if (j < REC_IDS) v = lo | (hi << 16);
+      else v = j - REC_IDS < nstage ? L.stage_fid[j - REC_IDS] : 0u;
 #ifdef EGM_AB_NO_ID_STORES   // measurement only (tools/build_variant.py): the walk without its id stores
-    if (L.stage_fid[i] != 0x7FFFFFF1u) continue;
+      if (v != 0x7FFFFFF1u) continue;
 #endif
-    if (k < cap) w.ids_fix[(uint64_t)(t0 + tt) * cap + k] = L.stage_fid[i];
-    else if (ok) w.ids_tmp[base + (f & 0xFFFFu) + (k - max(cb, cap))] = L.stage_fid[i];
+      st_u32(out + j, v);
+    }
   }
   wave_sync();
   L.cnt[lane] += fl;
   L.fcnt[lane] = 0;
   wave_sync();
 }
-
-#endif  // EGM_FLUSH_V2
 
 // Slot search from slot k0 of bucket b on (rare: both first slots hold other keys).
 __device__ __forceinline__ bool edge_probe_from(const DevTable& tab, uint32_t b, int k0, uint32_t node, uint32_t w,
@@ -1022,7 +844,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
   root.w = uni(root.w);
   uint32_t created = 0;
   unsigned long long iters = 0, popped = 0, bounded = 0, lit_probes = 0, plus_reads = 0;
-  Slab sid{0, 0}, spc{0, 0};
+  RecCursor rc{0, 0, 0, 0};
   const uint32_t guard_lim = (w.debug & DEBUG_FORCE_GUARD) ? 2u : (1u << EGM_GUARD_BITS);
   // sorted batch: the record of the chunk's j-th topic in walk order, loaded
   // one chunk ahead (a grid stride: the wave's next chunk is c + gridDim.x)
@@ -1061,6 +883,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
       if (lane == 0) {
         const uint32_t d = atomicAdd(&w.stats->n_deferred, 1u);
         w.deferred[d] = c;
+        w.chunks[c] = make_uint4(0, 0, 0, CHUNK_HEAVY);
       }
       continue;
     }
@@ -1078,6 +901,8 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
     uint32_t S = WALK_CHUNK;
     while (S > 1 && S * dmax > WALK_WORDS) S >>= 1;
     uint32_t nstage = 0;
+    rc.nrec = 0;
+    const uint32_t flim = w.flush_lim;
     wave_sync();
     for (uint32_t sub = 0; sub < nt; sub += S) {
       const uint32_t end = min(sub + S, nt);
@@ -1110,8 +935,8 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
         // lookup, no item) ----
         if (sp < 64u && next < end) {
           const uint32_t k = min(64u - sp, end - next);
-          if (nstage + 64u > WALK_STAGE) {
-            flush_stage(L, nstage, t0, my_t, lane, w, sid, spc);
+          if (nstage && nstage + 64u > flim) {
+            flush_stage(L, nstage, lane, w, rc);
             nstage = 0;
           }
           bool has = false, em = false;
@@ -1213,9 +1038,9 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
           sp += nc;
           const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
           const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
-          if (nstage + ne > WALK_STAGE) {
+          if (nstage && nstage + ne > flim) {   // (flim <= WALK_STAGE: the stage never overfills)
             wave_sync();
-            flush_stage(L, nstage, t0, my_t, lane, w, sid, spc);
+            flush_stage(L, nstage, lane, w, rc);
             nstage = 0;
           }
           const uint8_t st = (uint8_t)qt;
@@ -1249,16 +1074,12 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
         wave_sync();
       }
     }
-    if (nstage) flush_stage(L, nstage, t0, my_t, lane, w, sid, spc);
-    if (lane < nt) {
-      w.cnt[my_t] = L.cnt[lane];
-      w.inv[my_t] = t0 + lane;   // its fixed block (k_compact_fix)
-    }
+    if (nstage) flush_stage(L, nstage, lane, w, rc);
+    if (lane < nt) w.cnt[w.walk_rows ? t0 + lane : my_t] = L.cnt[lane];
+    if (lane == 0) w.chunks[c] = make_uint4((uint32_t)rc.first, (uint32_t)(rc.first >> 32), rc.nrec, CHUNK_WALKED);
     wave_sync();
   }
   if (!DEEP && n_pend) deep_flush(w, deep_c, n_pend, lane);
-  for (unsigned long long i = spc.cur + lane; i < spc.end && i < w.pieces_cap; i += 64)
-    w.pieces[i] = empty_piece();   // unused tail of the last pieces slab
   unsigned long long v = created;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -1315,7 +1136,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
     if (pos >= n) continue;
     const uint64_t rec = w.order ? w.order[pos] : (uint64_t)pos;
     const uint32_t t = uni((uint32_t)rec);
-    if (lane == 0) w.inv[t] = NONE;   // every id of a heavy topic is in its piece (no fixed block)
+    const uint32_t row = w.walk_rows ? pos : t;   // every id of a heavy topic is in its piece
     // a sorted batch keeps a short topic's words only at the fixed stride (k_tokenise)
     const bool fixed = w.order && (rec >> 63);
     const uint32_t* words = fixed ? w.wfix : w.wid;
@@ -1329,12 +1150,12 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
           const unsigned long long p = atomicAdd(&w.stats->pieces, 1ull);
           if (base < w.ids_cap && p < w.pieces_cap) {
             w.ids_tmp[base] = fid;
-            w.pieces[p] = make_uint4(t, 1, (uint32_t)base, 0);
+            w.pieces[p] = make_uint4(row, 1, (uint32_t)base, 0);
           } else {
             atomicOr(&w.stats->overflow, 1u);
           }
         }
-        w.cnt[t] = em ? 1u : 0u;
+        w.cnt[row] = em ? 1u : 0u;
         w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
       }
       continue;
@@ -1342,7 +1163,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
     if (D + 192u > cap) {   // cannot happen for a legal topic (the host sizes cap from the batch)
       if (lane == 0) {
         atomicAdd(&w.stats->errors, 1u);
-        w.cnt[t] = 0;
+        w.cnt[row] = 0;
         w.tfl[t] = (uint8_t)(tf | TF_HEAVY | TF_ERROR);
       }
       continue;
@@ -1420,8 +1241,8 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
         fits = count == 0 || (base + count <= w.ids_cap && pb < w.pieces_cap);
         if (lane == 0) {
           if (!fits) atomicOr(&w.stats->overflow, 1u);
-          w.cnt[t] = count;
-          if (count && fits) w.pieces[pb] = make_uint4(t, count, (uint32_t)base, 0);
+          w.cnt[row] = count;
+          if (count && fits) w.pieces[pb] = make_uint4(row, count, (uint32_t)base, 0);
           w.tfl[t] = (uint8_t)(tf | TF_HEAVY);
         }
         if (!count || !fits) break;
@@ -1593,100 +1414,88 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
   }
 }
 
-// Fixed blocks -> CSR rows in input order: one wave per 64 consecutive
-// topics, whose rows are one contiguous run of the output.
-//
-// Round 4: a quarter-wave (16 lanes) copies one topic's
-// run — lane l moves ids k*16 + l of the block — so every load instruction
-// reads one 64-B line per quarter (a block is 16-B aligned: cap*4 B, cap a
-// multiple of 16... or not: the loads are then two lines) and every store
-// writes 64 contiguous bytes of the row, with no per-id owner search.  The
-// wave takes its 64 topics four at a time, two rounds per step so 8 loads per
-// lane are in flight; loads are unconditional (clamped to the run's last id:
-// a load under a branch is waited for at the branch's end) and the stores
-// are predicated.  Round 3's version (a wave scan laying the 64 runs out as
-// one range, 8 ids per lane, a 6-step LDS binary search per id to find its
-// run) stays under EGM_COMPACT_FIX_QUARTER=0 for A/B.
-// (A chunk-major variant — rank-major blocks staged through LDS and rows
-// written scattered — measured 6x slower: DESIGN.md §4.1.)
-#ifndef EGM_COMPACT_FIX_QUARTER
-#define EGM_COMPACT_FIX_QUARTER 0   // A/B (r4a): 1.19 ms against 0.97 — not kept
-#endif
-__global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact_fix(const uint32_t* __restrict__ cnt,
-                                                                    const uint32_t* __restrict__ inv,
-                                                                    const uint32_t* __restrict__ ids_fix,
-                                                                    uint32_t cap, uint32_t n,
-                                                                    const uint64_t* __restrict__ row_ptr,
-                                                                    uint32_t* __restrict__ ids, uint64_t ids_cap,
-                                                                    MatchStats* stats) {
-#if EGM_COMPACT_FIX_QUARTER
-  __shared__ uint32_t s_c[COMPACT_WAVES][64];
-  __shared__ uint64_t s_src[COMPACT_WAVES][64];
-  __shared__ uint64_t s_dst[COMPACT_WAVES][64];
-  if (!compact_checks(row_ptr, n, ids_cap, stats)) return;
+// Flush records -> CSR rows (round 5): one wave per chunk (a grid stride).
+// Lane j takes the chunk's j-th topic: its row (the walk position in
+// walk-order rows, else the input topic from the sorted record) and that row's
+// start from the scan; the wave then follows the chunk's record chain — each
+// record's 64 counts scanned into the topics' slots, its ids copied to
+// row start + the topic's running offset, an owner found per id by a 6-step
+// LDS search.  In walk-order rows a chunk's rows are one contiguous run, so
+// the copy writes whole lines (and topic[k] is written here); in input order
+// it writes each topic's piece of a record to a scattered row.  The next
+// record's header and counts are loaded before this record's ids are copied.
+// Chunks walked by k_heavy are skipped (their ids arrive as pieces, k_compact).
+constexpr int REC_WAVES = 4;
+constexpr int REC_IPL = 4;   // ids per lane per copy round in flight
+__global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __restrict__ rec, uint64_t rec_cap,
+                                                             const uint4* __restrict__ chunks,
+                                                             const uint64_t* __restrict__ order, uint32_t n,
+                                                             const uint64_t* __restrict__ row_ptr,
+                                                             uint32_t* __restrict__ topic, uint32_t* __restrict__ ids,
+                                                             uint64_t ids_cap, MatchStats* stats) {
+  __shared__ uint32_t s_ex[REC_WAVES][64];
+  __shared__ uint64_t s_dst[REC_WAVES][64];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t q = lane >> 4, l16 = lane & 15;
-  const uint32_t ngroups = (n + 63) / 64;
-  for (uint32_t g = blockIdx.x * COMPACT_WAVES + wave; g < ngroups; g += gridDim.x * COMPACT_WAVES) {
-    const uint32_t t = min(g * 64 + lane, n - 1);
-    const uint32_t p = inv[t], ct = cnt[t];   // independent loads, in flight together
-    const uint64_t rp = row_ptr[t];
-    const uint32_t c = min(ct, cap) & ((g * 64 + lane < n && p != NONE) ? 0xFFFFFFFFu : 0u);
-    s_c[wave][lane] = c;
-    s_src[wave][lane] = (uint64_t)(p != NONE ? p : 0u) * cap;
-    s_dst[wave][lane] = rp;
-    uint32_t cm = c;   // the wave's longest run: how many 16-id steps a round needs
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) cm = max(cm, (uint32_t)__shfl_xor(cm, d, 64));
-    const uint32_t steps = uni((cm + 15) / 16);
-    wave_sync();
-#pragma unroll 1
-    for (uint32_t j = 0; j < 16; j += 2) {   // topics 4j + q and 4(j+1) + q
-      const uint32_t ta = 4 * j + q, tb = ta + 4;
-      const uint32_t ca = s_c[wave][ta], cb = s_c[wave][tb];
-      const uint64_t sa = s_src[wave][ta], sb = s_src[wave][tb];
-      const uint64_t da = s_dst[wave][ta], db = s_dst[wave][tb];
-      const uint32_t la = ca ? ca - 1 : 0u, lb = cb ? cb - 1 : 0u;
-#pragma unroll 1
-      for (uint32_t k0 = 0; k0 < steps; k0 += 4) {
-        uint32_t va[4], vb[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          const uint32_t i = (k0 + k) * 16 + l16;
-          va[k] = ids_fix[sa + min(i, la)];
-          vb[k] = ids_fix[sb + min(i, lb)];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          const uint32_t i = (k0 + k) * 16 + l16;
-          if (i < ca) ids[da + i] = va[k];
-          if (i < cb) ids[db + i] = vb[k];
-        }
+  const bool ok = compact_checks(row_ptr, n, ids_cap, stats);
+  const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  for (uint32_t c = blockIdx.x * REC_WAVES + wave; c < nchunks; c += gridDim.x * REC_WAVES) {
+    const uint32_t t = c * WALK_CHUNK + lane;
+    const bool act = t < n;
+    const uint32_t my_t = act ? (order ? (uint32_t)order[t] : t) : 0u;
+    if (topic && act) topic[t] = my_t;   // written even when the rows are not (overflow): the map is the order
+    const uint4 ch = chunks[c];
+    if (!ok || !(ch.w & CHUNK_WALKED) || ch.z == 0) continue;
+    uint64_t dst = act ? row_ptr[topic ? t : my_t] : 0ull;
+    uint64_t off = (uint64_t)ch.x | ((uint64_t)ch.y << 32);
+    uint32_t guard = 0;
+    // the first record's header and counts
+    uint32_t hdr = 0, cr = 0;
+    auto load = [&](uint64_t o, uint32_t& h, uint32_t& cnt) {
+      const bool in = o + REC_IDS <= rec_cap;   // out of the slab: a broken chain (header 0 fails the tag check)
+      const uint64_t oc = in ? o : 0ull;
+      h = in ? rec[oc] : 0u;
+      cnt = ((const uint16_t*)(rec + oc + REC_HDR))[lane];
+    };
+    load(off, hdr, cr);
+    for (uint32_t r = 0; r < ch.z; ++r) {
+      if ((hdr & 0xFFFF0000u) == REC_JUMP) {   // wave-uniform: the record continues in another segment
+        off = (uint64_t)rec[off + 2] | ((uint64_t)rec[off + 3] << 32);
+        load(off, hdr, cr);
       }
+      uint32_t tot;
+      const uint32_t ex = wave_excl_scan(cr, lane, &tot);
+      if ((hdr & 0xFFFF0000u) != REC_TAG || (hdr & 0xFFFFu) != tot || ++guard > (1u << 24)) {
+        if (lane == 0) atomicOr(&stats->guard, GUARD_STACK);   // a broken chain: a bug, reported, never followed
+        break;
+      }
+      s_ex[wave][lane] = ex;
+      s_dst[wave][lane] = dst;
+      dst += cr;
+      const uint32_t* src = rec + off + REC_IDS;
+      off += rec_size(tot);
+      wave_sync();
+      if (r + 1 < ch.z) load(off, hdr, cr);   // the next record, in flight during the copy
+#pragma unroll 1
+      for (uint32_t q0 = lane; q0 < tot; q0 += 64 * REC_IPL) {
+        uint32_t v[REC_IPL];
+        uint64_t d[REC_IPL];
+#pragma unroll
+        for (int k = 0; k < REC_IPL; ++k) {
+          const uint32_t q = min(q0 + 64u * k, tot - 1);
+          uint32_t o = 0;
+#pragma unroll
+          for (uint32_t step = 32; step >= 1; step >>= 1)
+            if (s_ex[wave][o + step] <= q) o += step;
+          d[k] = s_dst[wave][o] + (q - s_ex[wave][o]);
+          v[k] = src[q];
+        }
+#pragma unroll
+        for (int k = 0; k < REC_IPL; ++k)
+          if (q0 + 64u * k < tot) ids[d[k]] = v[k];
+      }
+      wave_sync();
     }
-    wave_sync();
   }
-#else
-  __shared__ uint32_t s_scan[COMPACT_WAVES][64];
-  __shared__ uint64_t s_src[COMPACT_WAVES][64];
-  __shared__ uint64_t s_dst[COMPACT_WAVES][64];
-  if (!compact_checks(row_ptr, n, ids_cap, stats)) return;
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t ngroups = (n + 63) / 64;
-  for (uint32_t g = blockIdx.x * COMPACT_WAVES + wave; g < ngroups; g += gridDim.x * COMPACT_WAVES) {
-    const uint32_t t = min(g * 64 + lane, n - 1);
-    const uint32_t p = inv[t];
-    const uint32_t c = (g * 64 + lane < n && p != NONE) ? min(cnt[t], cap) : 0u;
-    uint32_t tot;
-    const uint32_t ex = wave_excl_scan(c, lane, &tot);
-    s_scan[wave][lane] = ex;
-    s_src[wave][lane] = (uint64_t)(p != NONE ? p : 0u) * cap;
-    s_dst[wave][lane] = row_ptr[t];
-    wave_sync();
-    copy_runs(ids_fix, ids, s_scan[wave], s_src[wave], s_dst[wave], tot, lane);
-    wave_sync();
-  }
-#endif
 }
 
 // ------------------------------------------------------------- launchers ----
@@ -1699,7 +1508,7 @@ int walk_grid_blocks(uint32_t n) {
 }
 
 // The deep pass: 10 waves per CU fit its LDS; a grid stride over the chunks handed to it.
-static int deep_grid_blocks(uint32_t n) {
+int deep_grid_blocks(uint32_t n) {
   const uint32_t chunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
   uint32_t blocks = chunks < 256u * 10u ? chunks : 256u * 10u;
   blocks = (blocks + 7) & ~7u;
@@ -1707,6 +1516,8 @@ static int deep_grid_blocks(uint32_t n) {
 }
 
 uint32_t heavy_stack_items(uint64_t max_levels) { return (uint32_t)(max_levels + 256); }
+
+uint32_t walk_stage() { return WALK_STAGE; }
 
 size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
@@ -1762,6 +1573,7 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
     return hipMemsetAsync(out.row_ptr, 0, sizeof(uint64_t), s);
   }
   MatchWork w = w_in;
+  w.walk_rows = out.topic != nullptr;
   const uint32_t kbits = min(walk_key_bits(w.key_shape), 32u);
   // (fixed-stride word offsets t * FIX_WORDS stay 32-bit below 2^29 topics)
   const bool sorted = kbits && w.order && n >= SORT_MIN_TOPICS && n < (1u << 29) && !(w.debug & DEBUG_INPUT_ORDER);
@@ -1801,11 +1613,11 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   // get a small grid (the piece count is only known on the device)
   const uint32_t cblocks =
       (uint32_t)std::min<uint64_t>(EGM_COMPACT_BLOCKS, std::max<uint64_t>(256, ((uint64_t)n + 63) / 64));
-  const uint32_t fblocks = (uint32_t)std::min<uint64_t>(
-      65536, std::max<uint64_t>(1, (((uint64_t)n + 63) / 64 + COMPACT_WAVES - 1) / COMPACT_WAVES));
-  hipLaunchKernelGGL(k_compact_fix, dim3(fblocks), dim3(64 * COMPACT_WAVES), 0, s, w.cnt, w.inv, w.ids_fix, w.fix_cap,
-                     n, out.row_ptr, out.ids, out.ids_cap, w.stats);
-  trace(s, "k_compact_fix");
+  const uint32_t rblocks = (uint32_t)std::min<uint64_t>(
+      65536, std::max<uint64_t>(1, (((uint64_t)n + 63) / 64 + REC_WAVES - 1) / REC_WAVES));
+  hipLaunchKernelGGL(k_rec_rows, dim3(rblocks), dim3(64 * REC_WAVES), 0, s, w.rec, w.rec_cap, w.chunks, w.order, n,
+                     out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats);
+  trace(s, "k_rec_rows");
   hipLaunchKernelGGL(k_compact, dim3(cblocks), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.ids_tmp, n, out.row_ptr,
                      out.ids, out.ids_cap, w.pieces_cap, w.stats);
   return hipGetLastError();

@@ -218,6 +218,13 @@ class GpuMatcher:
         self._check(self.lib.egm_match_device(self.ctx, d_blob, blob_bytes, d_off, n, mode, stream or None, d_row,
                                               d_ids, ids_cap, d_flags or None), "egm_match_device")
 
+    def match_device_ordered(self, d_blob: int, blob_bytes: int, d_off: int, n: int, mode: int, stream: int,
+                             d_row: int, d_topic: int, d_ids: int, ids_cap: int):
+        """egm_match_device with rows in the walk's order: row k is input topic d_topic[k]."""
+        self._check(self.lib.egm_match_device_ordered(self.ctx, d_blob, blob_bytes, d_off, n, mode, stream or None,
+                                                      d_row, d_topic or None, d_ids, ids_cap),
+                    "egm_match_device_ordered")
+
     def match_device_counted(self, d_blob: int, blob_bytes: int, d_off: int, n_max: int, d_n: int, mode: int,
                              stream: int, d_row: int, d_ids: int, ids_cap: int):
         """egm_match_device over a batch whose topic count (<= n_max) is at d_n on the device."""

@@ -184,6 +184,19 @@ int egm_match_cancel(egm_ctx* ctx, uint64_t ticket);
 int egm_match_device(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_offsets,
                      uint32_t n_topics, int mode, void* hip_stream, uint64_t* d_row_ptr, uint32_t* d_ids,
                      uint64_t ids_cap, uint8_t* d_flags);
+/* egm_match_device with the rows in the walk's order (round 5; SURVEY §8b,
+   the result form the NIF consumes): row k holds the matches of input topic
+   d_topic[k] (every topic exactly once), d_row_ptr[n+1] is that CSR.  The
+   walk visits topics sorted by their first levels; in this
+   form each chunk of 64 consecutive rows is one contiguous run of d_ids, so
+   no row is scattered and there is no second pass over the ids to put them
+   in input order.  The sets are egm_match_device's: topic d_topic[k]'s row
+   there equals row k here, as a set.  Asynchronous on hip_stream (NULL = the
+   HIP default stream); egm_last_stats() reports overflow (rerun with a larger
+   ids_cap). */
+int egm_match_device_ordered(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_offsets,
+                             uint32_t n_topics, int mode, void* hip_stream, uint64_t* d_row_ptr, uint32_t* d_topic,
+                             uint32_t* d_ids, uint64_t ids_cap);
 /* egm_match_device over a batch whose topic count is on the device: d_n is a
    device slot header {count, bytes, overflow, 0} (u32 x 4, egm_prefix_route's
    layout).  The first count (<= n_max) topics are matched, the rest (padding;

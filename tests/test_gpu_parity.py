@@ -206,11 +206,11 @@ def test_config_c0_heavy_path_vs_cpp_oracle(gm, mode):
 def test_walk_orders_vs_cpp_oracle(gm, mode, monkeypatch):
     """The walk's locality order (the key k_tokenise computes, the radix sort,
     the walk reading sorted topic records and fixed-stride words) and the
-    output layout (fixed per-topic blocks + spilled pieces) never change a
-    result: several key shapes, input order, a partial last
-    chunk, sorted + every chunk through k_heavy, and fixed blocks of 1-3 ids
-    (nearly every id spilled), all bit-exact against the C++ oracle
-    (egm_kernels.hip launch_match)."""
+    output path (flush records chained per chunk, k_rec_rows) never change a
+    result: several key shapes, input order, a partial last chunk, sorted +
+    every chunk through k_heavy, and records of 1..40 entries in segments of
+    64-100 u32 (every chunk's chain jumps between segments many times), all
+    bit-exact against the C++ oracle (egm_kernels.hip launch_match)."""
     f, t = synth.config("c0", n_topics=70_001)
     gm.build(f.blob, f.off)
     monkeypatch.setenv("EGM_WALK_SORT_MIN_BYTES", "0")   # sort whatever the table size
@@ -218,18 +218,84 @@ def test_walk_orders_vs_cpp_oracle(gm, mode, monkeypatch):
     o.add(f.blob, f.off)
     row, ids = o.match(t.blob, t.off, threads=8)
     want = canonical(row, ids)
-    for bits, debug, cap in (("a86", 0, 96), ("8888", 0, 96), ("444", 0, 96), ("68a6", 0, 96), ("0", 0, 96),
-                             ("a86", 4, 96), ("a86", 1, 96), ("a86", 0, 1), ("a86", 0, 3), ("0", 0, 2), ("a86", 1, 1)):
+    for bits, debug, flush_at, seg in (("a86", 0, 320, 16384), ("8888", 0, 320, 16384), ("444", 0, 320, 16384),
+                                       ("68a6", 0, 320, 16384), ("0", 0, 320, 16384), ("a86", 4, 320, 16384),
+                                       ("a86", 1, 320, 16384), ("a86", 0, 1, 64), ("a86", 0, 7, 100),
+                                       ("0", 0, 40, 64), ("a86", 1, 1, 64), ("8a86", 0, 300, 400)):
         monkeypatch.setenv("EGM_WALK_KEY", bits)   # key bits per level (hex nibbles, level 0 lowest)
-        monkeypatch.setenv("EGM_FIX_CAP", str(cap))   # ids per fixed block: small caps spill most ids into pieces
+        monkeypatch.setenv("EGM_FLUSH_AT", str(flush_at))   # staged emits per flush record
+        monkeypatch.setenv("EGM_REC_SEG", str(seg))         # u32 per record segment
         gm.set_debug(debug)   # 4: EGM_DEBUG_INPUT_ORDER, 1: EGM_DEBUG_FORCE_HEAVY
         try:
             res = gm.match(t.blob, t.off, mode)
         finally:
             gm.set_debug(0)
         assert res.n_error == 0
-        assert np.array_equal(res.row_ptr, row), (bits, debug, cap)
-        assert np.array_equal(canonical(res.row_ptr, res.ids), want), (bits, debug, cap)
+        assert np.array_equal(res.row_ptr, row), (bits, debug, flush_at, seg)
+        assert np.array_equal(canonical(res.row_ptr, res.ids), want), (bits, debug, flush_at, seg)
+
+
+def ordered_to_input(row_w, topic, ids_w):
+    """Rows in walk order (egm_match_device_ordered) -> the input-order CSR;
+    asserts topic is a permutation."""
+    n = len(topic)
+    assert np.array_equal(np.sort(topic), np.arange(n, dtype=topic.dtype))
+    cnt_w = np.diff(row_w.astype(np.int64))
+    cnt = np.zeros(n, np.int64)
+    cnt[topic] = cnt_w
+    row = np.zeros(n + 1, np.uint64)
+    row[1:] = np.cumsum(cnt)
+    out = np.empty(int(row[-1]), np.uint32)
+    for k in range(n):   # (small batches only)
+        a, b = int(row_w[k]), int(row_w[k + 1])
+        s = int(row[topic[k]])
+        out[s:s + b - a] = ids_w[a:b]
+    return row, out
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_device_ordered_vs_cpp_oracle(gm, mode, monkeypatch):
+    """egm_match_device_ordered (rows in walk order + the row -> topic map,
+    the bench's form): every topic's set equals the oracle's, sorted and
+    input-order walks, the heavy path, short records with jumps."""
+    import torch
+    f, t = synth.config("c0", n_topics=40_003)
+    gm.build(f.blob, f.off)
+    monkeypatch.setenv("EGM_WALK_SORT_MIN_BYTES", "0")
+    o = OracleTrie(True, mode)
+    o.add(f.blob, f.off)
+    row, ids = o.match(t.blob, t.off, threads=8)
+    want = canonical(row, ids)
+    dev = torch.device("cuda:0")
+    d_blob = torch.from_numpy(t.blob).to(dev)
+    d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+    n, cap = t.n, len(ids) + 1024
+    for debug, flush_at, seg in ((0, 320, 16384), (4, 320, 16384), (1, 320, 16384), (0, 3, 64)):
+        monkeypatch.setenv("EGM_FLUSH_AT", str(flush_at))
+        monkeypatch.setenv("EGM_REC_SEG", str(seg))
+        d_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        d_top = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
+        gm.set_debug(debug)
+        try:
+            gm.match_device_ordered(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, mode, 0,
+                                    d_row.data_ptr(), d_top.data_ptr(), d_ids.data_ptr(), cap)
+            st = gm.last_stats()
+        finally:
+            gm.set_debug(0)
+        assert st["overflow"] == 0 and st["errors"] == 0 and st["n_ids"] == len(ids)
+        row_w = d_row.cpu().numpy().view(np.uint64)
+        topic = d_top.cpu().numpy().view(np.uint32)
+        ids_w = d_ids.cpu().numpy().view(np.uint32)[:len(ids)]
+        if debug == 4:
+            assert np.array_equal(topic, np.arange(n, dtype=np.uint32))   # input order: the identity map
+        r2, i2 = ordered_to_input(row_w, topic, ids_w)
+        assert np.array_equal(r2, row), (debug, flush_at)
+        assert np.array_equal(canonical(r2, i2), want), (debug, flush_at)
+    # too small: overflow reported, nothing written past the buffer
+    gm.match_device_ordered(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, mode, 0, d_row.data_ptr(),
+                            d_top.data_ptr(), d_ids.data_ptr(), 16)
+    assert gm.last_stats()["overflow"] != 0
 
 
 @pytest.mark.parametrize("mode", MODES)

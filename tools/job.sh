@@ -93,7 +93,6 @@ for step in "$@"; do
       v=${step#host_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 python tools/bench_host.py ;;
     s2) run s2 400 python $R/bench.py --steps 20 --warmup 3 --streams 2 --cpu-baseline off --host-e2e off --x-orders "a86,0" ;;
-    cap128) EGM_FIX_CAP=128 run cap128 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86/128,a86/96,a86/128" ;;
     orders4) run orders4 500 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off --x-orders "a86,68a8,8a86,a86,68a8,8a86,9a8" ;;
     orders5) run orders5 600 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off --x-orders "8a86,a886,88a6,8a95,6a88,7a87,8a86,7a96,8b75" ;;
     orders) run orders 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86,0,a86/128,a86" ;;
