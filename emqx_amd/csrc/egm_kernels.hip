@@ -1426,7 +1426,7 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
 // record's header and counts are loaded before this record's ids are copied.
 // Chunks walked by k_heavy are skipped (their ids arrive as pieces, k_compact).
 constexpr int REC_WAVES = 4;
-constexpr int REC_IPL = 4;   // ids per lane per copy round in flight
+constexpr uint32_t REC_IPL = (WALK_STAGE + 63) / 64;   // a record's ids, all loaded in one round
 __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __restrict__ rec, uint64_t rec_cap,
                                                              const uint4* __restrict__ chunks,
                                                              const uint64_t* __restrict__ order, uint32_t n,
@@ -1438,6 +1438,12 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool ok = compact_checks(row_ptr, n, ids_cap, stats);
   const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  auto load = [&](uint64_t o, uint32_t& h, uint32_t& cnt) {
+    const bool in = o + REC_IDS <= rec_cap;   // out of the slab: a broken chain (header 0 fails the tag check)
+    const uint64_t oc = in ? o : 0ull;
+    h = in ? rec[oc] : 0u;
+    cnt = ((const uint16_t*)(rec + oc + REC_HDR))[lane];
+  };
   for (uint32_t c = blockIdx.x * REC_WAVES + wave; c < nchunks; c += gridDim.x * REC_WAVES) {
     const uint32_t t = c * WALK_CHUNK + lane;
     const bool act = t < n;
@@ -1447,51 +1453,40 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
     if (!ok || !(ch.w & CHUNK_WALKED) || ch.z == 0) continue;
     uint64_t dst = act ? row_ptr[topic ? t : my_t] : 0ull;
     uint64_t off = (uint64_t)ch.x | ((uint64_t)ch.y << 32);
-    uint32_t guard = 0;
-    // the first record's header and counts
-    uint32_t hdr = 0, cr = 0;
-    auto load = [&](uint64_t o, uint32_t& h, uint32_t& cnt) {
-      const bool in = o + REC_IDS <= rec_cap;   // out of the slab: a broken chain (header 0 fails the tag check)
-      const uint64_t oc = in ? o : 0ull;
-      h = in ? rec[oc] : 0u;
-      cnt = ((const uint16_t*)(rec + oc + REC_HDR))[lane];
-    };
+    uint32_t hdr, cr;
     load(off, hdr, cr);
     for (uint32_t r = 0; r < ch.z; ++r) {
-      if ((hdr & 0xFFFF0000u) == REC_JUMP) {   // wave-uniform: the record continues in another segment
+      if ((hdr & 0xFFFF0000u) == REC_JUMP) {   // wave-uniform: the chain continues in another segment
         off = (uint64_t)rec[off + 2] | ((uint64_t)rec[off + 3] << 32);
         load(off, hdr, cr);
       }
       uint32_t tot;
       const uint32_t ex = wave_excl_scan(cr, lane, &tot);
-      if ((hdr & 0xFFFF0000u) != REC_TAG || (hdr & 0xFFFFu) != tot || ++guard > (1u << 24)) {
+      if ((hdr & 0xFFFF0000u) != REC_TAG || (hdr & 0xFFFFu) != tot || tot > WALK_STAGE) {
         if (lane == 0) atomicOr(&stats->guard, GUARD_STACK);   // a broken chain: a bug, reported, never followed
         break;
       }
       s_ex[wave][lane] = ex;
       s_dst[wave][lane] = dst;
       dst += cr;
+      // this record's ids (one round: tot <= WALK_STAGE), then the next record's header, all in flight together
       const uint32_t* src = rec + off + REC_IDS;
-      off += rec_size(tot);
-      wave_sync();
-      if (r + 1 < ch.z) load(off, hdr, cr);   // the next record, in flight during the copy
-#pragma unroll 1
-      for (uint32_t q0 = lane; q0 < tot; q0 += 64 * REC_IPL) {
-        uint32_t v[REC_IPL];
-        uint64_t d[REC_IPL];
+      uint32_t v[REC_IPL];
 #pragma unroll
-        for (int k = 0; k < REC_IPL; ++k) {
-          const uint32_t q = min(q0 + 64u * k, tot - 1);
+      for (uint32_t k = 0; k < REC_IPL; ++k) v[k] = src[min(lane + 64u * k, tot ? tot - 1 : 0u)];
+      off += rec_size(tot);
+      if (r + 1 < ch.z) load(off, hdr, cr);
+      wave_sync();
+#pragma unroll
+      for (uint32_t k = 0; k < REC_IPL; ++k) {
+        const uint32_t q = lane + 64u * k;
+        if (q < tot) {
           uint32_t o = 0;
 #pragma unroll
           for (uint32_t step = 32; step >= 1; step >>= 1)
             if (s_ex[wave][o + step] <= q) o += step;
-          d[k] = s_dst[wave][o] + (q - s_ex[wave][o]);
-          v[k] = src[q];
+          ids[s_dst[wave][o] + (q - s_ex[wave][o])] = v[k];
         }
-#pragma unroll
-        for (int k = 0; k < REC_IPL; ++k)
-          if (q0 + 64u * k < tot) ids[d[k]] = v[k];
       }
       wave_sync();
     }
