@@ -148,7 +148,7 @@ inline uint32_t ticket_gen(uint64_t t) { return (uint32_t)(t >> 16); }
 struct MatchWs {
   DevBuf wid, lv, tfl, cnt, ids_tmp, pieces, deferred, heavy_stack, tile_sums, stats;
   DevBuf skey, skey_out, sval, order, wfix, sort_tmp;   // walk-order sort
-  DevBuf rec, chunks;                                    // flush records and their per-chunk chains (k_rec_rows)
+  DevBuf rec, chunks, dir;                               // flush records, per-chunk chains and directories
   uint64_t pieces_cap = 0, ids_tmp_cap = 0, rec_cap = 0;
   uint32_t rec_grain = REC_GRAIN, flush_lim = 0;
   uint32_t heavy_cap = 0;        // stack items per heavy wave
@@ -647,7 +647,10 @@ static int ensure_work(egm_ctx* c, MatchWs& W, uint32_t n, uint64_t blob_bytes, 
   const uint64_t rcap = rec_capacity(ids_cap, n, W.flush_lim, W.rec_grain);
   if ((e = W.rec.ensure(rcap * 4)) != hipSuccess) return c->hip_fail(e, "flush records");
   W.rec_cap = W.rec.cap / 4;
+  if (W.rec_cap >= (1ull << 34)) return c->fail(EGM_E_INVAL, "batch too large: > 16G u32 of flush records (split it)");
   if ((e = W.chunks.ensure(((uint64_t)n / WALK_CHUNK + 2) * 16)) != hipSuccess) return c->hip_fail(e, "chunk records");
+  if ((e = W.dir.ensure(((uint64_t)n / WALK_CHUNK + 2) * REC_DIR * 4)) != hipSuccess)
+    return c->hip_fail(e, "chunk directories");
   // heavy topics: their ids (count then fill, one piece per topic)
   const uint64_t tcap = ids_cap + 4096;
   if (tcap >= 0xFFFFFFF0ull) return c->fail(EGM_E_INVAL, "batch too large: > 4G matched ids (split it)");
@@ -688,6 +691,7 @@ static MatchWork work_view(egm_ctx* c, MatchWs& W) {
   w.rec_grain = W.rec_grain;
   w.flush_lim = W.flush_lim;
   w.chunks = W.chunks.as<uint4>();
+  w.dir = W.dir.as<uint32_t>();
   w.ids_tmp = W.ids_tmp.as<uint32_t>();
   w.ids_cap = W.ids_tmp_cap;   // ids_tmp entries (the output capacity is MatchOut's)
   w.pieces = W.pieces.as<uint4>();

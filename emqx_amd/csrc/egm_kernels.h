@@ -60,6 +60,7 @@ constexpr uint32_t REC_IDS = REC_HDR + 32;        // u32 before the ids
 constexpr uint32_t REC_TAG = 0x5EC0u << 16;
 constexpr uint32_t REC_JUMP = 0x4A4Du << 16;
 constexpr uint32_t REC_GRAIN = 16384;             // default u32 per segment (EGM_REC_SEG)
+constexpr uint32_t REC_DIR = 64;                  // record offsets per chunk in its directory (longer: the chain)
 __host__ __device__ constexpr uint32_t rec_size(uint32_t n_entries) { return (REC_IDS + n_entries + 3u) & ~3u; }
 // Per chunk (uint4): {first record lo, first record hi, records, flags}.
 constexpr uint32_t CHUNK_WALKED = 1u;             // walked by k_walk (either pass): its records hold its ids
@@ -76,6 +77,7 @@ struct MatchWork {                // per-batch device workspace
   uint32_t rec_grain;             // u32 per record segment
   uint32_t flush_lim;             // staged emits that trigger a flush (<= WALK_STAGE; smaller: tests)
   uint4* chunks;                  // [n / CHUNK + 1] ChunkRec per chunk
+  uint32_t* dir;                  // [(n / CHUNK + 1) * REC_DIR] each chunk's first REC_DIR record offsets / 4
   uint32_t* ids_tmp;              // [ids_cap] ids of heavy topics (one piece each)
   uint64_t ids_cap;
   uint4* pieces;                  // [pieces_cap] {row, count, ids_tmp offset, 0}

@@ -533,6 +533,7 @@ struct RecCursor {
   unsigned long long cur, end;     // free space [cur, end - REC_HDR) of the segment ({0, 0}: none yet)
   unsigned long long first;        // the chunk's first record
   uint32_t nrec;                   // the chunk's records so far
+  uint32_t roff;                   // per lane: lane r holds the chunk's record r (offset / 4; r < REC_DIR)
 };
 
 #ifndef EGM_FLUSH_NT
@@ -589,6 +590,7 @@ __device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t la
   const unsigned long long base = rc.cur;
   rc.cur += size;
   if (rc.nrec == 0) rc.first = base;
+  if (lane == rc.nrec) rc.roff = (uint32_t)(base >> 2);
   rc.nrec += 1;
   const bool ok = base + size <= w.rec_cap;
   if (!ok && lane == 0) atomicOr(&w.stats->overflow, 1u);
@@ -844,7 +846,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
   root.w = uni(root.w);
   uint32_t created = 0;
   unsigned long long iters = 0, popped = 0, bounded = 0, lit_probes = 0, plus_reads = 0;
-  RecCursor rc{0, 0, 0, 0};
+  RecCursor rc{0, 0, 0, 0, 0};
   const uint32_t guard_lim = (w.debug & DEBUG_FORCE_GUARD) ? 2u : (1u << EGM_GUARD_BITS);
   // sorted batch: the record of the chunk's j-th topic in walk order, loaded
   // one chunk ahead (a grid stride: the wave's next chunk is c + gridDim.x)
@@ -1077,6 +1079,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
     if (nstage) flush_stage(L, nstage, lane, w, rc);
     if (lane < nt) w.cnt[w.walk_rows ? t0 + lane : my_t] = L.cnt[lane];
     if (lane == 0) w.chunks[c] = make_uint4((uint32_t)rc.first, (uint32_t)(rc.first >> 32), rc.nrec, CHUNK_WALKED);
+    if (lane < min(rc.nrec, REC_DIR)) w.dir[(uint64_t)c * REC_DIR + lane] = rc.roff;   // the chunk's directory
     wave_sync();
   }
   if (!DEEP && n_pend) deep_flush(w, deep_c, n_pend, lane);
@@ -1417,18 +1420,27 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
 // Flush records -> CSR rows (round 5): one wave per chunk (a grid stride).
 // Lane j takes the chunk's j-th topic: its row (the walk position in
 // walk-order rows, else the input topic from the sorted record) and that row's
-// start from the scan; the wave then follows the chunk's record chain — each
-// record's 64 counts scanned into the topics' slots, its ids copied to
-// row start + the topic's running offset, an owner found per id by a 6-step
-// LDS search.  In walk-order rows a chunk's rows are one contiguous run, so
-// the copy writes whole lines (and topic[k] is written here); in input order
-// it writes each topic's piece of a record to a scattered row.  The next
-// record's header and counts are loaded before this record's ids are copied.
-// Chunks walked by k_heavy are skipped (their ids arrive as pieces, k_compact).
+// start from the scan.  The chunk's records come from its directory (the
+// walk's record offsets, REC_DIR of them; a longer chunk continues along the
+// chain), so the loads of record r + 1 — header, counts and all its ids — are
+// in flight while record r is placed: its 64 counts scanned into the topics'
+// slots, each id stored at row start + the topic's running offset (an owner
+// found per id by a 6-step LDS search).  In walk-order rows a chunk's rows are
+// one contiguous run (and topic[k] is written here); in input order each
+// topic's piece of a record goes to a scattered row.  A chunk is placed in
+// about one memory round trip, so its partly written output lines are still
+// in L2 when the next record completes them.  Chunks walked by k_heavy are
+// skipped (their ids arrive as pieces, k_compact).
 constexpr int REC_WAVES = 4;
 constexpr uint32_t REC_IPL = (WALK_STAGE + 63) / 64;   // a record's ids, all loaded in one round
+struct RecLoad {
+  uint64_t off;
+  uint32_t hdr, cr;
+  uint32_t v[REC_IPL];
+};
 __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __restrict__ rec, uint64_t rec_cap,
                                                              const uint4* __restrict__ chunks,
+                                                             const uint32_t* __restrict__ dir,
                                                              const uint64_t* __restrict__ order, uint32_t n,
                                                              const uint64_t* __restrict__ row_ptr,
                                                              uint32_t* __restrict__ topic, uint32_t* __restrict__ ids,
@@ -1438,11 +1450,15 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool ok = compact_checks(row_ptr, n, ids_cap, stats);
   const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
-  auto load = [&](uint64_t o, uint32_t& h, uint32_t& cnt) {
-    const bool in = o + REC_IDS <= rec_cap;   // out of the slab: a broken chain (header 0 fails the tag check)
+  // every load of one record (out of the slab: header 0, which fails the tag check)
+  auto issue = [&](uint64_t o, RecLoad& L) {
+    const bool in = o + REC_IDS <= rec_cap;
     const uint64_t oc = in ? o : 0ull;
-    h = in ? rec[oc] : 0u;
-    cnt = ((const uint16_t*)(rec + oc + REC_HDR))[lane];
+    L.off = o;
+    L.hdr = in ? rec[oc] : 0u;
+    L.cr = ((const uint16_t*)(rec + oc + REC_HDR))[lane];
+#pragma unroll
+    for (uint32_t k = 0; k < REC_IPL; ++k) L.v[k] = rec[min(oc + REC_IDS + lane + 64u * k, rec_cap - 1)];
   };
   for (uint32_t c = blockIdx.x * REC_WAVES + wave; c < nchunks; c += gridDim.x * REC_WAVES) {
     const uint32_t t = c * WALK_CHUNK + lane;
@@ -1451,32 +1467,29 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
     if (topic && act) topic[t] = my_t;   // written even when the rows are not (overflow): the map is the order
     const uint4 ch = chunks[c];
     if (!ok || !(ch.w & CHUNK_WALKED) || ch.z == 0) continue;
+    const uint32_t nrec = ch.z;
     uint64_t dst = act ? row_ptr[topic ? t : my_t] : 0ull;
-    uint64_t off = (uint64_t)ch.x | ((uint64_t)ch.y << 32);
-    uint32_t hdr, cr;
-    load(off, hdr, cr);
-    for (uint32_t r = 0; r < ch.z; ++r) {
-      if ((hdr & 0xFFFF0000u) == REC_JUMP) {   // wave-uniform: the chain continues in another segment
-        off = (uint64_t)rec[off + 2] | ((uint64_t)rec[off + 3] << 32);
-        load(off, hdr, cr);
-      }
+    const uint32_t roff = lane < min(nrec, REC_DIR) ? dir[(uint64_t)c * REC_DIR + lane] : 0u;
+    RecLoad A, B;
+    issue((uint64_t)ch.x | ((uint64_t)ch.y << 32), A);
+    for (uint32_t r = 0; r < nrec; ++r) {
+      const bool next_dir = r + 1 < nrec && r + 1 < REC_DIR;
+      if (next_dir) issue((uint64_t)(uint32_t)__shfl((int)roff, (int)(r + 1), 64) << 2, B);   // in flight now
       uint32_t tot;
-      const uint32_t ex = wave_excl_scan(cr, lane, &tot);
-      if ((hdr & 0xFFFF0000u) != REC_TAG || (hdr & 0xFFFFu) != tot || tot > WALK_STAGE) {
-        if (lane == 0) atomicOr(&stats->guard, GUARD_STACK);   // a broken chain: a bug, reported, never followed
+      const uint32_t ex = wave_excl_scan(A.cr, lane, &tot);
+      if ((A.hdr & 0xFFFF0000u) != REC_TAG || (A.hdr & 0xFFFFu) != tot || tot > WALK_STAGE) {
+        if (lane == 0) atomicOr(&stats->guard, GUARD_STACK);   // a broken directory or chain: a bug, reported
         break;
       }
       s_ex[wave][lane] = ex;
       s_dst[wave][lane] = dst;
-      dst += cr;
-      // this record's ids (one round: tot <= WALK_STAGE), then the next record's header, all in flight together
-      const uint32_t* src = rec + off + REC_IDS;
-      uint32_t v[REC_IPL];
-#pragma unroll
-      for (uint32_t k = 0; k < REC_IPL; ++k) v[k] = src[min(lane + 64u * k, tot ? tot - 1 : 0u)];
-      off += rec_size(tot);
-      if (r + 1 < ch.z) load(off, hdr, cr);
+      dst += A.cr;
       wave_sync();
+#ifdef EGM_AB_REC_STORE   // measurement only: 0 = no id stores
+#pragma unroll
+      for (uint32_t k = 0; k < REC_IPL; ++k)
+        if (A.v[k] == 0x7FFFFFF1u) ids[0] = A.v[k];
+#else
 #pragma unroll
       for (uint32_t k = 0; k < REC_IPL; ++k) {
         const uint32_t q = lane + 64u * k;
@@ -1485,10 +1498,18 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
 #pragma unroll
           for (uint32_t step = 32; step >= 1; step >>= 1)
             if (s_ex[wave][o + step] <= q) o += step;
-          ids[s_dst[wave][o] + (q - s_ex[wave][o])] = v[k];
+          ids[s_dst[wave][o] + (q - s_ex[wave][o])] = A.v[k];
         }
       }
+#endif
       wave_sync();
+      if (r + 1 < nrec && !next_dir) {   // past the directory: the chain (rare: a chunk of > REC_DIR records)
+        uint64_t o = A.off + rec_size(tot);
+        if (o + REC_HDR <= rec_cap && (rec[o] & 0xFFFF0000u) == REC_JUMP)   // wave-uniform
+          o = (uint64_t)rec[o + 2] | ((uint64_t)rec[o + 3] << 32);
+        issue(o, B);
+      }
+      A = B;
     }
   }
 }
@@ -1610,8 +1631,8 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
       (uint32_t)std::min<uint64_t>(EGM_COMPACT_BLOCKS, std::max<uint64_t>(256, ((uint64_t)n + 63) / 64));
   const uint32_t rblocks = (uint32_t)std::min<uint64_t>(
       65536, std::max<uint64_t>(1, (((uint64_t)n + 63) / 64 + REC_WAVES - 1) / REC_WAVES));
-  hipLaunchKernelGGL(k_rec_rows, dim3(rblocks), dim3(64 * REC_WAVES), 0, s, w.rec, w.rec_cap, w.chunks, w.order, n,
-                     out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats);
+  hipLaunchKernelGGL(k_rec_rows, dim3(rblocks), dim3(64 * REC_WAVES), 0, s, w.rec, w.rec_cap, w.chunks, w.dir,
+                     w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats);
   trace(s, "k_rec_rows");
   hipLaunchKernelGGL(k_compact, dim3(cblocks), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.ids_tmp, n, out.row_ptr,
                      out.ids, out.ids_cap, w.pieces_cap, w.stats);

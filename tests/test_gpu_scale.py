@@ -178,6 +178,34 @@ class TestC2Full:
         assert np.array_equal(got_sum, row_checksums(res.row_ptr, res.ids))
         assert max(sizes) < 0.45 * f.n, sizes   # a partition, not a replica (37 % at 8 ranks)
 
+    def test_c2_full_ordered_rows(self, c2):
+        """The bench's result form at full size: egm_match_device_ordered (rows
+        in walk order + the row -> topic map).  The map is a permutation and
+        every topic's row equals its row of the oracle-checked input-order
+        result (count and an order-independent checksum)."""
+        import torch
+        t, res, gm = c2["t"], c2["res"], c2["gm"]
+        dev = torch.device("cuda:0")
+        n, cap = t.n, int(res.row_ptr[-1]) + 4096
+        d_blob = torch.from_numpy(t.blob).to(dev)
+        d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
+        d_row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        d_top = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        d_ids = torch.zeros(cap, dtype=torch.int32, device=dev)
+        gm.match_device_ordered(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES, 0,
+                                d_row.data_ptr(), d_top.data_ptr(), d_ids.data_ptr(), cap)
+        st = gm.last_stats()
+        assert st["overflow"] == 0 and st["errors"] == 0 and st["n_ids"] == int(res.row_ptr[-1])
+        row_w = d_row.cpu().numpy().view(np.uint64)
+        topic = d_top.cpu().numpy().view(np.uint32).astype(np.int64)
+        ids_w = d_ids[:st["n_ids"]].cpu().numpy().view(np.uint32)
+        del d_ids, d_row, d_top, d_blob, d_off
+        assert np.array_equal(np.sort(topic), np.arange(n))
+        assert np.count_nonzero(topic != np.arange(n)) > n // 2   # the walk's order, not the input's
+        want_cnt = np.diff(res.row_ptr).astype(np.int64)
+        assert np.array_equal(np.diff(row_w).astype(np.int64), want_cnt[topic])
+        assert np.array_equal(row_checksums(row_w, ids_w), row_checksums(res.row_ptr, res.ids)[topic])
+
     def test_c2_full_determinism(self, c2):
         t, res, gm = c2["t"], c2["res"], c2["gm"]
         again = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
@@ -272,28 +300,32 @@ def test_c4_full_size_match_and_fanout():
         torch.cuda.synchronize()
         drow = d_drow.cpu().numpy().view(np.uint64)
         assert np.array_equal(drow, dpos[mrow.astype(np.int64)])   # every delivery row
-        rng = np.random.default_rng(5)
-        for i in rng.choice(n, 3_000, replace=False):
+        # the rows checked id-exact against the oracle below, and 3K of them
+        # whose delivery lists are also checked against the oracle's ids
+        # (the delivery check used the GPU's own match ids only)
+        idx = np.sort(np.random.default_rng(4).choice(n, 20_000, replace=False))
+        dsel = np.sort(np.random.default_rng(5).choice(idx, 3_000, replace=False))
+        got_dl = {}
+        for i in dsel:
             a, b = int(mrow[i]), int(mrow[i + 1])
-            wf, ws = _expected_deliveries(mids[a:b], srow, subs)
+            wf, ws = _expected_deliveries(mids[a:b], srow, subs)   # dispatch order of the GPU's match row
             lo, hi = int(drow[i]), int(drow[i + 1])
             assert hi - lo == len(wf)
-            if hi > lo:
-                assert np.array_equal(d_fid[lo:hi].cpu().numpy().view(np.uint32), wf), i
-                assert np.array_equal(d_sub[lo:hi].cpu().numpy().view(np.uint32), ws), i
+            gf = d_fid[lo:hi].cpu().numpy().view(np.uint32).copy()
+            gs = d_sub[lo:hi].cpu().numpy().view(np.uint32).copy()
+            assert np.array_equal(gf, wf) and np.array_equal(gs, ws), i
+            got_dl[int(i)] = (gf, gs)
         grp = d_sub[: min(tot, 50_000_000)].cpu().numpy().view(np.uint32)
         assert np.count_nonzero(grp & np.uint32(L.GROUP_BIT)) > 0   # (filter, group) entries, never members
         del d_fid, d_sub, d_ids, grp
         torch.cuda.empty_cache()
         gm.close()
         gm = None
-        del srow, subs
         # the oracle, 10 disjoint shards of 10M filters
         t0 = time.time()
         shards = _oracle_shards(f, 10, L.EGM_MODE_ROUTES, par=10)
         print(f"[c4] oracle shards built in {time.time() - t0:.0f}s", flush=True)
         want = np.zeros(n, np.uint64)
-        idx = np.sort(np.random.default_rng(4).choice(n, 20_000, replace=False))
         sub = t.subset(idx)
         parts = []
         for o in shards:
@@ -308,6 +340,15 @@ def test_c4_full_size_match_and_fanout():
         grow, gids = sampled_rows(mrow, mids, idx)
         assert np.array_equal(grow, orow)
         assert np.array_equal(canonical(grow, gids), canonical(orow, oids))
+        # delivery multisets from the ORACLE's match ids (emqx_broker.erl:283-308)
+        pos = {int(i): k for k, i in enumerate(idx)}
+        for i, (gf, gs) in got_dl.items():
+            k = pos[i]
+            of = oids[int(orow[k]):int(orow[k + 1])]
+            wf, ws = _expected_deliveries(of, srow, subs)
+            want_pairs = np.sort(wf.astype(np.uint64) << np.uint64(32) | ws.astype(np.uint64))
+            got_pairs = np.sort(gf.astype(np.uint64) << np.uint64(32) | gs.astype(np.uint64))
+            assert np.array_equal(got_pairs, want_pairs), i
     finally:
         if gm is not None:
             gm.close()
