@@ -1514,6 +1514,122 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
   }
 }
 
+// The staged form of k_rec_rows (round 5, the default): the chunk's output
+// is assembled in LDS and written out as whole lines.  k_rec_rows stores each
+// record's ~5-id run per topic straight to its row; a line of the chunk's
+// output is completed by ~6 records over the chunk's placement, and with
+// thousands of chunks in progress the partly written lines left L2 first:
+// 4.1 GB written per C2 batch for 1.99 GB of ids (PMC, r5g).  Here one wave
+// per chunk places every record's ids into an LDS window of REC_STAGE ids of
+// the chunk's output (topic j's ids at its chunk offset + the ids of j in
+// earlier records + rank), then writes the window out: one contiguous run in
+// walk-order rows, a contiguous run per row in input order.  A chunk with
+// more ids than the window is placed window by window (its records re-read).
+// The next record's loads are in flight while one is placed (the directory).
+#ifndef EGM_REC_STAGE
+#define EGM_REC_STAGE 4096   // ids per LDS window (16 KB: 10 waves per CU)
+#endif
+constexpr uint32_t REC_STAGE = EGM_REC_STAGE;
+__global__ __launch_bounds__(64) void k_rec_rows_staged(const uint32_t* __restrict__ rec, uint64_t rec_cap,
+                                                        const uint4* __restrict__ chunks,
+                                                        const uint32_t* __restrict__ dir,
+                                                        const uint64_t* __restrict__ order, uint32_t n,
+                                                        const uint64_t* __restrict__ row_ptr,
+                                                        uint32_t* __restrict__ topic, uint32_t* __restrict__ ids,
+                                                        uint64_t ids_cap, MatchStats* stats) {
+  __shared__ uint32_t stage[REC_STAGE];
+  __shared__ uint32_t s_ex[64], s_pos[64], s_co[64];
+  __shared__ uint64_t s_rs[64];
+  const uint32_t lane = threadIdx.x;
+  const bool ok = compact_checks(row_ptr, n, ids_cap, stats);
+  const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  auto issue = [&](uint64_t o, RecLoad& L) {
+    const bool in = o + REC_IDS <= rec_cap;
+    const uint64_t oc = in ? o : 0ull;
+    L.off = o;
+    L.hdr = in ? rec[oc] : 0u;
+    L.cr = ((const uint16_t*)(rec + oc + REC_HDR))[lane];
+#pragma unroll
+    for (uint32_t k = 0; k < REC_IPL; ++k) L.v[k] = rec[min(oc + REC_IDS + lane + 64u * k, rec_cap - 1)];
+  };
+  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uint32_t t = c * WALK_CHUNK + lane;
+    const bool act = t < n;
+    const uint32_t my_t = act ? (order ? (uint32_t)order[t] : t) : 0u;
+    if (topic && act) topic[t] = my_t;   // written even when the rows are not (overflow): the map is the order
+    const uint4 ch = chunks[c];
+    if (!ok || !(ch.w & CHUNK_WALKED) || ch.z == 0) continue;
+    const uint32_t nrec = ch.z;
+    const uint32_t row = topic ? t : my_t;
+    const uint64_t rs = act ? row_ptr[row] : 0ull;
+    const uint32_t cnt = act ? (uint32_t)(row_ptr[row + 1] - rs) : 0u;
+    uint32_t T;
+    const uint32_t co = wave_excl_scan(cnt, lane, &T);   // the topic's offset in the chunk's output
+    s_co[lane] = co;
+    s_rs[lane] = rs;
+    const uint32_t roff = lane < min(nrec, REC_DIR) ? dir[(uint64_t)c * REC_DIR + lane] : 0u;
+    bool broken = false;
+    for (uint32_t w0 = 0; w0 < T && !broken; w0 += REC_STAGE) {
+      const uint32_t w1 = min(T, w0 + REC_STAGE);
+      uint32_t before = 0;   // lane j: ids of topic j in the records placed so far
+      RecLoad A, B;
+      issue((uint64_t)ch.x | ((uint64_t)ch.y << 32), A);
+      for (uint32_t r = 0; r < nrec; ++r) {
+        const bool next_dir = r + 1 < nrec && r + 1 < REC_DIR;
+        if (next_dir) issue((uint64_t)(uint32_t)__shfl((int)roff, (int)(r + 1), 64) << 2, B);   // in flight now
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan(A.cr, lane, &tot);
+        if ((A.hdr & 0xFFFF0000u) != REC_TAG || (A.hdr & 0xFFFFu) != tot || tot > WALK_STAGE) {
+          if (lane == 0) atomicOr(&stats->guard, GUARD_STACK);   // a broken directory or chain: a bug, reported
+          broken = true;
+          break;
+        }
+        s_ex[lane] = ex;
+        s_pos[lane] = co + before - ex;   // + entry index q = the entry's offset in the chunk's output
+        before += A.cr;
+        wave_sync();
+#pragma unroll
+        for (uint32_t k = 0; k < REC_IPL; ++k) {
+          const uint32_t q = lane + 64u * k;
+          if (q < tot) {
+            uint32_t o = 0;
+#pragma unroll
+            for (uint32_t step = 32; step >= 1; step >>= 1)
+              if (s_ex[o + step] <= q) o += step;
+            const uint32_t p = s_pos[o] + q;
+            if (p >= w0 && p < w1) stage[p - w0] = A.v[k];
+          }
+        }
+        wave_sync();
+        if (r + 1 < nrec && !next_dir) {   // past the directory: the chain (rare: a chunk of > REC_DIR records)
+          uint64_t o = A.off + rec_size(tot);
+          if (o + REC_HDR <= rec_cap && (rec[o] & 0xFFFF0000u) == REC_JUMP)   // wave-uniform
+            o = (uint64_t)rec[o + 2] | ((uint64_t)rec[o + 3] << 32);
+          issue(o, B);
+        }
+        A = B;
+      }
+      if (broken) break;
+      // the window out: whole lines
+      if (topic) {   // walk-order rows: the chunk's rows are one run from the first topic's row
+        const uint64_t base = s_rs[0];
+#pragma unroll 4
+        for (uint32_t p = w0 + lane; p < w1; p += 64) ids[base + p] = stage[p - w0];
+      } else {       // input order: a run per row
+#pragma unroll 4
+        for (uint32_t p = w0 + lane; p < w1; p += 64) {
+          uint32_t o = 0;
+#pragma unroll
+          for (uint32_t step = 32; step >= 1; step >>= 1)
+            if (s_co[o + step] <= p) o += step;
+          ids[s_rs[o] + (p - s_co[o])] = stage[p - w0];
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
 // ------------------------------------------------------------- launchers ----
 // One wave per block; a grid stride over the chunks beyond 32 waves per CU.
 int walk_grid_blocks(uint32_t n) {
@@ -1629,10 +1745,17 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   // get a small grid (the piece count is only known on the device)
   const uint32_t cblocks =
       (uint32_t)std::min<uint64_t>(EGM_COMPACT_BLOCKS, std::max<uint64_t>(256, ((uint64_t)n + 63) / 64));
+#ifndef EGM_REC_ROWS_DIRECT
+  // one wave per chunk, as many as fit (10 per CU with a 16 KB window), a grid stride over the chunks
+  const uint32_t rblocks = (uint32_t)std::min<uint64_t>(256ull * 10, std::max<uint64_t>(1, ((uint64_t)n + 63) / 64));
+  hipLaunchKernelGGL(k_rec_rows_staged, dim3(rblocks), dim3(64), 0, s, w.rec, w.rec_cap, w.chunks, w.dir,
+                     w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats);
+#else   // A/B: each record's runs stored straight to the rows
   const uint32_t rblocks = (uint32_t)std::min<uint64_t>(
       65536, std::max<uint64_t>(1, (((uint64_t)n + 63) / 64 + REC_WAVES - 1) / REC_WAVES));
   hipLaunchKernelGGL(k_rec_rows, dim3(rblocks), dim3(64 * REC_WAVES), 0, s, w.rec, w.rec_cap, w.chunks, w.dir,
                      w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats);
+#endif
   trace(s, "k_rec_rows");
   hipLaunchKernelGGL(k_compact, dim3(cblocks), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.ids_tmp, n, out.row_ptr,
                      out.ids, out.ids_cap, w.pieces_cap, w.stats);
