@@ -130,6 +130,7 @@ for step in "$@"; do
     ab_*)   # A/B variant built by tools/build_variant.py: C2 bench under rocprof stats
       v=${step#ab_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$v" -o run --output-format csv -- $B --steps 10 --warmup 2 --cpu-baseline off --host-e2e off ;;
+    chunkhist) run chunkhist 600 env PYTHONPATH=$R python $R/tools/chunk_hist.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
