@@ -62,7 +62,11 @@ class Broker:
         self._rr: Dict[Tuple[bytes, bytes], int] = {}
         self._sticky: Dict[Tuple[bytes, bytes], int] = {}
         self._shards = shards
-        self._csr_dirty = True
+        # the GPU subscriber table (egm_subs_*): built once, then kept by deltas
+        self._built = False
+        self._d_add: List[Tuple[bytes, int]] = []   # (filter, subscriber entry) since the last commit
+        self._d_del: List[Tuple[bytes, int]] = []
+        self.subscriptions: Dict[int, set] = {}     # ?SUBSCRIPTION: sub -> {(filter, group or None)}
         self.dead: set = set()   # subscribers whose process is gone (is_process_alive/1 false)
         self.metrics = {"messages.publish": 0, "messages.dropped": 0, "messages.dropped.no_subscribers": 0,
                         "messages.forward": 0}
@@ -86,6 +90,7 @@ class Broker:
             if len(subs) > SHARD_THRESHOLD:
                 self.shard_of[(flt, sub_id)] = zlib.crc32(str(sub_id).encode()) % self._shards + 1
             self.router.do_add_route(flt, self.node)
+            self._d_add.append((flt, sub_id))
         else:
             mem = self.shared.setdefault((group, flt), [])
             if sub_id in mem:
@@ -95,17 +100,24 @@ class Broker:
                 self.group_ids[group] = len(self.group_names)
                 self.group_names.append(group)
             self.router.do_add_route(flt, ("group", group))
-        self._csr_dirty = True
+            if len(mem) == 1:   # the (filter, group) entry: one per group, whatever its members
+                self._d_add.append((flt, GROUP_BIT | self.group_ids[group]))
+        self.subscriptions.setdefault(sub_id, set()).add((flt, group))
         return "ok"
 
     def unsubscribe(self, topic: bytes, sub_id: int, opts: Optional[dict] = None):
         flt, o = parse(topic, opts)
         group = o.get("share")
+        self._unsubscribe(flt, group, sub_id)
+        return "ok"
+
+    def _unsubscribe(self, flt: bytes, group, sub_id: int):
         if group is None:
             subs = self.subscribers.get(flt, [])
             if sub_id in subs:
                 subs.remove(sub_id)
                 self.shard_of.pop((flt, sub_id), None)
+                self._d_del.append((flt, sub_id))
                 if not subs:
                     del self.subscribers[flt]
                     self.router.do_delete_route(flt, self.node)
@@ -115,16 +127,45 @@ class Broker:
                 mem.remove(sub_id)
                 if not mem:
                     del self.shared[(group, flt)]
+                    self._d_del.append((flt, GROUP_BIT | self.group_ids[group]))
                     self.router.do_delete_route(flt, ("group", group))
-        self._csr_dirty = True
-        return "ok"
+        s = self.subscriptions.get(sub_id)
+        if s is not None:
+            s.discard((flt, group))
+            if not s:
+                del self.subscriptions[sub_id]
+
+    def subscriber_down(self, sub_id: int):
+        """emqx_broker:subscriber_down/1 (emqx_broker.erl:331-345, driven by
+        emqx_broker_helper's monitor, emqx_broker_helper.erl:133-163; a $share
+        member by emqx_shared_sub's): every subscription of the dead subscriber
+        is removed, and a filter left without subscribers loses its route."""
+        for flt, group in sorted(self.subscriptions.get(sub_id, ()), key=lambda x: (x[0], x[1] or b"")):
+            self._unsubscribe(flt, group, sub_id)
+        self.dead.discard(sub_id)
 
     # -- fan-out table ------------------------------------------------------------
     def _upload_csr(self):
-        if not self._csr_dirty:
-            return
+        """The GPU subscriber table before a publish: built once (egm_subs_build),
+        then every subscribe / unsubscribe / subscriber_down since the last
+        publish goes in as one delta and one epoch (egm_subs_apply_delta +
+        egm_subs_commit) instead of a rebuild."""
         r = self.router
         r.commit()
+        if self._built:
+            if self._d_add or self._d_del:
+                fid = r.filter_id
+                add = [(fid(f), s) for f, s in self._d_add]
+                dele = [(fid(f), s) for f, s in self._d_del if fid(f) is not None]
+                # (an add and a later delete of the same pair in one delta: the delete
+                # applies after; a re-add after a delete must come after it)
+                self._apply_ordered(add, dele)
+                r.m.subs_commit()
+                self._d_add.clear()
+                self._d_del.clear()
+            return
+        self._d_add.clear()
+        self._d_del.clear()
         n = r._next
         lists: List[List[int]] = [[] for _ in range(n)]
         for flt, subs in self.subscribers.items():
@@ -135,7 +176,25 @@ class Broker:
         row[1:] = np.cumsum([len(x) for x in lists]) if n else []
         flat = np.fromiter((s for x in lists for s in x), dtype=np.uint32, count=int(row[-1]) if n else 0)
         r.m.subs_build(row, flat)
-        self._csr_dirty = False
+        self._built = True
+
+    def _apply_ordered(self, add, dele):
+        """One delta for the pairs touched since the last publish: each pair's
+        net effect, read from the host lists (a pair deleted and added again
+        is present; the C-ABI applies a call's adds before its deletes, so the
+        raw event log could not be replayed in one call).  Sets, not order,
+        are what dispatch/2 parity is about."""
+        touched = dict.fromkeys(list(add) + list(dele))
+        a2 = [p for p in touched if self._present(*p)]
+        d2 = [p for p in touched if not self._present(*p)]
+        self.router.m.subs_apply_delta(add=a2, delete=d2)
+
+    def _present(self, fid: int, entry: int) -> bool:
+        flt = self.router.filter_of(fid)
+        if entry & GROUP_BIT:
+            g = self.group_names[entry & ~GROUP_BIT]
+            return bool(self.shared.get((g, flt)))
+        return entry in self.subscribers.get(flt, [])
 
     # -- publish side -------------------------------------------------------------------
     def publish(self, topic: bytes, clientid: bytes = b"") -> List[tuple]:

@@ -17,6 +17,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -177,6 +178,31 @@ struct Slot {
   }
 };
 
+// The subscriber table of the fan-out (emqx_subscriber, emqx_broker.erl:144-197,
+// 331-345), kept incrementally: the authoritative lists on the host (the CSR
+// of the last full build + the lists changed since), and on the device the
+// entries (sub_ids: the build's rows, then every changed row appended) and
+// two copies of the per-filter records the fan-out reads (k_sub_pairs'
+// layout).  A commit appends the changed rows past the entries any reader
+// can reach, patches them into the record copy no reader uses (after its
+// last readers finished) and makes it current — the table's two-slot epoch
+// scheme (egm_table_commit) for the subscriber side.
+struct SubsState {
+  bool built = false;
+  std::vector<uint64_t> row;                                  // the last full build's CSR
+  std::vector<uint32_t> subs;
+  std::unordered_map<uint32_t, std::vector<uint32_t>> lists;  // filters changed since that build
+  std::unordered_map<uint32_t, uint4> recs;                   // their current records
+  std::vector<uint32_t> pending;                              // changed since the last commit
+  std::vector<uint32_t> stale[2];                             // records a copy lacks (changed since it was written)
+  uint64_t tail = 0, garbage = 0;                             // device entries in use / superseded
+  int cur = 0;                                                // the record copy the fan-out reads
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses[2];    // last reading launch per stream, per copy
+  uint64_t epoch = 0;
+  uint64_t last_appended = 0, last_patched = 0;
+  bool last_rebuilt = false;
+};
+
 struct Epoch {
   DevTable view{};
   int slot = 0;
@@ -225,9 +251,11 @@ struct egm_ctx {
   DevBuf p_ctr, p_dst;
 
   // fan-out
-  DevBuf sub_row, sub_rp, sub_ids, f_dc, f_ds0, f_dpos, f_wbase, f_tiles, f_ovf, f_mrow, f_mids, f_drow, f_dfid,
-      f_dsub;
+  DevBuf sub_row, sub_rp, sub_rp2, sub_ids, f_dc, f_ds0, f_dpos, f_wbase, f_tiles, f_ovf, f_mrow, f_mids, f_drow,
+      f_dfid, f_dsub;
   uint32_t n_fid_slots = 0;
+  SubsState subs;
+  DevBuf& sub_rec(int k) { return k ? sub_rp2 : sub_rp; }
 
   // timing
   bool timing = false;
@@ -338,6 +366,14 @@ static void drain_slot(Slot& sl) {
     hipEventDestroy(u.second);
   }
   sl.uses.clear();
+}
+
+static void drain_uses(std::vector<std::pair<hipStream_t, hipEvent_t>>& u) {
+  for (auto& p : u) {
+    hipEventSynchronize(p.second);
+    hipEventDestroy(p.second);
+  }
+  u.clear();
 }
 
 static void note_use(egm_ctx* c, int slot, hipStream_t s) {
@@ -876,6 +912,8 @@ void egm_close(egm_ctx* c) {
     drain_slot(c->slots[1]);
     if (c->patch_host) hipHostFree(c->patch_host);
     c->patch_host = nullptr;
+    drain_uses(c->subs.uses[0]);
+    drain_uses(c->subs.uses[1]);
     if (c->work_ev) hipEventDestroy(c->work_ev);
     c->work_ev = nullptr;
     if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
@@ -1578,6 +1616,54 @@ static void pipe_release(egm_ctx* c, uint64_t slot) {
 }
 
 // ---------------------------------------------------------------- fan-out --
+// The record of filter f with subscribers L whose row (if stored) starts at
+// `start` — k_sub_pairs' layout (egm_kernels.hip): x = the third subscriber
+// of a row of at most FAN_INLINE_ALL (3), else the row start's low 32 bits;
+// y = start bits 32-39 | count (24 bits, saturated) << 8; z, w = the first two.
+static uint4 sub_record(const uint32_t* L, uint64_t cnt, uint64_t start) {
+  const uint32_t cs = (uint32_t)std::min<uint64_t>(cnt, (1u << 24) - 1);
+  const uint32_t x = cnt <= 3 ? (cnt > 2 ? L[2] : 0u) : (uint32_t)start;
+  const uint32_t y = (cnt <= 3 ? 0u : ((uint32_t)(start >> 32) & 0xFFu)) | (cs << 8);
+  return make_uint4(x, y, cnt > 0 ? L[0] : 0u, cnt > 1 ? L[1] : 0u);
+}
+
+// Full build from the host lists (egm_subs_build, and a commit that cannot patch).
+static int subs_upload(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint32_t* subs) {
+  const uint64_t ns = row[n_slots];
+  hipError_t e;
+  drain_uses(c->subs.uses[0]);
+  drain_uses(c->subs.uses[1]);
+  if ((e = hipDeviceSynchronize()) != hipSuccess) return c->hip_fail(e, "subs: device sync");
+  if ((e = c->sub_row.ensure(((uint64_t)n_slots + 1) * 8)) != hipSuccess) return c->hip_fail(e, "sub_row");
+  // room for appended rows: a quarter of the table + 64K entries before the next full build
+  if ((e = c->sub_ids.ensure((ns + ns / 4 + 65536) * 4 + 16)) != hipSuccess) return c->hip_fail(e, "sub_ids");
+  if ((e = hipMemcpy(c->sub_row.p, row, ((uint64_t)n_slots + 1) * 8, hipMemcpyHostToDevice)) != hipSuccess)
+    return c->hip_fail(e, "H2D sub_row");
+  if (ns && (e = hipMemcpy(c->sub_ids.p, subs, ns * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    return c->hip_fail(e, "H2D subs");
+  for (int k = 0; k < 2; ++k)
+    if ((e = c->sub_rec(k).ensure(((uint64_t)n_slots + 1) * 16)) != hipSuccess) return c->hip_fail(e, "sub_rp");
+  if ((e = launch_sub_pairs(c->sub_row.as<uint64_t>(), c->sub_ids.as<uint32_t>(), n_slots, c->sub_rp.as<uint4>(),
+                            c->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(c->sub_rp2.p, c->sub_rp.p, (uint64_t)n_slots * 16, hipMemcpyDeviceToDevice, c->stream)) !=
+          hipSuccess ||
+      (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+    return c->hip_fail(e, "sub pairs");
+  c->n_fid_slots = n_slots;
+  SubsState& S = c->subs;
+  S.lists.clear();
+  S.recs.clear();
+  S.pending.clear();
+  S.stale[0].clear();
+  S.stale[1].clear();
+  S.tail = ns;
+  S.garbage = 0;
+  S.cur = 0;
+  S.built = true;
+  S.epoch += 1;
+  return EGM_OK;
+}
+
 int egm_subs_build(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint32_t* subs) {
   if (!c || !row) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
@@ -1587,20 +1673,171 @@ int egm_subs_build(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint
   const uint64_t ns = row[n_slots];
   if (ns && !subs) return EGM_E_INVAL;
   if (ns >= (1ull << 40)) return c->fail(EGM_E_INVAL, "subscriber table: at most 2^40 entries (40-bit row starts)");
+  // the host keeps the lists: the base of later incremental changes (egm_subs_apply_delta)
+  SubsState& S = c->subs;
+  S.row.assign(row, row + (uint64_t)n_slots + 1);
+  if (subs)
+    S.subs.assign(subs, subs + ns);
+  else
+    S.subs.clear();
+  return subs_upload(c, S.row.data(), n_slots, S.subs.data());
+}
+
+// The current subscriber list of filter f (host).
+static std::vector<uint32_t>* subs_list(SubsState& S, uint32_t f, bool create) {
+  auto it = S.lists.find(f);
+  if (it != S.lists.end()) return &it->second;
+  if (!create) return nullptr;
+  std::vector<uint32_t>& L = S.lists[f];
+  if ((uint64_t)f + 1 < S.row.size()) L.assign(S.subs.begin() + S.row[f], S.subs.begin() + S.row[f + 1]);
+  return &L;
+}
+
+int egm_subs_apply_delta(egm_ctx* c, const egm_sub_pair* add, uint64_t n_add, const egm_sub_pair* del,
+                         uint64_t n_del) {
+  if (!c || (n_add && !add) || (n_del && !del)) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  SubsState& S = c->subs;
+  if (!S.built) return c->fail(EGM_E_STATE, "subscriber table: egm_subs_build first");
+  for (uint64_t i = 0; i < n_add; ++i)
+    if (add[i].fid >= WID_MAX) return c->fail(EGM_E_INVAL, "subscriber delta: filter id out of range");
+  // subscribe: a subscriber is in a filter's bag at most once (an ets bag keeps
+  // one copy of an identical object, emqx_broker.erl:144-157)
+  for (uint64_t i = 0; i < n_add; ++i) {
+    std::vector<uint32_t>& L = *subs_list(S, add[i].fid, true);
+    if (std::find(L.begin(), L.end(), add[i].sub) == L.end()) L.push_back(add[i].sub);
+    S.pending.push_back(add[i].fid);
+  }
+  // unsubscribe / subscriber_down: removed wherever present, order kept (:178-190, 331-345)
+  for (uint64_t i = 0; i < n_del; ++i) {
+    if (del[i].fid >= WID_MAX) continue;
+    std::vector<uint32_t>* L = subs_list(S, del[i].fid, (uint64_t)del[i].fid + 1 < S.row.size());
+    if (!L) continue;
+    auto it = std::find(L->begin(), L->end(), del[i].sub);
+    if (it != L->end()) {
+      L->erase(it);
+      S.pending.push_back(del[i].fid);
+    }
+  }
+  return EGM_OK;
+}
+
+int egm_subs_commit(egm_ctx* c, uint64_t* epoch) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  SubsState& S = c->subs;
+  if (!S.built) return c->fail(EGM_E_STATE, "subscriber table: egm_subs_build first");
+  S.last_appended = S.last_patched = 0;
+  S.last_rebuilt = false;
+  std::vector<uint32_t> P = S.pending;
+  sort_unique(P);
+  // a full build instead of a patch: a new filter id past the table's slots, a
+  // row too long for the record's 24-bit count, no room left for appended rows,
+  // or more superseded entries than live ones
+  bool rebuild = false;
+  uint64_t append = 0;
+  uint32_t max_f = c->n_fid_slots;
+  for (uint32_t f : P) {
+    const std::vector<uint32_t>& L = *subs_list(S, f, true);
+    if (f >= c->n_fid_slots) {
+      rebuild = true;
+      max_f = std::max(max_f, f + 1);
+    }
+    if (L.size() >= (1u << 24) - 1) rebuild = true;
+    if (L.size() > 3) append += L.size();
+  }
+  const uint64_t cap_ids = c->sub_ids.cap / 4;
+  if (S.tail + append + 16 > cap_ids || S.garbage + append > S.tail / 2 + 65536) rebuild = true;
+  if (rebuild) {
+    // flatten: the build's lists with every changed list in place
+    const uint32_t n = max_f;
+    std::vector<uint64_t> row((uint64_t)n + 1, 0);
+    for (uint32_t f = 0; f < n; ++f) {
+      auto it = S.lists.find(f);
+      const uint64_t k = it != S.lists.end() ? it->second.size()
+                         : ((uint64_t)f + 1 < S.row.size() ? S.row[f + 1] - S.row[f] : 0);
+      row[f + 1] = row[f] + k;
+    }
+    std::vector<uint32_t> flat(row[n]);
+    for (uint32_t f = 0; f < n; ++f) {
+      auto it = S.lists.find(f);
+      if (it != S.lists.end())
+        std::copy(it->second.begin(), it->second.end(), flat.begin() + row[f]);
+      else if ((uint64_t)f + 1 < S.row.size())
+        std::copy(S.subs.begin() + S.row[f], S.subs.begin() + S.row[f + 1], flat.begin() + row[f]);
+    }
+    if (row[n] >= (1ull << 40)) return c->fail(EGM_E_INVAL, "subscriber table: at most 2^40 entries");
+    S.row.swap(row);
+    S.subs.swap(flat);
+    const int r = subs_upload(c, S.row.data(), n, S.subs.data());
+    if (r == EGM_OK) S.last_rebuilt = true;
+    if (epoch) *epoch = S.epoch;
+    return r;
+  }
+  // appended rows and the new records of the changed filters
+  std::vector<uint32_t> app;
+  app.reserve(append);
+  const uint64_t base = S.tail;
+  for (uint32_t f : P) {
+    const std::vector<uint32_t>& L = *subs_list(S, f, true);
+    const uint64_t start = L.size() > 3 ? base + app.size() : 0;
+    if (L.size() > 3) app.insert(app.end(), L.begin(), L.end());
+    auto old = S.recs.find(f);
+    const uint64_t old_cnt = old != S.recs.end() ? (old->second.y >> 8)
+                             : ((uint64_t)f + 1 < S.row.size() ? S.row[f + 1] - S.row[f] : 0);
+    if (old_cnt > 3) S.garbage += old_cnt;
+    S.recs[f] = sub_record(L.data(), L.size(), start);
+  }
+  // the copy no reader uses: its last readers first, then every record it lacks
+  const int x = 1 - S.cur;
+  drain_uses(S.uses[x]);
+  std::vector<uint32_t> need = S.stale[x];
+  need.insert(need.end(), P.begin(), P.end());
+  sort_unique(need);
   hipError_t e;
-  hipStreamSynchronize(c->stream);
-  if ((e = c->sub_row.ensure(((uint64_t)n_slots + 1) * 8)) != hipSuccess) return c->hip_fail(e, "sub_row");
-  if ((e = c->sub_ids.ensure(ns * 4 + 16)) != hipSuccess) return c->hip_fail(e, "sub_ids");
-  if ((e = hipMemcpy(c->sub_row.p, row, ((uint64_t)n_slots + 1) * 8, hipMemcpyHostToDevice)) != hipSuccess)
-    return c->hip_fail(e, "H2D sub_row");
-  if (ns && (e = hipMemcpy(c->sub_ids.p, subs, ns * 4, hipMemcpyHostToDevice)) != hipSuccess)
-    return c->hip_fail(e, "H2D subs");
-  if ((e = c->sub_rp.ensure(((uint64_t)n_slots + 1) * 16)) != hipSuccess) return c->hip_fail(e, "sub_rp");
-  if ((e = launch_sub_pairs(c->sub_row.as<uint64_t>(), c->sub_ids.as<uint32_t>(), n_slots, c->sub_rp.as<uint4>(),
-                            c->stream)) != hipSuccess ||
-      (e = hipStreamSynchronize(c->stream)) != hipSuccess)
-    return c->hip_fail(e, "sub pairs");
-  c->n_fid_slots = n_slots;
+  const size_t o_app = 0, o_idx = (app.size() * 4 + 15) & ~(size_t)15, o_rec = (o_idx + need.size() * 4 + 15) & ~(size_t)15;
+  const size_t total = o_rec + need.size() * 16;
+  if (total) {
+    uint8_t* h = patch_stage(c, total);
+    if (!h) return c->fail(EGM_E_NOMEM, "subs commit: pinned staging");
+    memcpy(h + o_app, app.data(), app.size() * 4);
+    memcpy(h + o_idx, need.data(), need.size() * 4);
+    for (size_t i = 0; i < need.size(); ++i) memcpy(h + o_rec + 16 * i, &S.recs[need[i]], 16);
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "subs commit: stream");
+    if ((e = c->patch_dev.ensure(total)) != hipSuccess) return c->hip_fail(e, "subs commit: patch buffer");
+    if ((e = hipMemcpyAsync(c->patch_dev.p, h, total, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "subs commit: upload");
+    uint8_t* dp = (uint8_t*)c->patch_dev.p;
+    // appended rows lie past every entry a reader of either copy can reach
+    if (!app.empty() &&
+        (e = hipMemcpyAsync(c->sub_ids.as<uint32_t>() + base, dp + o_app, app.size() * 4, hipMemcpyDeviceToDevice,
+                            c->stream)) != hipSuccess)
+      return c->hip_fail(e, "subs commit: rows");
+    if ((e = launch_patch(c->sub_rec(x).p, 16, (const uint32_t*)(dp + o_idx), dp + o_rec, need.size(), c->stream)) !=
+        hipSuccess)
+      return c->hip_fail(e, "subs commit: patch");
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "subs commit: sync");
+  }
+  S.tail = base + app.size();
+  S.stale[x].clear();
+  S.stale[S.cur].insert(S.stale[S.cur].end(), P.begin(), P.end());   // the old copy now lacks this commit
+  S.cur = x;
+  S.pending.clear();
+  S.epoch += 1;
+  S.last_appended = app.size();
+  S.last_patched = need.size();
+  if (epoch) *epoch = S.epoch;
+  return EGM_OK;
+}
+
+int egm_subs_last_commit(egm_ctx* c, uint64_t* appended, uint64_t* patched, int* rebuilt, uint64_t* entries) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (appended) *appended = c->subs.last_appended;
+  if (patched) *patched = c->subs.last_patched;
+  if (rebuilt) *rebuilt = c->subs.last_rebuilt ? 1 : 0;
+  if (entries) *entries = c->subs.tail;
   return EGM_OK;
 }
 
@@ -1622,7 +1859,8 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   uint64_t* dpos = d_entry_pos ? d_entry_pos : c->f_dpos.as<uint64_t>();   // the caller's, in the compact form
   if ((e = c->f_tiles.ensure((scan_tiles((uint32_t)nwin) + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_tiles");
   if ((e = c->f_ovf.ensure(16)) != hipSuccess) return c->hip_fail(e, "f_ovf");
-  SubTable st{c->sub_row.as<uint64_t>(), c->sub_ids.as<uint32_t>(), c->n_fid_slots, c->sub_rp.as<uint4>()};
+  const int rk = c->subs.cur;   // the current record copy; a commit patches the other one
+  SubTable st{c->sub_row.as<uint64_t>(), c->sub_ids.as<uint32_t>(), c->n_fid_slots, c->sub_rec(rk).as<uint4>()};
   hipEvent_t evp[2] = {nullptr, nullptr};
   if (c->timing) {
     evp[0] = c->take_event();
@@ -1638,6 +1876,20 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
                     c->f_ds0.as<uint4>(), dpos, c->f_wbase.as<uint64_t>(), c->f_tiles.as<uint64_t>(),
                     c->f_ovf.as<unsigned int>(), s, c->timing ? evp : nullptr, ord ? c->last_walk.order : nullptr);
   if (OW) ws_done(*OW, s);
+  {   // a later subscriber commit must not patch this copy before the fan-out has read it
+    auto& u = c->subs.uses[rk];
+    bool found = false;
+    for (auto& p : u)
+      if (p.first == s) {
+        hipEventRecord(p.second, s);
+        found = true;
+      }
+    hipEvent_t ev = nullptr;
+    if (!found && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
+      hipEventRecord(ev, s);
+      u.push_back({s, ev});
+    }
+  }
   if (c->timing) {
     c->ev_fan.push_back(evp[0]);
     c->ev_fan.push_back(evp[1]);

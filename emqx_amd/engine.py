@@ -287,6 +287,26 @@ class GpuMatcher:
         subs = np.ascontiguousarray(subs, dtype=np.uint32)
         self._check(self.lib.egm_subs_build(self.ctx, _ptr(row), len(row) - 1, _ptr(subs)), "egm_subs_build")
 
+    def subs_apply_delta(self, add=(), delete=()):
+        """egm_subs_apply_delta: (filter id, subscriber) pairs to add / remove."""
+        a = np.ascontiguousarray(np.asarray(add, dtype=np.uint32).reshape(-1, 2))
+        d = np.ascontiguousarray(np.asarray(delete, dtype=np.uint32).reshape(-1, 2))
+        self._check(self.lib.egm_subs_apply_delta(self.ctx, _ptr(a) if len(a) else None, len(a),
+                                                  _ptr(d) if len(d) else None, len(d)), "egm_subs_apply_delta")
+
+    def subs_commit(self) -> int:
+        """egm_subs_commit: publish the staged subscriber changes; returns the epoch."""
+        ep = C.c_uint64()
+        self._check(self.lib.egm_subs_commit(self.ctx, C.byref(ep)), "egm_subs_commit")
+        return ep.value
+
+    def subs_last_commit(self) -> dict:
+        a, p, e = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        r = C.c_int()
+        self._check(self.lib.egm_subs_last_commit(self.ctx, C.byref(a), C.byref(p), C.byref(r), C.byref(e)),
+                    "egm_subs_last_commit")
+        return {"appended": a.value, "patched": p.value, "rebuilt": bool(r.value), "entries": e.value}
+
     def fanout(self, m: MatchResult) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         n = len(m.row_ptr) - 1
         counts = np.diff(m.row_ptr).astype(np.uint32)

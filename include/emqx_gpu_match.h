@@ -244,6 +244,29 @@ int egm_get_timing(egm_ctx* ctx, double* walk_ms, uint64_t* walk_launches, doubl
 /* ---- subscriber fan-out (emqx_broker:dispatch/2) ---- */
 /* filter id -> subscriber ids CSR (sub | 0x80000000 marks a shared group id). */
 int egm_subs_build(egm_ctx* ctx, const uint64_t* row_ptr, uint32_t n_fid_slots, const uint32_t* subs);
+/* Incremental subscriber changes, the table kept by emqx_broker's
+   subscribe/3, unsubscribe/1 and subscriber_down/1 (apps/emqx/src/
+   emqx_broker.erl:144-197, 331-345; emqx_broker_helper.erl:133-163 purges a
+   dead subscriber): add / remove (filter id, subscriber) pairs on the host —
+   a pair already present is not added twice (an ets bag keeps one copy of an
+   identical object), removing an absent one does nothing, a list keeps its
+   order — then egm_subs_commit publishes them to the fan-out in one epoch.
+   The commit appends the changed rows to the device entries and patches
+   their records into the record copy no fan-out in flight reads (after its
+   last readers finished), then makes it current: fan-outs already launched
+   keep the epoch they started with.  A new filter id past the table, a row of
+   2^24 subscribers, or appended rows past the reserve make it a full build
+   (egm_subs_last_commit reports which).  EGM_E_STATE before egm_subs_build. */
+typedef struct egm_sub_pair {
+  uint32_t fid;   /* filter id */
+  uint32_t sub;   /* subscriber id, or a $share group id | 0x80000000 */
+} egm_sub_pair;
+int egm_subs_apply_delta(egm_ctx* ctx, const egm_sub_pair* add, uint64_t n_add, const egm_sub_pair* del,
+                         uint64_t n_del);
+int egm_subs_commit(egm_ctx* ctx, uint64_t* epoch);
+/* What the last egm_subs_commit did: subscriber entries appended, records
+   patched, whether it was a full build, entries now on the device. */
+int egm_subs_last_commit(egm_ctx* ctx, uint64_t* appended, uint64_t* patched, int* rebuilt, uint64_t* entries);
 int egm_fanout_batch(egm_ctx* ctx, const egm_result* matched, egm_delivery** out);
 /* Device variant over a device CSR match result.  match_ids_len = entries
    d_match_ids holds: a match row whose total exceeds it (an overflowed match

@@ -188,3 +188,110 @@ def test_publish_result_random_vs_oracle():
         dropped += 0 if want or t.startswith(b"$SYS/") else 1
         assert sorted(g, key=repr) == sorted(want, key=repr), t
     assert br.metrics["messages.dropped"] == dropped
+
+
+def test_broker_subscriber_churn_vs_oracle():
+    """the fan-out's subscriber table follows
+    subscribe/3, unsubscribe/1 and subscriber_down/1 between publishes
+    (emqx_broker.erl:144-197, 331-345; emqx_broker_helper.erl:133-163) by
+    deltas (egm_subs_apply_delta + egm_subs_commit), not rebuilds: eight
+    rounds of random churn — new and repeated subscriptions, unsubscribes,
+    dead subscribers purged, $share members joining and leaving, a filter
+    crossing the 1024-subscriber shard threshold — each followed by a batch
+    of publishes whose delivery sets equal the oracle broker's
+    (oracle/trie_ref.py deliveries over the reference's match_routes)."""
+    rng = random.Random(23)
+    br = Broker(shared_strategy="hash_topic")
+    o = R.Router()
+    subs, shared = {}, {}          # oracle: filter -> [sub]; (group, filter) -> [member]
+    fl = list(dict.fromkeys(rand_filter(rng) for _ in range(200)))
+    nxt = [0]
+
+    def sub(f, s=None):
+        s = nxt[0] if s is None else s
+        nxt[0] = max(nxt[0], s + 1)
+        br.subscribe(f, s)
+        lst = subs.setdefault(f, [])
+        if s not in lst:
+            lst.append(s)
+        o.do_add_route(f, ("node", "local"))
+        return s
+
+    def unsub(f, s):
+        br.unsubscribe(f, s)
+        if s in subs.get(f, []):
+            subs[f].remove(s)
+            if not subs[f]:
+                del subs[f]
+                o.do_delete_route(f, ("node", "local"))
+
+    def share(g, f, s):
+        br.subscribe(b"$share/" + g + b"/" + f, s)
+        mem = shared.setdefault((g, f), [])
+        if s not in mem:
+            mem.append(s)
+        o.do_add_route(f, ("group", g))
+
+    def unshare(g, f, s):
+        br.unsubscribe(b"$share/" + g + b"/" + f, s)
+        mem = shared.get((g, f), [])
+        if s in mem:
+            mem.remove(s)
+            if not mem:
+                del shared[(g, f)]
+                o.do_delete_route(f, ("group", g))
+
+    for f in fl[:150]:
+        for _ in range(rng.randint(1, 3)):
+            sub(f)
+    rounds_checked = 0
+    stats = []
+    for rnd in range(8):
+        if rnd:
+            for _ in range(rng.randint(20, 80)):
+                op = rng.random()
+                if op < 0.35:       # subscribe (a new or an existing filter; sometimes a repeat)
+                    f = rng.choice(fl)
+                    if rng.random() < 0.2 and subs.get(f):
+                        sub(f, rng.choice(subs[f]))
+                    else:
+                        sub(f)
+                elif op < 0.6 and subs:      # unsubscribe
+                    f = rng.choice(sorted(subs))
+                    unsub(f, rng.choice(subs[f]))
+                elif op < 0.7 and subs:      # subscriber_down: every subscription of one subscriber
+                    f = rng.choice(sorted(subs))
+                    s = rng.choice(subs[f])
+                    br.subscriber_down(s)
+                    for g, ff in [k for k in shared if s in shared[k]]:
+                        mem = shared[(g, ff)]
+                        mem.remove(s)
+                        if not mem:
+                            del shared[(g, ff)]
+                            o.do_delete_route(ff, ("group", g))
+                    for ff in [k for k in subs if s in subs[k]]:
+                        subs[ff].remove(s)
+                        if not subs[ff]:
+                            del subs[ff]
+                            o.do_delete_route(ff, ("node", "local"))
+                elif op < 0.85:              # a $share member joins
+                    share(b"g%d" % rng.randint(0, 3), rng.choice(fl), 500000 + rng.randint(0, 40))
+                elif shared:                 # ... or leaves
+                    g, f = rng.choice(sorted(shared))
+                    unshare(g, f, rng.choice(shared[(g, f)]))
+            if rnd == 4:   # one filter past the 1024-subscriber shard threshold
+                for k in range(1100):
+                    sub(fl[0], 200000 + k)
+        topics = [rand_topic(rng) for _ in range(200)] + [f.replace(b"+", b"x").replace(b"#", b"y") for f in fl[:100]]
+        got = br.publish_batch(topics)
+        if rnd:
+            stats.append(br.router.m.subs_last_commit())
+        for t, g in zip(topics, got):
+            want = R.deliveries(o, subs, t)
+            assert set(d[:3] for d in g) == want, (rnd, t)
+            for d in g:
+                if d[0] == "group":
+                    assert d[3] in shared[(d[2], d[1])]   # exactly one live member of that group
+        rounds_checked += 1
+    assert rounds_checked == 8
+    assert any(not s["rebuilt"] and s["patched"] > 0 for s in stats), stats   # deltas, not rebuilds
