@@ -64,9 +64,10 @@ class Broker:
         self._shards = shards
         # the GPU subscriber table (egm_subs_*): built once, then kept by deltas
         self._built = False
-        self._d_add: List[Tuple[bytes, int]] = []   # (filter, subscriber entry) since the last commit
+        self._d_add: List[Tuple[int, int]] = []   # (filter id, subscriber entry) since the last commit
         self._d_del: List[Tuple[bytes, int]] = []
         self.subscriptions: Dict[int, set] = {}     # ?SUBSCRIPTION: sub -> {(filter, group or None)}
+        self._fid_flt: Dict[int, bytes] = {}         # filter ids seen in subscriber events
         self.dead: set = set()   # subscribers whose process is gone (is_process_alive/1 false)
         self.metrics = {"messages.publish": 0, "messages.dropped": 0, "messages.dropped.no_subscribers": 0,
                         "messages.forward": 0}
@@ -90,7 +91,7 @@ class Broker:
             if len(subs) > SHARD_THRESHOLD:
                 self.shard_of[(flt, sub_id)] = zlib.crc32(str(sub_id).encode()) % self._shards + 1
             self.router.do_add_route(flt, self.node)
-            self._d_add.append((flt, sub_id))
+            self._note(self._d_add, flt, sub_id)
         else:
             mem = self.shared.setdefault((group, flt), [])
             if sub_id in mem:
@@ -101,7 +102,7 @@ class Broker:
                 self.group_names.append(group)
             self.router.do_add_route(flt, ("group", group))
             if len(mem) == 1:   # the (filter, group) entry: one per group, whatever its members
-                self._d_add.append((flt, GROUP_BIT | self.group_ids[group]))
+                self._note(self._d_add, flt, GROUP_BIT | self.group_ids[group])
         self.subscriptions.setdefault(sub_id, set()).add((flt, group))
         return "ok"
 
@@ -117,7 +118,7 @@ class Broker:
             if sub_id in subs:
                 subs.remove(sub_id)
                 self.shard_of.pop((flt, sub_id), None)
-                self._d_del.append((flt, sub_id))
+                self._note(self._d_del, flt, sub_id)   # (its filter id, before the route may go)
                 if not subs:
                     del self.subscribers[flt]
                     self.router.do_delete_route(flt, self.node)
@@ -127,7 +128,7 @@ class Broker:
                 mem.remove(sub_id)
                 if not mem:
                     del self.shared[(group, flt)]
-                    self._d_del.append((flt, GROUP_BIT | self.group_ids[group]))
+                    self._note(self._d_del, flt, GROUP_BIT | self.group_ids[group])
                     self.router.do_delete_route(flt, ("group", group))
         s = self.subscriptions.get(sub_id)
         if s is not None:
@@ -154,12 +155,7 @@ class Broker:
         r.commit()
         if self._built:
             if self._d_add or self._d_del:
-                fid = r.filter_id
-                add = [(fid(f), s) for f, s in self._d_add]
-                dele = [(fid(f), s) for f, s in self._d_del if fid(f) is not None]
-                # (an add and a later delete of the same pair in one delta: the delete
-                # applies after; a re-add after a delete must come after it)
-                self._apply_ordered(add, dele)
+                self._apply_ordered(self._d_add, self._d_del)
                 r.m.subs_commit()
                 self._d_add.clear()
                 self._d_del.clear()
@@ -189,8 +185,19 @@ class Broker:
         d2 = [p for p in touched if not self._present(*p)]
         self.router.m.subs_apply_delta(add=a2, delete=d2)
 
+    def _note(self, log: list, flt: bytes, entry: int):
+        """A subscriber-table event as (filter id, entry), the id taken now: a
+        filter whose last route goes loses its id, and its row must still be
+        emptied on the GPU."""
+        fid = self.router.filter_id(flt)
+        if fid is not None:
+            self._fid_flt[fid] = flt
+            log.append((fid, entry))
+
     def _present(self, fid: int, entry: int) -> bool:
-        flt = self.router.filter_of(fid)
+        flt = self._fid_flt[fid]
+        if self.router.filter_id(flt) != fid:   # the filter left the table (its id is not reused)
+            return False
         if entry & GROUP_BIT:
             g = self.group_names[entry & ~GROUP_BIT]
             return bool(self.shared.get((g, flt)))
