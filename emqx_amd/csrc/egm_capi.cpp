@@ -1675,12 +1675,16 @@ int egm_subs_build(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint
   if (ns >= (1ull << 40)) return c->fail(EGM_E_INVAL, "subscriber table: at most 2^40 entries (40-bit row starts)");
   // the host keeps the lists: the base of later incremental changes (egm_subs_apply_delta)
   SubsState& S = c->subs;
+  // record slots beyond the given filter ids (empty rows): new filters subscribed
+  // later are patched in, not rebuilt
+  const uint32_t cap_slots = (uint32_t)std::min<uint64_t>(WID_MAX, (uint64_t)n_slots + n_slots / 4 + 4096);
   S.row.assign(row, row + (uint64_t)n_slots + 1);
+  S.row.resize((uint64_t)cap_slots + 1, row[n_slots]);
   if (subs)
     S.subs.assign(subs, subs + ns);
   else
     S.subs.clear();
-  return subs_upload(c, S.row.data(), n_slots, S.subs.data());
+  return subs_upload(c, S.row.data(), cap_slots, S.subs.data());
 }
 
 // The current subscriber list of filter f (host).
@@ -1750,8 +1754,8 @@ int egm_subs_commit(egm_ctx* c, uint64_t* epoch) {
   const uint64_t cap_ids = c->sub_ids.cap / 4;
   if (S.tail + append + 16 > cap_ids || S.garbage + append > S.tail / 2 + 65536) rebuild = true;
   if (rebuild) {
-    // flatten: the build's lists with every changed list in place
-    const uint32_t n = max_f;
+    // flatten: the build's lists with every changed list in place (and new empty slots)
+    const uint32_t n = (uint32_t)std::min<uint64_t>(WID_MAX, (uint64_t)max_f + max_f / 4 + 4096);
     std::vector<uint64_t> row((uint64_t)n + 1, 0);
     for (uint32_t f = 0; f < n; ++f) {
       auto it = S.lists.find(f);
