@@ -1797,11 +1797,12 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_burst(const uint32_t* __
 #pragma unroll
       for (uint32_t b = 0; b < REC_BURST; ++b) {
         if (b < nb && from_dir) {
-          const uint64_t o = (uint64_t)(uint32_t)__shfl((int)roff, (int)(r0 + b), 64) << 2;
+          // the record's offset and header are wave-uniform: scalar registers and a scalar load
+          const uint64_t o = (uint64_t)uni((uint32_t)__shfl((int)roff, (int)(r0 + b), 64)) << 2;
           const bool in = o + REC_IDS <= rec_cap;
           const uint64_t oc = in ? o : 0ull;
           off[b] = o;
-          hdr[b] = in ? rec[oc] : 0u;
+          hdr[b] = in ? uni(rec[oc]) : 0u;
           cr[b] = ((const uint16_t*)(rec + oc + REC_HDR))[lane];
 #pragma unroll
           for (uint32_t k = 0; k < REC_IPL; ++k) v[b][k] = rec[min(oc + REC_IDS + lane + 64u * k, rec_cap - 1)];
