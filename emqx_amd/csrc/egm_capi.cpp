@@ -646,7 +646,7 @@ static uint32_t env_u32(const char* name, uint32_t dflt, uint32_t lo, uint32_t h
   return (uint32_t)std::min<long long>(std::max<long long>(k, lo), hi);
 }
 static uint32_t flush_lim() { return env_u32("EGM_FLUSH_AT", walk_stage(), 1, walk_stage()); }
-static uint32_t rec_grain() { return env_u32("EGM_REC_SEG", REC_GRAIN, 64, 1u << 24); }
+static uint32_t rec_grain() { return env_u32("EGM_REC_SEG", REC_GRAIN, 64, 1u << 24) & ~(uint32_t)(EGM_REC_ALIGN - 1); }
 
 // The workspace for a batch on stream s: the one that last ran on s (stream
 // order protects it), else the least recently used one, ordered after its

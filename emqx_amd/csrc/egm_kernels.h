@@ -48,7 +48,7 @@ struct MatchStats {               // device-side counters, zeroed per batch
 //   [0, 4)        header {n_entries | REC_TAG, 0, 0, 0}
 //   [4, 36)       64 x u16: the entries of each of the chunk's topics
 //   [36, 36 + n)  the entries' filter ids, grouped by topic (topic 0's first)
-//   padded to a multiple of 4 u32 (16 B).
+//   padded to a whole 128-B line (EGM_REC_ALIGN u32), segments line-aligned too.
 // A wave reserves segments of rec_grain u32 (one device-scope atomic each:
 // a counter bumped per flush would serialise across the 8 XCDs) and always
 // keeps REC_HDR u32 free at a segment's end: when the next record does not
@@ -59,9 +59,14 @@ constexpr uint32_t REC_HDR = 4;
 constexpr uint32_t REC_IDS = REC_HDR + 32;        // u32 before the ids
 constexpr uint32_t REC_TAG = 0x5EC0u << 16;
 constexpr uint32_t REC_JUMP = 0x4A4Du << 16;
-constexpr uint32_t REC_GRAIN = 16384;             // default u32 per segment (EGM_REC_SEG)
+constexpr uint32_t REC_GRAIN = 16384;             // default u32 per segment (EGM_REC_SEG; a multiple of 32)
 constexpr uint32_t REC_DIR = 64;                  // record offsets per chunk in its directory (longer: the chain)
-__host__ __device__ constexpr uint32_t rec_size(uint32_t n_entries) { return (REC_IDS + n_entries + 3u) & ~3u; }
+#ifndef EGM_REC_ALIGN
+#define EGM_REC_ALIGN 32   // u32: records start on 128-B lines, so no line is shared by two flushes
+#endif
+__host__ __device__ constexpr uint32_t rec_size(uint32_t n_entries) {
+  return (REC_IDS + n_entries + (EGM_REC_ALIGN - 1u)) & ~(EGM_REC_ALIGN - 1u);
+}
 // Per chunk (uint4): {first record lo, first record hi, records, flags}.
 constexpr uint32_t CHUNK_WALKED = 1u;             // walked by k_walk (either pass): its records hold its ids
 constexpr uint32_t CHUNK_HEAVY = 2u;              // deferred to k_heavy: its ids are in pieces
@@ -149,7 +154,7 @@ uint32_t heavy_stack_items(uint64_t max_levels);
 int deep_grid_blocks(uint32_t n_topics);
 uint32_t walk_stage();   // WALK_STAGE: the most emits a flush record holds
 // Record slab u32 for a batch of up to `ids` matched ids: every record carries
-// REC_IDS + 3 u32 beyond its entries and holds at least flush_lim - 256 + 1 of
+// REC_IDS + EGM_REC_ALIGN - 1 u32 beyond its entries and holds at least flush_lim - 256 + 1 of
 // them (a flush is due once the next step could overfill the stage; the last
 // record of a chunk can be shorter: one per chunk), plus every wave's segment
 // tail.
@@ -157,7 +162,8 @@ inline uint64_t rec_capacity(uint64_t ids, uint32_t n, uint32_t flush_lim, uint3
   const uint64_t per = flush_lim > 256 ? flush_lim - 256 : 1;
   const uint64_t chunks = (uint64_t)n / WALK_CHUNK + 2;
   const uint64_t waves = (uint64_t)walk_grid_blocks(n) + (uint64_t)deep_grid_blocks(n);
-  return ids + ids * (REC_IDS + 3 + per - 1) / per + chunks * (REC_IDS + 3 + REC_HDR) + waves * (grain + REC_HDR);
+  constexpr uint64_t over = REC_IDS + EGM_REC_ALIGN - 1;
+  return ids + ids * (over + per - 1) / per + chunks * (over + REC_HDR) + waves * (grain + EGM_REC_ALIGN + REC_HDR);
 }
 
 // Timing hooks: when ev != nullptr, ev[0]/ev[1] bracket the walk kernel.

@@ -578,7 +578,8 @@ __device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t la
   // reserve the record: a new segment when the current one cannot hold it and a jump
   const uint32_t size = rec_size(nstage);
   if (rc.cur + size + REC_HDR > rc.end) {   // wave-uniform
-    const unsigned long long grain = max((unsigned long long)w.rec_grain, (unsigned long long)(size + REC_HDR));
+    const unsigned long long grain =
+        max((unsigned long long)w.rec_grain, (unsigned long long)(size + EGM_REC_ALIGN));   // (keeps the line alignment)
     unsigned long long b = 0;
     if (lane == 0) b = atomicAdd(&w.stats->rec_cursor, grain);
     b = uni64(__shfl(b, 0, 64));
@@ -1794,19 +1795,20 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_burst(const uint32_t* __
       uint32_t hdr[REC_BURST], cr[REC_BURST], v[REC_BURST][REC_IPL];
       uint64_t off[REC_BURST];
       const bool from_dir = r0 + nb <= REC_DIR;   // wave-uniform
+      // every slot's loads issued unconditionally (a slot past the burst re-reads its
+      // first record): a load under a branch is waited for at the branch's end
 #pragma unroll
       for (uint32_t b = 0; b < REC_BURST; ++b) {
-        if (b < nb && from_dir) {
-          // the record's offset and header are wave-uniform: scalar registers and a scalar load
-          const uint64_t o = (uint64_t)uni((uint32_t)__shfl((int)roff, (int)(r0 + b), 64)) << 2;
-          const bool in = o + REC_IDS <= rec_cap;
-          const uint64_t oc = in ? o : 0ull;
-          off[b] = o;
-          hdr[b] = in ? uni(rec[oc]) : 0u;
-          cr[b] = ((const uint16_t*)(rec + oc + REC_HDR))[lane];
+        // the record's offset and header are wave-uniform: scalar registers and a scalar load
+        const uint32_t rb = from_dir ? r0 + (b < nb ? b : 0u) : 0u;
+        const uint64_t o = (uint64_t)uni((uint32_t)__shfl((int)roff, (int)min(rb, REC_DIR - 1), 64)) << 2;
+        const bool in = o + REC_IDS <= rec_cap;
+        const uint64_t oc = in ? o : 0ull;
+        off[b] = o;
+        hdr[b] = in ? uni(rec[oc]) : 0u;
+        cr[b] = ((const uint16_t*)(rec + oc + REC_HDR))[lane];
 #pragma unroll
-          for (uint32_t k = 0; k < REC_IPL; ++k) v[b][k] = rec[min(oc + REC_IDS + lane + 64u * k, rec_cap - 1)];
-        }
+        for (uint32_t k = 0; k < REC_IPL; ++k) v[b][k] = rec[min(oc + REC_IDS + lane + 64u * k, rec_cap - 1)];
       }
 #pragma unroll
       for (uint32_t b = 0; b < REC_BURST; ++b) {
