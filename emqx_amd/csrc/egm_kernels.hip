@@ -1423,19 +1423,22 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
 // walk-order rows, else the input topic from the sorted record) and that row's
 // start from the scan.  The chunk's records come from its directory (the
 // walk's record offsets, REC_DIR of them; a longer chunk continues along the
-// chain), so the loads of record r + 1 — header, counts and all its ids — are
-// in flight while record r is placed: its 64 counts scanned into the topics'
-// slots, each id stored at row start + the topic's running offset (an owner
-// found per id by a 6-step LDS search).  In walk-order rows a chunk's rows are
+// chain).  Each record is placed by scanning its 64 counts into the topics'
+// slots and storing every id at row start + the topic's running offset (its
+// owner found by a 6-step LDS search).  In walk-order rows a chunk's rows are
 // one contiguous run (and topic[k] is written here); in input order each
-// topic's piece of a record goes to a scattered row.  A chunk is placed in
-// about one memory round trip, so its partly written output lines are still
-// in L2 when the next record completes them.  Chunks walked by k_heavy are
-// skipped (their ids arrive as pieces, k_compact).
-#ifndef EGM_REC_TAB
-#define EGM_REC_TAB 16   // records per chunk in the gather's LDS table (longer chunks: k_rec_rows)
-#endif
-constexpr uint32_t REC_TAB = EGM_REC_TAB;
+// topic's piece of a record goes to a scattered row.  Chunks walked by k_heavy
+// are skipped (their ids arrive as pieces, k_compact).
+//
+// k_rec_rows (A/B, EGM_REC_ROWS=0) places one record at a time with the next
+// one's loads in flight; k_rec_burst (the default) loads REC_BURST records at
+// once.  Measured at C2 (r5, rocprof): 1.93 / 1.65 ms.  Two forms that
+// assemble the chunk in LDS first and store whole lines were slower: a 16 KB
+// LDS window per wave (4.2 ms: 9 waves per CU, a round trip per record) and
+// an in-order gather through an LDS table of the chunk's records (1.52 ms +
+// 0.37 ms for chunks of more than 16 records).  Stores of records as one
+// contiguous run (measurement only) take 0.93 ms and no stores 0.46 ms: the
+// runs of ~5 ids per topic and record are what costs.
 constexpr int REC_WAVES = 4;
 constexpr uint32_t REC_IPL = (WALK_STAGE + 63) / 64;   // a record's ids, all loaded in one round
 struct RecLoad {
@@ -1449,7 +1452,7 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
                                                              const uint64_t* __restrict__ order, uint32_t n,
                                                              const uint64_t* __restrict__ row_ptr,
                                                              uint32_t* __restrict__ topic, uint32_t* __restrict__ ids,
-                                                             uint64_t ids_cap, MatchStats* stats, bool long_only) {
+                                                             uint64_t ids_cap, MatchStats* stats) {
   __shared__ uint32_t s_ex[REC_WAVES][64];
   __shared__ uint64_t s_dst[REC_WAVES][64];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1469,9 +1472,9 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
     const uint32_t t = c * WALK_CHUNK + lane;
     const bool act = t < n;
     const uint32_t my_t = act ? (order ? (uint32_t)order[t] : t) : 0u;
+    if (topic && act) topic[t] = my_t;   // written even when the rows are not (overflow): the map is the order
     const uint4 ch = chunks[c];
-    if (topic && act && !long_only) topic[t] = my_t;   // (after the gather: it wrote the map)
-    if (!ok || !(ch.w & CHUNK_WALKED) || ch.z == 0 || (long_only && ch.z <= REC_TAB)) continue;
+    if (!ok || !(ch.w & CHUNK_WALKED) || ch.z == 0) continue;
     const uint32_t nrec = ch.z;
     uint64_t dst = act ? row_ptr[topic ? t : my_t] : 0ull;
     const uint32_t roff = lane < min(nrec, REC_DIR) ? dir[(uint64_t)c * REC_DIR + lane] : 0u;
@@ -1516,243 +1519,6 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
       }
       A = B;
     }
-  }
-}
-
-// The staged form of k_rec_rows (round 5, the default): the chunk's output
-// is assembled in LDS and written out as whole lines.  k_rec_rows stores each
-// record's ~5-id run per topic straight to its row; a line of the chunk's
-// output is completed by ~6 records over the chunk's placement, and with
-// thousands of chunks in progress the partly written lines left L2 first:
-// 4.1 GB written per C2 batch for 1.99 GB of ids (PMC, r5g).  Here one wave
-// per chunk places every record's ids into an LDS window of REC_STAGE ids of
-// the chunk's output (topic j's ids at its chunk offset + the ids of j in
-// earlier records + rank), then writes the window out: one contiguous run in
-// walk-order rows, a contiguous run per row in input order.  A chunk with
-// more ids than the window is placed window by window (its records re-read).
-// The next record's loads are in flight while one is placed (the directory).
-#ifndef EGM_REC_STAGE
-#define EGM_REC_STAGE 4096   // ids per LDS window (16 KB: 10 waves per CU)
-#endif
-constexpr uint32_t REC_STAGE = EGM_REC_STAGE;
-__global__ __launch_bounds__(64) void k_rec_rows_staged(const uint32_t* __restrict__ rec, uint64_t rec_cap,
-                                                        const uint4* __restrict__ chunks,
-                                                        const uint32_t* __restrict__ dir,
-                                                        const uint64_t* __restrict__ order, uint32_t n,
-                                                        const uint64_t* __restrict__ row_ptr,
-                                                        uint32_t* __restrict__ topic, uint32_t* __restrict__ ids,
-                                                        uint64_t ids_cap, MatchStats* stats) {
-  __shared__ uint32_t stage[REC_STAGE];
-  __shared__ uint32_t s_ex[64], s_pos[64], s_co[64];
-  __shared__ uint64_t s_rs[64];
-  const uint32_t lane = threadIdx.x;
-  const bool ok = compact_checks(row_ptr, n, ids_cap, stats);
-  const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
-  auto issue = [&](uint64_t o, RecLoad& L) {
-    const bool in = o + REC_IDS <= rec_cap;
-    const uint64_t oc = in ? o : 0ull;
-    L.off = o;
-    L.hdr = in ? rec[oc] : 0u;
-    L.cr = ((const uint16_t*)(rec + oc + REC_HDR))[lane];
-#pragma unroll
-    for (uint32_t k = 0; k < REC_IPL; ++k) L.v[k] = rec[min(oc + REC_IDS + lane + 64u * k, rec_cap - 1)];
-  };
-  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    const uint32_t t = c * WALK_CHUNK + lane;
-    const bool act = t < n;
-    const uint32_t my_t = act ? (order ? (uint32_t)order[t] : t) : 0u;
-    if (topic && act) topic[t] = my_t;   // written even when the rows are not (overflow): the map is the order
-    const uint4 ch = chunks[c];
-    if (!ok || !(ch.w & CHUNK_WALKED) || ch.z == 0) continue;
-    const uint32_t nrec = ch.z;
-    const uint32_t row = topic ? t : my_t;
-    const uint64_t rs = act ? row_ptr[row] : 0ull;
-    const uint32_t cnt = act ? (uint32_t)(row_ptr[row + 1] - rs) : 0u;
-    uint32_t T;
-    const uint32_t co = wave_excl_scan(cnt, lane, &T);   // the topic's offset in the chunk's output
-    s_co[lane] = co;
-    s_rs[lane] = rs;
-    const uint32_t roff = lane < min(nrec, REC_DIR) ? dir[(uint64_t)c * REC_DIR + lane] : 0u;
-    bool broken = false;
-    for (uint32_t w0 = 0; w0 < T && !broken; w0 += REC_STAGE) {
-      const uint32_t w1 = min(T, w0 + REC_STAGE);
-      uint32_t before = 0;   // lane j: ids of topic j in the records placed so far
-      RecLoad A, B;
-      issue((uint64_t)ch.x | ((uint64_t)ch.y << 32), A);
-      for (uint32_t r = 0; r < nrec; ++r) {
-        const bool next_dir = r + 1 < nrec && r + 1 < REC_DIR;
-        if (next_dir) issue((uint64_t)(uint32_t)__shfl((int)roff, (int)(r + 1), 64) << 2, B);   // in flight now
-        uint32_t tot;
-        const uint32_t ex = wave_excl_scan(A.cr, lane, &tot);
-        if ((A.hdr & 0xFFFF0000u) != REC_TAG || (A.hdr & 0xFFFFu) != tot || tot > WALK_STAGE) {
-          if (lane == 0) atomicOr(&stats->guard, GUARD_STACK);   // a broken directory or chain: a bug, reported
-          broken = true;
-          break;
-        }
-        s_ex[lane] = ex;
-        s_pos[lane] = co + before - ex;   // + entry index q = the entry's offset in the chunk's output
-        before += A.cr;
-        wave_sync();
-#pragma unroll
-        for (uint32_t k = 0; k < REC_IPL; ++k) {
-          const uint32_t q = lane + 64u * k;
-          if (q < tot) {
-            uint32_t o = 0;
-#pragma unroll
-            for (uint32_t step = 32; step >= 1; step >>= 1)
-              if (s_ex[o + step] <= q) o += step;
-            const uint32_t p = s_pos[o] + q;
-            if (p >= w0 && p < w1) stage[p - w0] = A.v[k];
-          }
-        }
-        wave_sync();
-        if (r + 1 < nrec && !next_dir) {   // past the directory: the chain (rare: a chunk of > REC_DIR records)
-          uint64_t o = A.off + rec_size(tot);
-          if (o + REC_HDR <= rec_cap && (rec[o] & 0xFFFF0000u) == REC_JUMP)   // wave-uniform
-            o = (uint64_t)rec[o + 2] | ((uint64_t)rec[o + 3] << 32);
-          issue(o, B);
-        }
-        A = B;
-      }
-      if (broken) break;
-      // the window out: whole lines
-      if (topic) {   // walk-order rows: the chunk's rows are one run from the first topic's row
-        const uint64_t base = s_rs[0];
-#pragma unroll 4
-        for (uint32_t p = w0 + lane; p < w1; p += 64) ids[base + p] = stage[p - w0];
-      } else {       // input order: a run per row
-#pragma unroll 4
-        for (uint32_t p = w0 + lane; p < w1; p += 64) {
-          uint32_t o = 0;
-#pragma unroll
-          for (uint32_t step = 32; step >= 1; step >>= 1)
-            if (s_co[o + step] <= p) o += step;
-          ids[s_rs[o] + (p - s_co[o])] = stage[p - w0];
-        }
-      }
-      wave_sync();
-    }
-  }
-}
-
-// The gathered form of k_rec_rows (round 5, the default): one wave per chunk
-// writes the chunk's output IN ORDER — lane p of a sweep takes output id p of
-// the chunk, finds its topic (a 6-step search over the topics' chunk
-// offsets) and the record holding it (a search over that topic's running
-// counts across the chunk's records), and gathers it from there — so every
-// store instruction writes 256 contiguous bytes, and only the line the sweep
-// is on is ever partly written (k_rec_rows: 4.1 GB written per C2 batch for
-// 1.99 GB of ids).  The gathers hit the ~nrec record lines the sweep is on
-// (L1/L2).  The chunk's record table — per record and topic the ids before it
-// and the offset inside the record — is built in LDS from the records'
-// counts, which come from the directory in one round.  A chunk of more than
-// REC_TAB records is left to k_rec_rows (launched after, for those chunks
-// only).
-#ifndef EGM_REC_UNROLL
-#define EGM_REC_UNROLL 8   // sweep steps (64 ids each) with their gathers in flight together
-#endif
-constexpr uint32_t REC_UNROLL = EGM_REC_UNROLL;
-constexpr int GATHER_WAVES = 4;
-static_assert(REC_TAB <= REC_DIR, "the table comes from the directory");
-__global__ __launch_bounds__(64 * GATHER_WAVES) void k_rec_gather(const uint32_t* __restrict__ rec,
-                                                                  uint64_t rec_cap,
-                                                                  const uint4* __restrict__ chunks,
-                                                                  const uint32_t* __restrict__ dir,
-                                                                  const uint64_t* __restrict__ order, uint32_t n,
-                                                                  const uint64_t* __restrict__ row_ptr,
-                                                                  uint32_t* __restrict__ topic,
-                                                                  uint32_t* __restrict__ ids, uint64_t ids_cap,
-                                                                  MatchStats* stats) {
-  __shared__ uint32_t s_bf[GATHER_WAVES][REC_TAB + 1][64];   // ids of topic j before record r (row r = nrec: its total)
-  __shared__ uint16_t s_ex[GATHER_WAVES][REC_TAB][64];       // topic j's first entry inside record r
-  __shared__ uint32_t s_ro[GATHER_WAVES][REC_TAB];           // record r's offset (u32 units / 4)
-  __shared__ uint32_t s_co[GATHER_WAVES][65];                // topic j's offset in the chunk's output (65: T)
-  __shared__ uint64_t s_rs[GATHER_WAVES][64];                // topic j's row start
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool ok = compact_checks(row_ptr, n, ids_cap, stats);
-  const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
-  uint32_t(*bf)[64] = s_bf[wave];
-  uint16_t(*exr)[64] = s_ex[wave];
-  for (uint32_t c = blockIdx.x * GATHER_WAVES + wave; c < nchunks; c += gridDim.x * GATHER_WAVES) {
-    const uint32_t t = c * WALK_CHUNK + lane;
-    const bool act = t < n;
-    const uint32_t my_t = act ? (order ? (uint32_t)order[t] : t) : 0u;
-    if (topic && act) topic[t] = my_t;   // written even when the rows are not (overflow): the map is the order
-    const uint4 ch = chunks[c];
-    const uint32_t nrec = ch.z;
-    if (!ok || !(ch.w & CHUNK_WALKED) || nrec == 0 || nrec > REC_TAB) continue;
-    const uint32_t row = topic ? t : my_t;
-    const uint64_t rs = act ? row_ptr[row] : 0ull;
-    const uint32_t ro = lane < nrec ? dir[(uint64_t)c * REC_DIR + lane] : 0u;
-    // the records' headers and counts, all in one round: lane (r, j/2) reads two counts of record r
-    uint32_t cpair[(REC_TAB * 32 + 63) / 64], hdr = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < (REC_TAB * 32 + 63) / 64; ++k) {
-      const uint32_t i = lane + 64u * k, r = i >> 5;
-      const uint32_t o = (uint32_t)__shfl((int)ro, (int)min(r, nrec - 1), 64);
-      cpair[k] = r < nrec ? rec[((uint64_t)o << 2) + REC_HDR + (i & 31u)] : 0u;
-    }
-    if (lane < nrec) hdr = rec[(uint64_t)ro << 2];
-    uint32_t cnt = act ? (uint32_t)(row_ptr[row + 1] - rs) : 0u;
-    uint32_t T;
-    const uint32_t co = wave_excl_scan(cnt, lane, &T);
-    s_co[wave][lane] = co;
-    if (lane == 0) s_co[wave][64] = T;
-    s_rs[wave][lane] = rs;
-    if (lane < nrec) s_ro[wave][lane] = ro;
-    // counts -> LDS (as u16 pairs, the record's layout), then per record its scan and the running totals
-#pragma unroll
-    for (uint32_t k = 0; k < (REC_TAB * 32 + 63) / 64; ++k) {
-      const uint32_t i = lane + 64u * k;
-      if ((i >> 5) < nrec) ((uint32_t*)exr[i >> 5])[i & 31u] = cpair[k];
-    }
-    wave_sync();
-    bool bad = lane < nrec && ((hdr & 0xFFFF0000u) != REC_TAG);
-    uint32_t run = 0;
-    for (uint32_t r = 0; r < nrec; ++r) {   // lane j: topic j
-      const uint32_t cr = exr[r][lane];
-      uint32_t tot;
-      const uint32_t ex = wave_excl_scan(cr, lane, &tot);
-      bad |= tot != (uint32_t)__shfl((int)(hdr & 0xFFFFu), (int)r, 64);
-      wave_sync();
-      exr[r][lane] = (uint16_t)ex;
-      bf[r][lane] = run;
-      run += cr;
-    }
-    bf[nrec][lane] = run;
-    bad |= act && run != cnt;
-    if (__ballot(bad)) {
-      if (lane == 0) atomicOr(&stats->guard, GUARD_STACK);   // a broken directory or record: a bug, reported
-      wave_sync();
-      continue;
-    }
-    wave_sync();
-    // the sweep: output id p of the chunk, REC_UNROLL x 64 at a time
-    const uint64_t base = s_rs[wave][0];
-    for (uint32_t p0 = 0; p0 < T; p0 += 64u * REC_UNROLL) {
-      uint32_t v[REC_UNROLL];
-      uint64_t d[REC_UNROLL];
-#pragma unroll
-      for (uint32_t k = 0; k < REC_UNROLL; ++k) {
-        const uint32_t p = min(p0 + 64u * k + lane, T - 1);
-        uint32_t o = 0;   // the topic: last j with co[j] <= p (an empty topic never wins: the next has the same co)
-#pragma unroll
-        for (uint32_t step = 32; step >= 1; step >>= 1)
-          if (s_co[wave][o + step] <= p) o += step;
-        const uint32_t q = p - s_co[wave][o];
-        uint32_t r = 0;   // the record: last r with bf[r][o] <= q (q < the topic's total)
-#pragma unroll
-        for (uint32_t step = REC_TAB / 2; step >= 1; step >>= 1)
-          if (r + step < nrec && bf[r + step][o] <= q) r += step;
-        const uint64_t src = ((uint64_t)s_ro[wave][r] << 2) + REC_IDS + exr[r][o] + (q - bf[r][o]);
-        v[k] = rec[src];
-        d[k] = topic ? base + p : s_rs[wave][o] + q;
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < REC_UNROLL; ++k)
-        if (p0 + 64u * k + lane < T) ids[d[k]] = v[k];
-    }
-    wave_sync();
   }
 }
 
@@ -1970,27 +1736,16 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   const uint32_t cblocks =
       (uint32_t)std::min<uint64_t>(EGM_COMPACT_BLOCKS, std::max<uint64_t>(256, ((uint64_t)n + 63) / 64));
 #ifndef EGM_REC_ROWS
-#define EGM_REC_ROWS 3   // 3: k_rec_burst; 2: k_rec_gather (+ k_rec_rows for chunks of > REC_TAB records); 1: staged; 0: direct (A/B)
+#define EGM_REC_ROWS 1   // 1: k_rec_burst; 0: k_rec_rows (A/B)
 #endif
   const uint32_t rblocks = (uint32_t)std::min<uint64_t>(
       65536, std::max<uint64_t>(1, (((uint64_t)n + 63) / 64 + REC_WAVES - 1) / REC_WAVES));
-#if EGM_REC_ROWS == 3
+#if EGM_REC_ROWS
   hipLaunchKernelGGL(k_rec_burst, dim3(rblocks), dim3(64 * REC_WAVES), 0, s, w.rec, w.rec_cap, w.chunks, w.dir,
                      w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats);
-#elif EGM_REC_ROWS == 2
-  const uint32_t gblocks = (uint32_t)std::min<uint64_t>(
-      65536, std::max<uint64_t>(1, (((uint64_t)n + 63) / 64 + GATHER_WAVES - 1) / GATHER_WAVES));
-  hipLaunchKernelGGL(k_rec_gather, dim3(gblocks), dim3(64 * GATHER_WAVES), 0, s, w.rec, w.rec_cap, w.chunks, w.dir,
-                     w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats);
+#else   // A/B: one record at a time, the next in flight
   hipLaunchKernelGGL(k_rec_rows, dim3(rblocks), dim3(64 * REC_WAVES), 0, s, w.rec, w.rec_cap, w.chunks, w.dir,
-                     w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats, true);
-#elif EGM_REC_ROWS == 1
-  const uint32_t sblocks = (uint32_t)std::min<uint64_t>(256ull * 10, std::max<uint64_t>(1, ((uint64_t)n + 63) / 64));
-  hipLaunchKernelGGL(k_rec_rows_staged, dim3(sblocks), dim3(64), 0, s, w.rec, w.rec_cap, w.chunks, w.dir,
                      w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats);
-#else
-  hipLaunchKernelGGL(k_rec_rows, dim3(rblocks), dim3(64 * REC_WAVES), 0, s, w.rec, w.rec_cap, w.chunks, w.dir,
-                     w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats, false);
 #endif
   trace(s, "k_rec_rows");
   hipLaunchKernelGGL(k_compact, dim3(cblocks), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.ids_tmp, n, out.row_ptr,
