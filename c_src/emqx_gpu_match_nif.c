@@ -20,6 +20,7 @@
  *                      died), its destructor calls egm_match_cancel, so a dead
  *                      waiter never keeps a pipeline slot busy.
  *   cancel/2        -> egm_match_cancel
+ *   subs_delta/3    -> egm_subs_apply_delta + egm_subs_commit (subscriber changes)
  *   subs_build/2    -> egm_subs_build      (filter id -> subscriber ids: the
  *                      emqx_subscriber bag flattened, emqx_broker.erl:116-162)
  *   publish_batch/2 -> egm_match_batch (routes mode) + egm_fanout_batch: the
@@ -345,6 +346,51 @@ static ERL_NIF_TERM nif_subs_build(ErlNifEnv* env, int argc, const ERL_NIF_TERM 
   return rc ? error_tuple(env, r->ctx, rc) : ATOM_OK;
 }
 
+/* [{FilterId, Sub}] -> egm_sub_pair[] (malloc'd; *n pairs); 0 on a bad term */
+static int get_pairs(ErlNifEnv* env, ERL_NIF_TERM list, egm_sub_pair** out, unsigned* n) {
+  ERL_NIF_TERM head, tail = list;
+  if (!enif_get_list_length(env, list, n)) return 0;
+  *out = (egm_sub_pair*)malloc(sizeof(egm_sub_pair) * (*n ? *n : 1));
+  if (!*out) return 0;
+  for (unsigned i = 0; i < *n; ++i) {
+    const ERL_NIF_TERM* el;
+    int arity;
+    unsigned f, sub;
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_tuple(env, head, &arity, &el) || arity != 2 ||
+        !enif_get_uint(env, el[0], &f) || !enif_get_uint(env, el[1], &sub)) {
+      free(*out);
+      *out = NULL;
+      return 0;
+    }
+    (*out)[i].fid = f;
+    (*out)[i].sub = sub;
+  }
+  return 1;
+}
+
+/* subs_delta(Ctx, Adds, Dels) -> {ok, Epoch} | {error, _}: the subscriber
+   changes since the last call ({FilterId, Sub} pairs; a $share group as
+   GroupId bor 16#80000000) in one epoch of the fan-out's table —
+   emqx_broker:subscribe/3, unsubscribe/1 and subscriber_down/1
+   (emqx_broker.erl:144-197, 331-345). */
+static ERL_NIF_TERM nif_subs_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  egm_res_t* r;
+  egm_sub_pair *add = NULL, *del = NULL;
+  unsigned na = 0, nd = 0;
+  if (argc != 3 || !get_ctx(env, argv[0], &r)) return enif_make_badarg(env);
+  if (!get_pairs(env, argv[1], &add, &na)) return enif_make_badarg(env);
+  if (!get_pairs(env, argv[2], &del, &nd)) {
+    free(add);
+    return enif_make_badarg(env);
+  }
+  uint64_t epoch = 0;
+  int rc = egm_subs_apply_delta(r->ctx, add, na, del, nd);
+  if (!rc) rc = egm_subs_commit(r->ctx, &epoch);
+  free(add);
+  free(del);
+  return rc ? error_tuple(env, r->ctx, rc) : enif_make_tuple2(env, ATOM_OK, enif_make_uint64(env, epoch));
+}
+
 /* publish_batch(Ctx, [Topic]) -> {ok, [{[FilterId], [{FilterId, Sub}]}]} | {error, _} */
 static ERL_NIF_TERM nif_publish_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   egm_res_t* r;
@@ -387,6 +433,7 @@ static ErlNifFunc nif_funcs[] = {
     {"wait", 2, nif_wait, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"cancel", 2, nif_cancel, 0},
     {"subs_build", 2, nif_subs_build, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"subs_delta", 3, nif_subs_delta, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"publish_batch", 2, nif_publish_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
 };
 

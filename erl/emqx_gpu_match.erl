@@ -18,7 +18,7 @@
 -module(emqx_gpu_match).
 
 -export([open/1, build/2, apply_delta/3, match_batch/3, submit/3, wait/2, cancel/2, subs_build/2,
-         publish_batch/2]).
+         subs_delta/3, publish_batch/2]).
 -export([init/0, ctx/0, filter_of/1, filters_of/1, build/1, sync/2, match/1, match_routes/1]).
 
 -on_load(load_nif/0).
@@ -43,6 +43,7 @@ submit(_Ctx, _Topics, _Mode) -> erlang:nif_error(nif_not_loaded).
 wait(_Ctx, _Ticket) -> erlang:nif_error(nif_not_loaded).
 cancel(_Ctx, _Ticket) -> erlang:nif_error(nif_not_loaded).
 subs_build(_Ctx, _SubsByFilterId) -> erlang:nif_error(nif_not_loaded).
+subs_delta(_Ctx, _Adds, _Dels) -> erlang:nif_error(nif_not_loaded).
 publish_batch(_Ctx, _Topics) -> erlang:nif_error(nif_not_loaded).
 
 %% ---------------------------------------------------------------------
