@@ -130,6 +130,10 @@ for step in "$@"; do
     ab_*)   # A/B variant built by tools/build_variant.py: C2 bench under rocprof stats
       v=${step#ab_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$v" -o run --output-format csv -- $B --steps 10 --warmup 2 --cpu-baseline off --host-e2e off ;;
+    c3ab_*)   # the C3 bench line (no profiler) on variant V (c3ab_default: the default library)
+      v=${step#c3ab_}
+      lib=$R/emqx_amd/libemqx_gpu_match_$v.so; [ "$v" = default ] && lib=$R/emqx_amd/libemqx_gpu_match.so
+      EGM_LIB=$lib run "$step" 900 $B --config c3 --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
     chunkhist) run chunkhist 600 env PYTHONPATH=$R python $R/tools/chunk_hist.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
