@@ -72,6 +72,9 @@ for step in "$@"; do
     pmc)
       run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_fetch" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
       run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc_write" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
+    pmc_c3)   # FETCH_SIZE / WRITE_SIZE passes over the C3 bench (depth 16, the deep pass)
+      run pmc_c3_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_c3_fetch" -o run --output-format csv -- $B --config c3 --steps 2 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
+      run pmc_c3_write 600 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc_c3_write" -o run --output-format csv -- $B --config c3 --steps 2 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
     pmc_c4)   # FETCH_SIZE / WRITE_SIZE passes over the C4 bench (100M filters, match + fan-out)
       run pmc_c4_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc_c4_fetch" -o run --output-format csv -- $B --config c4 --steps 2 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
       run pmc_c4_write 600 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc_c4_write" -o run --output-format csv -- $B --config c4 --steps 2 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
