@@ -12,7 +12,7 @@ for d in sorted(glob.glob(os.path.join(root, f"{tag}_pmc_*"))):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         acc = collections.defaultdict(lambda: [0.0, 0])
         for r in csv.DictReader(open(f)):
-            k = (r["Kernel_Name"].split("(")[0].replace("egm::", ""), r["Counter_Name"])
+            k = (r["Kernel_Name"].split("(")[0].replace("egm::", "").replace("void ", ""), r["Counter_Name"])
             acc[k][0] += float(r["Counter_Value"])
             acc[k][1] += 1
         for (kn, cn), (v, c) in sorted(acc.items()):
