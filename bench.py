@@ -327,7 +327,8 @@ class PrefixLeg:
     + its prefixes, global ids) in `gm`, its own topic batch in HBM; a step
     routes the batch (egm_prefix_route), exchanges the slots with one
     all_to_all_single and matches each received slot in place
-    (egm_match_device_counted: the slot's count is read on the device)."""
+    (egm_match_device_counted_ordered: the slot's count is read on the device,
+    rows in the walk's order as the replicate leg's)."""
 
     def __init__(self, gm, f, t, rank, world, dev, stream, mode, have_pg, slack=1.25):
         import torch
@@ -357,7 +358,8 @@ class PrefixLeg:
     def _make(self, ps):
         from emqx_amd.dist import PrefixExchange, gpu_prefix_stages
         self.ex = PrefixExchange(self.rank, self.world, self.dev, ps,
-                                 gpu_prefix_stages(self.gm, self.d_vr, self.mode, self.sp, self.ids_per_topic))
+                                 gpu_prefix_stages(self.gm, self.d_vr, self.mode, self.sp, self.ids_per_topic,
+                                                   ordered=True))
 
     @property
     def ps(self):

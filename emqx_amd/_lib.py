@@ -103,6 +103,8 @@ SIGNATURES = {
     "egm_match_device_ordered": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, _P, _P, _P, C.c_uint64]),
     "egm_match_device_counted": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, _P, C.c_int, _P, _P, _P,
                                            C.c_uint64]),
+    "egm_match_device_counted_ordered": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, _P, C.c_int, _P, _P, _P, _P,
+                                                   C.c_uint64]),
     "egm_last_stats": (C.c_int, [_P, _u64p, _u64p, _u32p, _u32p, _u32p]),
     "egm_last_guard": (C.c_int, [_P, _u32p]),
     "egm_last_walk_counters": (C.c_int, [_P, _u64p, _u64p, _u64p, _u64p, _u64p]),

@@ -1077,6 +1077,13 @@ int egm_match_device_ordered(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_by
 int egm_match_device_counted(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_off,
                              uint32_t n_max, const uint32_t* d_n, int mode, void* hip_stream, uint64_t* d_row,
                              uint32_t* d_ids, uint64_t ids_cap) {
+  return egm_match_device_counted_ordered(c, d_blob, blob_bytes, d_off, n_max, d_n, mode, hip_stream, d_row, nullptr,
+                                          d_ids, ids_cap);
+}
+
+int egm_match_device_counted_ordered(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_off,
+                                     uint32_t n_max, const uint32_t* d_n, int mode, void* hip_stream, uint64_t* d_row,
+                                     uint32_t* d_topic, uint32_t* d_ids, uint64_t ids_cap) {
   if (!c || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES) || !d_row || !d_n) return EGM_E_INVAL;
   if (n_max && (!d_blob || !d_off || ((uintptr_t)d_blob & 3))) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
@@ -1086,7 +1093,7 @@ int egm_match_device_counted(egm_ctx* c, const uint8_t* d_blob, uint64_t blob_by
   int r = ensure_work(c, W, n_max, blob_bytes, ids_cap, std::min<uint64_t>(blob_bytes, 65535) + 1);
   if (r) return r;
   std::shared_ptr<Epoch> ep = c->cur;
-  r = run_match(c, W, *ep, d_blob, d_off, n_max, mode, s, d_row, d_ids, ids_cap, d_n);
+  r = run_match(c, W, *ep, d_blob, d_off, n_max, mode, s, d_row, d_ids, ids_cap, d_n, d_topic);
   ws_done(W, s);
   return r;
 }
@@ -1857,7 +1864,9 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   if (nids > mids_len) return c->fail(EGM_E_OVERFLOW, "match row total exceeds the id buffer (overflowed match batch)");
   const uint64_t nwin = (nids + 63) / 64;
   if ((e = c->f_dc.ensure((nwin + 1) * 4)) != hipSuccess) return c->hip_fail(e, "f_dc");   // window totals
-  if ((e = c->f_ds0.ensure((nids + 1) * 16)) != hipSuccess) return c->hip_fail(e, "f_ds0");   // entry records
+  const bool ord = c->last_walk.order && c->last_walk.row == d_mrow && c->last_walk.n == n;
+  if (fan_uses_ds0(ord) && (e = c->f_ds0.ensure((nids + 1) * 16)) != hipSuccess)
+    return c->hip_fail(e, "f_ds0");   // entry records (the two-pass form)
   if ((e = c->f_wbase.ensure((nwin + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_wbase");
   if (!d_entry_pos && (e = c->f_dpos.ensure((nids + 2) * 8)) != hipSuccess) return c->hip_fail(e, "f_dpos");
   uint64_t* dpos = d_entry_pos ? d_entry_pos : c->f_dpos.as<uint64_t>();   // the caller's, in the compact form
@@ -1873,7 +1882,6 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
   c->work_begin(s);
   // these rows are the last match's: count in its walk order (the workspace
   // holding it is then protected until this fan-out has read it)
-  const bool ord = c->last_walk.order && c->last_walk.row == d_mrow && c->last_walk.n == n;
   MatchWs* OW = ord ? &c->ws[c->last_walk.ws] : nullptr;
   if (OW && OW->used && OW->stream != s && OW->ev) hipStreamWaitEvent(s, OW->ev, 0);   // (stream 0 is a stream too)
   e = launch_fanout(st, d_mrow, d_mids, n, nids, d_drow, d_fid, d_sub, cap, c->f_dc.as<uint32_t>(),
@@ -1909,6 +1917,7 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
         (e = hipMemcpyAsync(&ovf, c->f_ovf.p, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipStreamSynchronize(s)) != hipSuccess)
       return c->hip_fail(e, "fanout readback");
+    if (ovf & 2u) return c->fail(EGM_E_DEVICE, "fan-out look-back guard tripped");
     if (ovf) return EGM_E_OVERFLOW;
   }
   return EGM_OK;

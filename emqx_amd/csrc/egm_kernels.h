@@ -179,6 +179,7 @@ struct SubTable {
   uint32_t n_fid_slots;
   const uint4* rp;                // [n_fid_slots] subscriber records (launch_sub_pairs, egm_kernels.hip)
 };
+bool fan_uses_ds0(bool walk_order_known);   // launch_fanout needs its ds0 buffer ((nids + 1) x 16 B)
 hipError_t launch_sub_pairs(const uint64_t* row, const uint32_t* subs, uint32_t n_slots, uint4* rp, hipStream_t s);
 // walk_order (optional): the batch's walk order (sort values, topic in the low
 // 32 bits, MatchWork::order) — the count then reads the subscriber records of

@@ -40,7 +40,8 @@ constexpr int TOK_BLOCK = 256;
 #endif
 constexpr int TOK_LDS = EGM_TOK_LDS;
 #ifndef EGM_TOK_WORDS
-#define EGM_TOK_WORDS 2048   // words per tokenise block (9 B of LDS each; 34 KB per block -> 4 blocks per CU)
+#define EGM_TOK_WORDS 2560   // words per tokenise block (7 B of LDS each; 40 KB per block -> 4 blocks per CU;
+                             // 2048 made C3's segments of 128 depth-16 topics retry as two of 64)
 #endif
 constexpr int TOK_WORDS = EGM_TOK_WORDS;
 #ifndef EGM_TOK_U
@@ -250,9 +251,9 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
                                                         uint8_t* __restrict__ tfl, WalkOrderOut wo) {
   __shared__ __attribute__((aligned(16))) uint32_t sw[TOK_LDS / 4 + 1];   // +1: lds_word reads one word past
   __shared__ uint32_t wpos[TOK_WORDS];   // start | len << 16 (LDS byte index)
-  __shared__ uint32_t wdst[TOK_WORDS];   // index into wid[]
+  __shared__ uint16_t wlv[TOK_WORDS];    // level of the word in its topic (a segment holds < 2^16 words)
   __shared__ uint8_t wtop[TOK_WORDS];    // topic within the segment
-  __shared__ uint32_t tg[TOK_BLOCK];     // wid index of the topic's word 0 (a word's level = wdst - tg)
+  __shared__ uint32_t tg[TOK_BLOCK];     // wid index of the topic's word 0 (a word's is tg + its level)
   __shared__ uint32_t kw[TOK_BLOCK][KEY_LEVELS];   // the topic's first word ids (walk-order key)
   __shared__ uint32_t tflag[TOK_BLOCK];   // TF_* flags | levels << 8
   __shared__ uint32_t wsum[TOK_BLOCK / 64];
@@ -357,14 +358,14 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
           const uint32_t p = q + (__builtin_ctz(m) >> 3);
           m &= m - 1;
           wpos[ex + l] = ws | ((p - ws) << 16);
-          wdst[ex + l] = g + l;
+          wlv[ex + l] = (uint16_t)l;
           wtop[ex + l] = (uint8_t)tid;
           ++l;
           ws = p + 1;
         }
       }
       wpos[ex + l] = ws | ((ts + len - ws) << 16);
-      wdst[ex + l] = g + l;
+      wlv[ex + l] = (uint16_t)l;
       wtop[ex + l] = (uint8_t)tid;
       tg[tid] = g;
       lv[t] = D;
@@ -412,12 +413,12 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         if (wo.key) {
           // sorted batch: a topic of <= FIX_WORDS levels is read only at the
           // fixed stride (its record's fixed bit), so wid[] is not written
-          const uint32_t tt = wtop[i], l = wdst[i] - tg[tt];
+          const uint32_t tt = wtop[i], l = wlv[i];
           if (l < KEY_LEVELS) kw[tt][l] = res[u];
           if ((tflag[tt] >> 8) <= FIX_WORDS) wo.wfix[(uint64_t)(t0 + tt) * FIX_WORDS + l] = res[u];
-          else wid[wdst[i]] = res[u];
+          else wid[tg[tt] + l] = res[u];
         } else {
-          wid[wdst[i]] = res[u];
+          wid[tg[wtop[i]] + wlv[i]] = res[u];
         }
       }
     }
@@ -476,7 +477,7 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #define EGM_WALK_STACK 320   // items (16 B) per wave: chunks of up to DEEP_MIN levels
 #endif
 #ifndef EGM_WALK_STACK_DEEP
-#define EGM_WALK_STACK_DEEP 640   // items per wave of the deep pass (deeper chunks: C3's wide frontiers)
+#define EGM_WALK_STACK_DEEP 448   // items per wave of the deep pass (deeper chunks: C3's wide frontiers; 640 until r5)
 #endif
 #ifndef EGM_WALK_DEEP_MIN
 #define EGM_WALK_DEEP_MIN 12   // a chunk with a deeper topic is walked by the deep pass
@@ -1629,10 +1630,30 @@ int walk_grid_blocks(uint32_t n) {
   return blocks ? (int)blocks : 1;
 }
 
-// The deep pass: 10 waves per CU fit its LDS; a grid stride over the chunks handed to it.
+// The deep pass: a grid stride over the chunks handed to it, exactly as many
+// waves as are resident together (its LDS stack sets that: 14 per CU at 448
+// items).  A wave that does not fit would start only when another ends, with
+// a whole share of chunks still to walk: C3 measured 59 ms at 10 waves per CU
+// and 640 items, 80 ms when an 11th was asked for, 53 ms at 14 waves of 448
+// items (r5 A/B).  EGM_DEEP_WAVES forces a count (A/B).
+#ifndef EGM_DEEP_WAVES
+#define EGM_DEEP_WAVES 0   // 0: the occupancy the runtime reports for k_walk<true>
+#endif
+static uint32_t deep_waves_per_cu() {
+  static const uint32_t v = [] {
+    int nb = EGM_DEEP_WAVES;
+    if (nb <= 0 &&
+        (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_walk<true>, 64, 0) != hipSuccess || nb <= 0))
+      nb = 8;
+    return (uint32_t)std::min(nb, 32);
+  }();
+  return v;
+}
+
 int deep_grid_blocks(uint32_t n) {
   const uint32_t chunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
-  uint32_t blocks = chunks < 256u * 10u ? chunks : 256u * 10u;
+  const uint32_t per = 256u * deep_waves_per_cu();
+  uint32_t blocks = chunks < per ? chunks : per;
   blocks = (blocks + 7) & ~7u;
   return blocks ? (int)blocks : 1;
 }
@@ -1771,6 +1792,9 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
 // subscribers (C4: 92 % of filters; the record travels to the fill as the
 // entry's 16-B dsrc): the fill's random row reads were a 64-B line per
 // entry for ~14 B of subscribers.
+#ifndef EGM_FAN_DS0
+#define EGM_FAN_DS0 1   // 1: the count pass copies each entry's record to ds0 for the fill; 0: the fill re-reads it (A/B)
+#endif
 constexpr uint32_t FAN_CNT_BITS = 24;
 constexpr uint32_t FAN_CNT_SAT = (1u << FAN_CNT_BITS) - 1;   // saturated: the fill reads the exact count from row[]
 constexpr uint32_t FAN_INLINE_ALL = 3;   // a row this short is carried whole in its record
@@ -1815,7 +1839,9 @@ __global__ __launch_bounds__(256) void k_fan_count(const uint32_t* __restrict__ 
       const bool ok = i < nids && f[u] < st.n_fid_slots;
       const uint32_t cs = ok ? rec_count(r[u]) : 0u;
       const uint32_t c = cs == FAN_CNT_SAT ? (uint32_t)min(st.row[f[u] + 1] - st.row[f[u]], (uint64_t)0xFFFFFFFFu) : cs;
+#if EGM_FAN_DS0
       if (i < nids) ds0[i] = ok ? r[u] : make_uint4(0, 0, 0, 0);
+#endif
       uint32_t sum = c;
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
@@ -1920,14 +1946,80 @@ __global__ __launch_bounds__(256) void k_fan_rows(const uint64_t* __restrict__ m
 
 constexpr int FAN_WAVES = 4;
 constexpr uint32_t FAN_BIG = 128;   // entries with this many subscribers are copied by the whole wave
-// One wave per window of 64 match entries, whose deliveries are contiguous:
-// the entry offsets (dpos, the compact form's output and the rows' source)
-// come from the window's scanned total plus a wave scan of the entries'
-// counts; then small rows are written lane per delivery (owner found by a
-// 6-step LDS search; a row's first two subscribers come with its record, the
-// rest from the subscriber table) and big rows streamed by the whole wave.
-// An overflowed batch (total > cap) still gets its offsets, so the caller
-// learns the size.
+
+struct FanLds {   // one wave's window of 64 entries
+  uint32_t pre[64], off[64], fid[64], cnt[64], in0[64], in1[64], in2[64];
+  uint64_t src[64];
+};
+
+// The deliveries of one window of 64 match entries, whose deliveries are
+// contiguous from `base`: small rows lane per delivery (the owning entry found
+// by a 6-step LDS search; a row's first subscribers come with its record v,
+// the rest from the subscriber table), big rows streamed by the whole wave.
+// Only deliveries below `cap` are written.
+__device__ __forceinline__ void fan_window(FanLds& L, const SubTable& st, uint32_t lane, uint32_t f, uint4 v,
+                                           uint32_t c, uint32_t off, uint64_t base, uint32_t* __restrict__ dfid,
+                                           uint32_t* __restrict__ dsub, uint64_t cap) {
+  const bool big = c >= FAN_BIG;
+  uint32_t tot_s;
+  const uint32_t pre_s = wave_excl_scan(big ? 0u : c, lane, &tot_s);   // small entries, packed
+  L.pre[lane] = pre_s;
+  L.off[lane] = off;
+  L.fid[lane] = f;
+  L.cnt[lane] = c;
+  L.src[lane] = rec_start(v);   // (meaningful only past FAN_INLINE_ALL subscribers)
+  L.in0[lane] = v.z;
+  L.in1[lane] = v.w;
+  L.in2[lane] = v.x;
+  wave_sync();
+  for (uint32_t q = lane; q < tot_s; q += 64) {
+    // the last k with pre[k] <= q (an entry with no small deliveries shares its
+    // successor's pre, so the last one found has deliveries)
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t b = 32; b; b >>= 1)
+      if (L.pre[k + b] <= q) k += b;
+    const uint32_t o = q - L.pre[k];
+    const uint64_t d = base + L.off[k] + o;
+    if (d >= cap) continue;
+    if (dfid) dfid[d] = L.fid[k];   // null: the compact form (the entry offsets give the filter)
+    const uint32_t inl = L.cnt[k] <= FAN_INLINE_ALL ? FAN_INLINE_ALL : 2u;   // subscribers in the record
+    uint32_t sub;
+    if (o >= inl) sub = st.subs[L.src[k] + o];   // only these lanes read the table
+    else sub = o == 0 ? L.in0[k] : (o == 1 ? L.in1[k] : L.in2[k]);
+    dsub[d] = sub;
+  }
+  // big entries (C4: 2 000-subscriber filters): the wave streams the row, 4 per lane in flight
+  for (uint64_t mb = __ballot(big); mb; mb &= mb - 1) {
+    const uint32_t k = (uint32_t)__builtin_ctzll(mb);
+    const uint32_t cnt = L.cnt[k], fk = L.fid[k];
+    const uint64_t src = L.src[k], dst = base + L.off[k];
+    for (uint32_t j0 = lane; j0 < cnt; j0 += 256) {
+      uint32_t vv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) vv[r] = st.subs[src + min(j0 + 64u * r, cnt - 1)];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (j0 + 64u * r < cnt && dst + j0 + 64u * r < cap) {
+          if (dfid) dfid[dst + j0 + 64u * r] = fk;
+          dsub[dst + j0 + 64u * r] = vv[r];
+        }
+    }
+  }
+  wave_sync();
+}
+
+// The subscriber count of a matched entry from its record.
+__device__ __forceinline__ uint32_t fan_count_of(const SubTable& st, uint32_t f, uint4 v) {
+  const uint32_t c = rec_count(v);
+  return c == FAN_CNT_SAT ? (uint32_t)min(st.row[f + 1] - st.row[f], (uint64_t)0xFFFFFFFFu) : c;   // rare: 2^24+
+}
+
+// Two-pass form (EGM_FAN_FUSED=0, A/B): one wave per window of 64 match
+// entries; the entry offsets (dpos, the compact form's output and the rows'
+// source) come from the window's scanned total plus a wave scan of the
+// entries' counts.  An overflowed batch (total > cap) still gets its offsets,
+// so the caller learns the size.
 __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __restrict__ mids, uint64_t nids,
                                                              SubTable st, const uint64_t* __restrict__ wbase,
                                                              const uint4* __restrict__ ds0,
@@ -1937,70 +2029,127 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
   const uint64_t nwin = (nids + 63) / 64;
   const bool ovf = wbase[nwin] > cap;
   if (ovf && blockIdx.x == 0 && threadIdx.x == 0) *overflow = 1u;
-  __shared__ uint32_t s_pre[FAN_WAVES][64], s_off[FAN_WAVES][64], s_fid[FAN_WAVES][64], s_cnt[FAN_WAVES][64];
-  __shared__ uint32_t s_in0[FAN_WAVES][64], s_in1[FAN_WAVES][64], s_in2[FAN_WAVES][64];
-  __shared__ uint64_t s_src[FAN_WAVES][64];
+  __shared__ FanLds S[FAN_WAVES];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (uint64_t w = (uint64_t)blockIdx.x * FAN_WAVES + wave; w < nwin; w += (uint64_t)gridDim.x * FAN_WAVES) {
     const uint64_t w0 = w * 64, i = w0 + lane, ic = min(i, nids - 1);
     const uint64_t base = wbase[w];
-    const uint4 v = ds0[ic];
     const uint32_t f = mids[ic];
-    uint32_t c = i < nids ? rec_count(v) : 0u;
-    if (c == FAN_CNT_SAT)   // a row of 2^24 or more subscribers (rare): its exact count
-      c = (uint32_t)min(st.row[f + 1] - st.row[f], (uint64_t)0xFFFFFFFFu);
+#if EGM_FAN_DS0
+    const uint4 v = ds0[ic];
+#else
+    const uint4 rv = st.rp[f < st.n_fid_slots ? f : 0u];   // unconditional
+    const uint4 v = f < st.n_fid_slots ? rv : make_uint4(0, 0, 0, 0);
+#endif
+    const uint32_t c = i < nids ? fan_count_of(st, f, v) : 0u;
     uint32_t tot;
     const uint32_t off = wave_excl_scan(c, lane, &tot);
     if (i < nids) dpos[i] = base + off;
     if (i == nids - 1) dpos[nids] = base + off + c;
     if (ovf) continue;
-    const bool big = c >= FAN_BIG;
-    uint32_t tot_s;
-    const uint32_t pre_s = wave_excl_scan(big ? 0u : c, lane, &tot_s);   // small entries, packed
-    s_pre[wave][lane] = pre_s;
-    s_off[wave][lane] = off;
-    s_fid[wave][lane] = f;
-    s_cnt[wave][lane] = c;
-    s_src[wave][lane] = rec_start(v);   // (meaningful only past FAN_INLINE_ALL subscribers)
-    s_in0[wave][lane] = v.z;
-    s_in1[wave][lane] = v.w;
-    s_in2[wave][lane] = v.x;
-    wave_sync();
-    // small entries: lane per delivery, the owning entry found by a 6-step search
-    for (uint32_t q = lane; q < tot_s; q += 64) {
-      // the last k with pre[k] <= q (an entry with no small deliveries shares its
-      // successor's pre, so the last one found has deliveries)
-      uint32_t k = 0;
+    fan_window(S[wave], st, lane, f, v, c, off, base, dfid, dsub, cap);
+  }
+}
+
+// Single-pass form (round 5, the default): count, scan and fill in one
+// kernel, so each entry's subscriber record is read once (the two-pass form
+// reads it in the count and again in the fill, or copies it through a
+// 16-B-per-entry buffer).  Windows are taken in ticket order; a wave publishes
+// its window's total, then finds the sum of all earlier windows by the
+// decoupled look-back (Merrill & Garland 2016, "Single-pass Parallel Prefix
+// Scan with Decoupled Look-back"): lane k reads window w-1-k's published
+// state — an aggregate, or an inclusive prefix that ends the look-back — and
+// the wave sums up to the first prefix, then publishes its own prefix.  Every
+// window it waits on took its ticket earlier and is already running, so the
+// wait always ends; a guard bounds it anyway (reported as FAN_GUARD).
+// States: bits 62-63 = 0 not yet / 1 aggregate / 2 inclusive prefix, bits
+// 0-61 the sum.  The deliveries below `cap` are written; dpos always.
+constexpr uint64_t FAN_ST_AGG = 1ull << 62, FAN_ST_PRE = 2ull << 62, FAN_ST_VAL = (1ull << 62) - 1;
+constexpr unsigned int FAN_OVERFLOW = 1u, FAN_GUARD = 2u;
+__device__ __forceinline__ uint64_t st_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#ifndef EGM_FAN_TILE
+#define EGM_FAN_TILE 8   // windows of 64 entries per ticket (one look-back per tile)
+#endif
+constexpr uint32_t FAN_TILE = EGM_FAN_TILE;
+__global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fused(const uint32_t* __restrict__ mids, uint64_t nids,
+                                                              SubTable st, uint64_t* __restrict__ state,
+                                                              unsigned int* __restrict__ ticket,
+                                                              uint64_t* __restrict__ dpos,
+                                                              uint32_t* __restrict__ dfid, uint32_t* __restrict__ dsub,
+                                                              uint64_t cap, unsigned int* overflow) {
+  __shared__ FanLds S[FAN_WAVES];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t ntiles = (nids + 64 * FAN_TILE - 1) / (64 * FAN_TILE);
+  for (;;) {
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(ticket, 1u);
+    const uint64_t b = uni((uint32_t)__shfl((int)tk, 0, 64));
+    if (b >= ntiles) break;
+    const uint64_t i0 = b * 64 * FAN_TILE + lane;
+    uint32_t f[FAN_TILE], c[FAN_TILE];
+    uint4 v[FAN_TILE];
 #pragma unroll
-      for (uint32_t b = 32; b; b >>= 1)
-        if (s_pre[wave][k + b] <= q) k += b;
-      const uint32_t o = q - s_pre[wave][k];
-      const uint64_t d = base + s_off[wave][k] + o;
-      if (dfid) dfid[d] = s_fid[wave][k];   // null: the compact form (the entry offsets give the filter)
-      const uint32_t inl = s_cnt[wave][k] <= FAN_INLINE_ALL ? FAN_INLINE_ALL : 2u;   // subscribers in the record
-      uint32_t sub;
-      if (o >= inl) sub = st.subs[s_src[wave][k] + o];   // only these lanes read the table
-      else sub = o == 0 ? s_in0[wave][k] : (o == 1 ? s_in1[wave][k] : s_in2[wave][k]);
-      dsub[d] = sub;
+    for (uint32_t k = 0; k < FAN_TILE; ++k) f[k] = mids[min(i0 + 64 * k, nids - 1)];
+#pragma unroll
+    for (uint32_t k = 0; k < FAN_TILE; ++k) v[k] = st.rp[f[k] < st.n_fid_slots ? f[k] : 0u];   // unconditional
+    uint32_t lsum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < FAN_TILE; ++k) {
+      if (f[k] >= st.n_fid_slots) v[k] = make_uint4(0, 0, 0, 0);
+      c[k] = i0 + 64 * k < nids ? fan_count_of(st, f[k], v[k]) : 0u;
+      lsum += c[k];
     }
-    // big entries (C4: 2 000-subscriber filters): the wave streams the row, 4 per lane in flight
-    for (uint64_t mb = __ballot(big); mb; mb &= mb - 1) {
-      const uint32_t k = (uint32_t)__builtin_ctzll(mb);
-      const uint32_t cnt = s_cnt[wave][k], fk = s_fid[wave][k];
-      const uint64_t src = s_src[wave][k], dst = base + s_off[wave][k];
-      for (uint32_t j0 = lane; j0 < cnt; j0 += 256) {
-        uint32_t vv[4];
+    uint64_t tot = lsum;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) vv[r] = st.subs[src + min(j0 + 64u * r, cnt - 1)];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (j0 + 64u * r < cnt) {
-            if (dfid) dfid[dst + j0 + 64u * r] = fk;
-            dsub[dst + j0 + 64u * r] = vv[r];
+    for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
+    if (lane == 0) st_store(state + b, (b == 0 ? FAN_ST_PRE : FAN_ST_AGG) | tot);
+    uint64_t base = 0;
+    if (b > 0) {
+      int64_t j = (int64_t)b - 1;   // lanes look at tiles j, j-1, ..., j-63
+      uint32_t spins = 0;
+      for (;;) {
+        const int64_t k = j - (int64_t)lane;
+        const uint64_t sv = k >= 0 ? st_load(state + k) : FAN_ST_PRE;   // (tile 0 is a prefix)
+        const uint64_t pre = __ballot((sv >> 62) == 2), none = __ballot((sv >> 62) == 0);
+        const uint32_t last = pre ? (uint32_t)__builtin_ctzll(pre) : 63u;   // lanes 0..last are needed
+        const uint64_t need = last == 63 ? ~0ull : ((2ull << last) - 1);
+        if (none & need) {
+          if (++spins > (1u << 22)) {   // never expected: report it, and still publish so later tiles go on
+            if (lane == 0) atomicOr(overflow, FAN_GUARD);
+            break;
           }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        uint64_t x = lane <= last ? (sv & FAN_ST_VAL) : 0ull;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+        base += x;
+        if (pre) break;
+        j -= 64;
+      }
+      if (lane == 0) st_store(state + b, FAN_ST_PRE | (base + tot));
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < FAN_TILE; ++k) {
+      const uint64_t i = i0 + 64 * k;
+      if (i - lane < nids) {   // wave-uniform: a window of the batch
+        uint32_t wt;
+        const uint32_t off = wave_excl_scan(c[k], lane, &wt);
+        if (i < nids) dpos[i] = base + off;
+        if (i == nids - 1) {
+          dpos[nids] = base + off + c[k];
+          if (base + off + c[k] > cap) atomicOr(overflow, FAN_OVERFLOW);
+        }
+        fan_window(S[wave], st, lane, f[k], v[k], c[k], off, base, dfid, dsub, cap);
+        base += wt;
       }
     }
-    wave_sync();
   }
 }
 
@@ -2012,6 +2161,14 @@ static bool fan_count_walk_order() {
   return e && strcmp(e, "walk") == 0;
 }
 
+#ifndef EGM_FAN_FUSED
+#define EGM_FAN_FUSED 1   // 1: k_fan_fused (one pass); 0: count -> scan -> fill (A/B)
+#endif
+// whether launch_fanout reads the 16-B-per-entry record copies (ds0)
+bool fan_uses_ds0(bool walk_order_known) {
+  return (walk_order_known && fan_count_walk_order()) || (!EGM_FAN_FUSED && EGM_FAN_DS0);
+}
+
 hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_t* mids, uint32_t n,
                          uint64_t nids, uint64_t* drow, uint32_t* dfid, uint32_t* dsub, uint64_t cap,
                          uint32_t* wsum, uint4* ds0, uint64_t* dpos, uint64_t* wbase, uint64_t* tile_sums,
@@ -2020,23 +2177,31 @@ hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_
   if (e != hipSuccess) return e;
   if (ev) hipEventRecord(ev[0], s);
   const uint64_t nwin = (nids + 63) / 64;
-  if (nids && walk_order && fan_count_walk_order()) {
-    if ((e = hipMemsetAsync(wsum, 0, (nwin + 1) * 4, s)) != hipSuccess) return e;
-    const uint32_t g = std::min<uint32_t>((n + 64 * FAN_ORD_WAVES - 1) / (64 * FAN_ORD_WAVES), 16384);
-    hipLaunchKernelGGL(k_fan_count_ord, dim3(g), dim3(64 * FAN_ORD_WAVES), 0, s, walk_order, n, mrow, mids, nids, st,
-                       wsum, ds0);
-  } else if (nids) {
-    const uint32_t g = (uint32_t)std::min<uint64_t>((nwin + 3) / 4 + 1, 8192);
-    hipLaunchKernelGGL(k_fan_count, dim3(g), dim3(256), 0, s, mids, nids, st, wsum, ds0);
-  }
-  scan_counts(wsum, (uint32_t)nwin, tile_sums, wbase, s);   // window totals -> window bases, wbase[nwin] = all
-  if (nids) {
+  const bool ord = nids && walk_order && fan_count_walk_order();
+  if (nids == 0) {
+    if ((e = hipMemsetAsync(dpos, 0, 8, s)) != hipSuccess) return e;
+  } else if (EGM_FAN_FUSED && !ord) {
+    // tile states (wbase) and the ticket (wsum[0]) start at zero
+    if ((e = hipMemsetAsync(wbase, 0, nwin * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(wsum, 0, 4, s)) != hipSuccess) return e;
+    const uint64_t ntiles = (nwin + FAN_TILE - 1) / FAN_TILE;
+    const uint32_t gf = (uint32_t)std::min<uint64_t>((ntiles + FAN_WAVES - 1) / FAN_WAVES, 2048);   // persistent
+    hipLaunchKernelGGL(k_fan_fused, dim3(gf), dim3(64 * FAN_WAVES), 0, s, mids, nids, st, wbase, wsum, dpos, dfid,
+                       dsub, cap, overflow);
+  } else {
+    if (ord) {
+      if ((e = hipMemsetAsync(wsum, 0, (nwin + 1) * 4, s)) != hipSuccess) return e;
+      const uint32_t g = std::min<uint32_t>((n + 64 * FAN_ORD_WAVES - 1) / (64 * FAN_ORD_WAVES), 16384);
+      hipLaunchKernelGGL(k_fan_count_ord, dim3(g), dim3(64 * FAN_ORD_WAVES), 0, s, walk_order, n, mrow, mids, nids,
+                         st, wsum, ds0);
+    } else {
+      const uint32_t g = (uint32_t)std::min<uint64_t>((nwin + 3) / 4 + 1, 8192);
+      hipLaunchKernelGGL(k_fan_count, dim3(g), dim3(256), 0, s, mids, nids, st, wsum, ds0);
+    }
+    scan_counts(wsum, (uint32_t)nwin, tile_sums, wbase, s);   // window totals -> window bases, wbase[nwin] = all
     const uint32_t gf = (uint32_t)std::min<uint64_t>((nwin + FAN_WAVES - 1) / FAN_WAVES, 16384);
     hipLaunchKernelGGL(k_fan_fill, dim3(gf), dim3(64 * FAN_WAVES), 0, s, mids, nids, st, wbase, ds0, dpos, dfid, dsub,
                        cap, overflow);
-  } else {
-    e = hipMemsetAsync(dpos, 0, 8, s);
-    if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_fan_rows, dim3(std::min<uint32_t>(n / 256 + 1, 8192)), dim3(256), 0, s, mrow, n, dpos, drow);
   if (ev) hipEventRecord(ev[1], s);

@@ -422,28 +422,37 @@ def gpu_route(gm, ps: PrefixSlots, d_vpart_rank, stream: int, send):
     return route
 
 
-def gpu_match_slot(gm, ps: PrefixSlots, mode: int, stream: int, rows: list, ids: list):
+def gpu_match_slot(gm, ps: PrefixSlots, mode: int, stream: int, rows: list, ids: list, topic: Optional[list] = None):
     """match_slot() of PrefixExchange on the GPU: slot g of the received buffer
     matched in place (no copy) with its count read on the device; rows[g]
     (int64[cap_topics + 1]) and ids[g] (int32) are the caller's output buffers.
-    Returns (row, ids, source topic indices) views of slot g."""
+    Returns (row, ids, source topic indices) views of slot g: row k holds the
+    matches of source topic tids[k].  With `topic` (int32[cap_topics] buffers)
+    the rows come in the walk's order (egm_match_device_counted_ordered) and
+    the returned indices are gathered through the row -> slot topic map."""
     import torch
 
     def match_slot(recv, g):
         base = recv.data_ptr() + g * ps.slot_bytes
-        gm.match_device_counted(base + ps.off_bytes, ps.cap_bytes, base + ps.off_offsets, ps.cap_topics, base, mode,
-                                stream, rows[g].data_ptr(), ids[g].data_ptr(), ids[g].numel())
         tids = recv[g * ps.slot_bytes + ps.off_tids:g * ps.slot_bytes + ps.off_offsets].view(torch.int32)
-        return rows[g], ids[g], tids
+        if topic is None:
+            gm.match_device_counted(base + ps.off_bytes, ps.cap_bytes, base + ps.off_offsets, ps.cap_topics, base,
+                                    mode, stream, rows[g].data_ptr(), ids[g].data_ptr(), ids[g].numel())
+            return rows[g], ids[g], tids
+        gm.match_device_counted_ordered(base + ps.off_bytes, ps.cap_bytes, base + ps.off_offsets, ps.cap_topics, base,
+                                        mode, stream, rows[g].data_ptr(), topic[g].data_ptr(), ids[g].data_ptr(),
+                                        ids[g].numel())
+        return rows[g], ids[g], tids[topic[g].long()]
 
     return match_slot
 
 
-def gpu_prefix_stages(gm, d_vpart_rank, mode: int, stream: int, ids_per_topic: int = 64):
+def gpu_prefix_stages(gm, d_vpart_rank, mode: int, stream: int, ids_per_topic: int = 64, ordered: bool = False):
     """make(ps) for PrefixExchange on the GPU: a send buffer, per-slot row and
     id buffers sized for ps (ids_per_topic per slot topic + 4096), and the
     route / match stages over them.  The buffers stay reachable as attributes
-    of the returned route function (`route.send`, `match.rows`, `match.ids`)."""
+    of the returned route function (`route.send`, `match.rows`, `match.ids`).
+    ordered: the slots' rows in the walk's order (gpu_match_slot)."""
     import torch
 
     def make(ps: PrefixSlots):
@@ -452,8 +461,10 @@ def gpu_prefix_stages(gm, d_vpart_rank, mode: int, stream: int, ids_per_topic: i
         rows = [torch.zeros(ps.cap_topics + 1, dtype=torch.int64, device=dev) for _ in range(ps.n_ranks)]
         ids = [torch.zeros(ids_per_topic * ps.cap_topics + 4096, dtype=torch.int32, device=dev)
                for _ in range(ps.n_ranks)]
+        topic = ([torch.zeros(ps.cap_topics, dtype=torch.int32, device=dev) for _ in range(ps.n_ranks)]
+                 if ordered else None)
         route = gpu_route(gm, ps, d_vpart_rank, stream, send)
-        match = gpu_match_slot(gm, ps, mode, stream, rows, ids)
+        match = gpu_match_slot(gm, ps, mode, stream, rows, ids, topic)
         route.send, match.rows, match.ids = send, rows, ids
         return route, match
 

@@ -232,6 +232,13 @@ class GpuMatcher:
                                                       stream or None, d_row, d_ids, ids_cap),
                     "egm_match_device_counted")
 
+    def match_device_counted_ordered(self, d_blob: int, blob_bytes: int, d_off: int, n_max: int, d_n: int,
+                                     mode: int, stream: int, d_row: int, d_topic: int, d_ids: int, ids_cap: int):
+        """match_device_counted with rows in the walk's order: row k is slot topic d_topic[k]."""
+        self._check(self.lib.egm_match_device_counted_ordered(self.ctx, d_blob, blob_bytes, d_off, n_max, d_n, mode,
+                                                              stream or None, d_row, d_topic, d_ids, ids_cap),
+                    "egm_match_device_counted_ordered")
+
     def prefix_route(self, d_blob: int, d_off: int, n: int, d_vpart_rank: int, n_vparts: int, n_ranks: int,
                      cap_topics: int, cap_bytes: int, stream: int, d_send: int):
         """egm_prefix_route: a device topic batch -> n_ranks slots (egm_prefix_slot_bytes each) at d_send."""

@@ -209,6 +209,14 @@ int egm_match_device_ordered(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_
 int egm_match_device_counted(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes, const uint32_t* d_offsets,
                              uint32_t n_max, const uint32_t* d_n, int mode, void* hip_stream, uint64_t* d_row_ptr,
                              uint32_t* d_ids, uint64_t ids_cap);
+/* egm_match_device_counted with the rows in the walk's order (as
+   egm_match_device_ordered): row k holds the matches of slot topic d_topic[k];
+   the first count rows are the counted topics (padding sorts last), the rest
+   are empty. */
+int egm_match_device_counted_ordered(egm_ctx* ctx, const uint8_t* d_blob, uint64_t blob_bytes,
+                                     const uint32_t* d_offsets, uint32_t n_max, const uint32_t* d_n, int mode,
+                                     void* hip_stream, uint64_t* d_row_ptr, uint32_t* d_topic, uint32_t* d_ids,
+                                     uint64_t ids_cap);
 /* Synchronises the last device batch and reports its counters.  overflow != 0
    means ids_cap was too small (rerun with a larger buffer) — capacity only.
    Returns EGM_E_DEVICE (counters still filled) when a walk guard tripped:

@@ -560,11 +560,16 @@ def test_fanout_device_exact_and_guarded(gm, monkeypatch, walk_sorted):
     # the host-buffer API gives the same rows
     hrow, hfid, hsub = gm.fanout(host)
     assert int(hrow[-1]) == tot
-    # delivery buffer too small: nothing written past it, the total still reported
+    # delivery buffer too small: nothing written past it, the total and every row still reported
+    d_sub[1000:] = -7
+    d_fid[1000:] = -7
+    d_drow.zero_()
     gm.fanout_device(d_row.data_ptr(), d_ids.data_ptr(), cap, n, s, d_drow.data_ptr(), d_fid.data_ptr(),
                      d_sub.data_ptr(), 1000)
     torch.cuda.synchronize()
     assert int(d_drow[n].item()) == tot
+    assert np.array_equal(d_drow.cpu().numpy().view(np.uint64), want_row)
+    assert bool((d_sub[1000:] == -7).all()) and bool((d_fid[1000:] == -7).all())
     # an overflowed match batch (row total > id buffer) is refused before any kernel reads ids
     gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES, s,
                     d_row.data_ptr(), d_ids.data_ptr(), 16)

@@ -355,8 +355,9 @@ def _skew_topics(f, t):
     return synth.StringSet(blob, off)
 
 
-@pytest.mark.parametrize("case,world", [("skew", 2), ("skew", 4), ("bytes", 2), ("plain", 2)])
-def test_prefix_exchange_run_logical_ranks(gm, case, world):
+@pytest.mark.parametrize("case,world,ordered", [("skew", 2, False), ("skew", 4, False), ("bytes", 2, False),
+                                                ("plain", 2, False), ("skew", 2, True)])
+def test_prefix_exchange_run_logical_ranks(gm, case, world, ordered):
     """dist.PrefixExchange.run on `world` logical ranks (threads, a context
     and a table partition each, _ThreadComm for the collectives):
     * skew — every topic shares one a/b prefix, so one slot per sender
@@ -365,7 +366,8 @@ def test_prefix_exchange_run_logical_ranks(gm, case, world):
     * bytes — the first layout has room for every topic but too few bytes,
       so the first step's slots overflow by bytes (matched as empty, no
       fault) and the rerun completes;
-    * plain — no overflow, no rerun.
+    * plain — no overflow, no rerun;
+    * ordered — the slots' rows in the walk's order (the bench's form).
     Every topic is matched on exactly one rank and the rows equal the whole
     table's (ROUTES mode)."""
     import threading
@@ -397,7 +399,7 @@ def test_prefix_exchange_run_logical_ranks(gm, case, world):
                 p = parts[r]
                 b = torch.from_numpy(p.blob.copy()).to(dev)
                 o = torch.from_numpy(p.off.view(np.int32).copy()).to(dev)
-                ex = PrefixExchange(r, world, dev, ps0, gpu_prefix_stages(g, dvr, L.EGM_MODE_ROUTES, 0, 128),
+                ex = PrefixExchange(r, world, dev, ps0, gpu_prefix_stages(g, dvr, L.EGM_MODE_ROUTES, 0, 128, ordered),
                                     comm=hub.rank(r))
                 out = ex.run(b, o, p.n, len(p.blob))
                 torch.cuda.synchronize()

@@ -81,6 +81,9 @@ for step in "$@"; do
     sq)
       run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU -d "$R/gpurun_out/${TAG}_pmc_sq" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off
       run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off ;;
+    sq_c3)   # SQ + TCC counter passes over the C3 bench (the deep pass)
+      run pmc_c3_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU -d "$R/gpurun_out/${TAG}_pmc_c3_sq" -o run --output-format csv -- $B --config c3 --steps 2 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
+      run pmc_c3_tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_c3_tcc" -o run --output-format csv -- $B --config c3 --steps 2 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
     sq_*)   # SQ + TCC counter passes over the C2 bench on variant V
       v=${step#sq_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "pmc_sq_$v" 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU -d "$R/gpurun_out/${TAG}_pmc_sq_$v" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
@@ -137,6 +140,9 @@ for step in "$@"; do
       v=${step#c3ab_}
       lib=$R/emqx_amd/libemqx_gpu_match_$v.so; [ "$v" = default ] && lib=$R/emqx_amd/libemqx_gpu_match.so
       EGM_LIB=$lib run "$step" 900 $B --config c3 --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
+    pmcw_*)   # WRITE_SIZE pass over the C2 bench on variant V
+      v=${step#pmcw_}
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc_write_$v" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
     chunkhist) run chunkhist 600 env PYTHONPATH=$R python $R/tools/chunk_hist.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
