@@ -1917,7 +1917,6 @@ static int run_fanout(egm_ctx* c, const uint64_t* d_mrow, const uint32_t* d_mids
         (e = hipMemcpyAsync(&ovf, c->f_ovf.p, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipStreamSynchronize(s)) != hipSuccess)
       return c->hip_fail(e, "fanout readback");
-    if (ovf & 2u) return c->fail(EGM_E_DEVICE, "fan-out look-back guard tripped");
     if (ovf) return EGM_E_OVERFLOW;
   }
   return EGM_OK;

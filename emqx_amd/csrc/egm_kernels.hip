@@ -1793,7 +1793,7 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
 // entry's 16-B dsrc): the fill's random row reads were a 64-B line per
 // entry for ~14 B of subscribers.
 #ifndef EGM_FAN_DS0
-#define EGM_FAN_DS0 1   // 1: the count pass copies each entry's record to ds0 for the fill; 0: the fill re-reads it (A/B)
+#define EGM_FAN_DS0 0   // 1: the count pass copies each entry's record to ds0 for the fill (A/B); 0: the fill re-reads it
 #endif
 constexpr uint32_t FAN_CNT_BITS = 24;
 constexpr uint32_t FAN_CNT_SAT = (1u << FAN_CNT_BITS) - 1;   // saturated: the fill reads the exact count from row[]
@@ -2015,11 +2015,17 @@ __device__ __forceinline__ uint32_t fan_count_of(const SubTable& st, uint32_t f,
   return c == FAN_CNT_SAT ? (uint32_t)min(st.row[f + 1] - st.row[f], (uint64_t)0xFFFFFFFFu) : c;   // rare: 2^24+
 }
 
-// Two-pass form (EGM_FAN_FUSED=0, A/B): one wave per window of 64 match
-// entries; the entry offsets (dpos, the compact form's output and the rows'
-// source) come from the window's scanned total plus a wave scan of the
-// entries' counts.  An overflowed batch (total > cap) still gets its offsets,
-// so the caller learns the size.
+// One wave per window of 64 match entries; the entry offsets (dpos, the
+// compact form's output and the rows' source) come from the window's scanned
+// total plus a wave scan of the entries' counts.  The fill reads each entry's
+// subscriber record again (mostly an L2 hit: the count pass just read it) —
+// round 4 had the count copy it to a 16-B-per-entry buffer (EGM_FAN_DS0=1,
+// A/B: C4 fan-out 14.17 vs 13.18 ms on one box, r5i).  A single-pass form
+// (count, decoupled look-back scan, fill; tiles of 8 windows per ticket)
+// measured 13.9 ms, 98 ms with one ticket per window: the ticket atomic, one
+// address hit by every wave, serialises (r5h/r5i).  An
+// overflowed batch (total > cap) still gets its offsets, so the caller learns
+// the size.
 __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __restrict__ mids, uint64_t nids,
                                                              SubTable st, const uint64_t* __restrict__ wbase,
                                                              const uint4* __restrict__ ds0,
@@ -2051,108 +2057,6 @@ __global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fill(const uint32_t* __r
   }
 }
 
-// Single-pass form (round 5, the default): count, scan and fill in one
-// kernel, so each entry's subscriber record is read once (the two-pass form
-// reads it in the count and again in the fill, or copies it through a
-// 16-B-per-entry buffer).  Windows are taken in ticket order; a wave publishes
-// its window's total, then finds the sum of all earlier windows by the
-// decoupled look-back (Merrill & Garland 2016, "Single-pass Parallel Prefix
-// Scan with Decoupled Look-back"): lane k reads window w-1-k's published
-// state — an aggregate, or an inclusive prefix that ends the look-back — and
-// the wave sums up to the first prefix, then publishes its own prefix.  Every
-// window it waits on took its ticket earlier and is already running, so the
-// wait always ends; a guard bounds it anyway (reported as FAN_GUARD).
-// States: bits 62-63 = 0 not yet / 1 aggregate / 2 inclusive prefix, bits
-// 0-61 the sum.  The deliveries below `cap` are written; dpos always.
-constexpr uint64_t FAN_ST_AGG = 1ull << 62, FAN_ST_PRE = 2ull << 62, FAN_ST_VAL = (1ull << 62) - 1;
-constexpr unsigned int FAN_OVERFLOW = 1u, FAN_GUARD = 2u;
-__device__ __forceinline__ uint64_t st_load(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_store(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-#ifndef EGM_FAN_TILE
-#define EGM_FAN_TILE 8   // windows of 64 entries per ticket (one look-back per tile)
-#endif
-constexpr uint32_t FAN_TILE = EGM_FAN_TILE;
-__global__ __launch_bounds__(64 * FAN_WAVES) void k_fan_fused(const uint32_t* __restrict__ mids, uint64_t nids,
-                                                              SubTable st, uint64_t* __restrict__ state,
-                                                              unsigned int* __restrict__ ticket,
-                                                              uint64_t* __restrict__ dpos,
-                                                              uint32_t* __restrict__ dfid, uint32_t* __restrict__ dsub,
-                                                              uint64_t cap, unsigned int* overflow) {
-  __shared__ FanLds S[FAN_WAVES];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t ntiles = (nids + 64 * FAN_TILE - 1) / (64 * FAN_TILE);
-  for (;;) {
-    uint32_t tk = 0;
-    if (lane == 0) tk = atomicAdd(ticket, 1u);
-    const uint64_t b = uni((uint32_t)__shfl((int)tk, 0, 64));
-    if (b >= ntiles) break;
-    const uint64_t i0 = b * 64 * FAN_TILE + lane;
-    uint32_t f[FAN_TILE], c[FAN_TILE];
-    uint4 v[FAN_TILE];
-#pragma unroll
-    for (uint32_t k = 0; k < FAN_TILE; ++k) f[k] = mids[min(i0 + 64 * k, nids - 1)];
-#pragma unroll
-    for (uint32_t k = 0; k < FAN_TILE; ++k) v[k] = st.rp[f[k] < st.n_fid_slots ? f[k] : 0u];   // unconditional
-    uint32_t lsum = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < FAN_TILE; ++k) {
-      if (f[k] >= st.n_fid_slots) v[k] = make_uint4(0, 0, 0, 0);
-      c[k] = i0 + 64 * k < nids ? fan_count_of(st, f[k], v[k]) : 0u;
-      lsum += c[k];
-    }
-    uint64_t tot = lsum;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
-    if (lane == 0) st_store(state + b, (b == 0 ? FAN_ST_PRE : FAN_ST_AGG) | tot);
-    uint64_t base = 0;
-    if (b > 0) {
-      int64_t j = (int64_t)b - 1;   // lanes look at tiles j, j-1, ..., j-63
-      uint32_t spins = 0;
-      for (;;) {
-        const int64_t k = j - (int64_t)lane;
-        const uint64_t sv = k >= 0 ? st_load(state + k) : FAN_ST_PRE;   // (tile 0 is a prefix)
-        const uint64_t pre = __ballot((sv >> 62) == 2), none = __ballot((sv >> 62) == 0);
-        const uint32_t last = pre ? (uint32_t)__builtin_ctzll(pre) : 63u;   // lanes 0..last are needed
-        const uint64_t need = last == 63 ? ~0ull : ((2ull << last) - 1);
-        if (none & need) {
-          if (++spins > (1u << 22)) {   // never expected: report it, and still publish so later tiles go on
-            if (lane == 0) atomicOr(overflow, FAN_GUARD);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        uint64_t x = lane <= last ? (sv & FAN_ST_VAL) : 0ull;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-        base += x;
-        if (pre) break;
-        j -= 64;
-      }
-      if (lane == 0) st_store(state + b, FAN_ST_PRE | (base + tot));
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < FAN_TILE; ++k) {
-      const uint64_t i = i0 + 64 * k;
-      if (i - lane < nids) {   // wave-uniform: a window of the batch
-        uint32_t wt;
-        const uint32_t off = wave_excl_scan(c[k], lane, &wt);
-        if (i < nids) dpos[i] = base + off;
-        if (i == nids - 1) {
-          dpos[nids] = base + off + c[k];
-          if (base + off + c[k] > cap) atomicOr(overflow, FAN_OVERFLOW);
-        }
-        fan_window(S[wave], st, lane, f[k], v[k], c[k], off, base, dfid, dsub, cap);
-        base += wt;
-      }
-    }
-  }
-}
-
 // EGM_FAN_ORDER=walk: the count in the match's walk order when it is known
 // (A/B: no faster at C4, 5.79 vs 5.77 ms — a chunk's topics share few matched
 // filters there; profiles/r4_c4_fan_order_ab.jsonl).  Read at each launch.
@@ -2161,13 +2065,8 @@ static bool fan_count_walk_order() {
   return e && strcmp(e, "walk") == 0;
 }
 
-#ifndef EGM_FAN_FUSED
-#define EGM_FAN_FUSED 1   // 1: k_fan_fused (one pass); 0: count -> scan -> fill (A/B)
-#endif
 // whether launch_fanout reads the 16-B-per-entry record copies (ds0)
-bool fan_uses_ds0(bool walk_order_known) {
-  return (walk_order_known && fan_count_walk_order()) || (!EGM_FAN_FUSED && EGM_FAN_DS0);
-}
+bool fan_uses_ds0(bool walk_order_known) { return (walk_order_known && fan_count_walk_order()) || EGM_FAN_DS0; }
 
 hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_t* mids, uint32_t n,
                          uint64_t nids, uint64_t* drow, uint32_t* dfid, uint32_t* dsub, uint64_t cap,
@@ -2180,14 +2079,6 @@ hipError_t launch_fanout(const SubTable& st, const uint64_t* mrow, const uint32_
   const bool ord = nids && walk_order && fan_count_walk_order();
   if (nids == 0) {
     if ((e = hipMemsetAsync(dpos, 0, 8, s)) != hipSuccess) return e;
-  } else if (EGM_FAN_FUSED && !ord) {
-    // tile states (wbase) and the ticket (wsum[0]) start at zero
-    if ((e = hipMemsetAsync(wbase, 0, nwin * 8, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(wsum, 0, 4, s)) != hipSuccess) return e;
-    const uint64_t ntiles = (nwin + FAN_TILE - 1) / FAN_TILE;
-    const uint32_t gf = (uint32_t)std::min<uint64_t>((ntiles + FAN_WAVES - 1) / FAN_WAVES, 2048);   // persistent
-    hipLaunchKernelGGL(k_fan_fused, dim3(gf), dim3(64 * FAN_WAVES), 0, s, mids, nids, st, wbase, wsum, dpos, dfid,
-                       dsub, cap, overflow);
   } else {
     if (ord) {
       if ((e = hipMemsetAsync(wsum, 0, (nwin + 1) * 4, s)) != hipSuccess) return e;
