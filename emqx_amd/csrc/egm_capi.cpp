@@ -617,13 +617,15 @@ static int commit_locked(egm_ctx* c, uint64_t* epoch) {
 // Walk order: the sort key's bits per level as hex nibbles,
 // level 0 in the lowest; 0 walks in input order.  EGM_WALK_KEY is a tuning
 // knob for A/B runs (read at every batch); the default is the measured best:
-// 6/8/10/8 bits over four levels (round 4 with the v3 flush, one process:
-// 11.94-11.97 ms per C2 step against 12.03-12.06 for round 3's 6/8/10;
-// profiles/r4_walk_key_ab.jsonl).
+// 4/6/7/7 bits over four levels — 24 bits, three sort passes (round 5, one
+// process: 11.63 ms per C2 step against 11.75-11.78 for round 4's 6/8/10/8,
+// whose fourth sort pass bought no walk time with the flush records; the
+// walk 8.57 vs 8.58-8.61 ms; profiles/r5_walk_key_ab.jsonl).
+constexpr uint32_t WALK_KEY_DEFAULT = 0x7764u;
 static uint32_t walk_key_shape() {
   const char* v = getenv("EGM_WALK_KEY");
-  const uint32_t shape = (v && *v) ? (uint32_t)strtoul(v, nullptr, 16) & 0xFFFFu : 0x8a86u;   // KEY_LEVELS nibbles
-  return walk_key_bits(shape) <= 32 ? shape : 0x8a86u;
+  const uint32_t shape = (v && *v) ? (uint32_t)strtoul(v, nullptr, 16) & 0xFFFFu : WALK_KEY_DEFAULT;   // KEY_LEVELS nibbles
+  return walk_key_bits(shape) <= 32 ? shape : WALK_KEY_DEFAULT;
 }
 
 // EGM_WALK_SORT_MIN_BYTES: tables smaller than this are walked in input order.
