@@ -451,7 +451,7 @@ int HostTable::bulk_build(const uint8_t* blob, const uint32_t* off, uint32_t n, 
               EdgeSlot& s = edges[bb * EDGE_BUCKET + k];
               if (s.parent != NONE) continue;
               const NodeRec& r = nodes[c];
-              s = EdgeSlot{parent_[c], via_[c], c, r.flags, r.plus_child, r.hash_fid, r.term_fid, 0};
+              s = EdgeSlot{parent_[c], via_[c], c, r.flags, r.plus_child, r.hash_fid, r.term_fid, plus_flags(c)};
               edge_slot_[c] = (uint32_t)(bb * EDGE_BUCKET + k);
               placed = true;
               break;
@@ -468,7 +468,7 @@ int HostTable::bulk_build(const uint8_t* blob, const uint32_t* off, uint32_t n, 
             EdgeSlot& s = edges[(size_t)b * EDGE_BUCKET + k];
             if (s.parent != NONE) continue;
             const NodeRec& r = nodes[c];
-            s = EdgeSlot{parent_[c], via_[c], c, r.flags, r.plus_child, r.hash_fid, r.term_fid, 0};
+            s = EdgeSlot{parent_[c], via_[c], c, r.flags, r.plus_child, r.hash_fid, r.term_fid, plus_flags(c)};
             edge_slot_[c] = (uint32_t)((size_t)b * EDGE_BUCKET + k);
             placed = true;
             break;

@@ -8,7 +8,7 @@
 //
 //   nodes[]  16 B  {plus_child, hash_fid, term_fid, flags}
 //   edges[]  128 B buckets of four 32 B slots {parent, word_id, child, flags,
-//            child's plus_child, hash_fid, term_fid, -}
+//            child's plus_child, hash_fid, term_fid, flags of the child's '+' child}
 //   dict[]   32 B slots {hash64, word_id, len, inline bytes[16]}  (+ blob for long words)
 //
 // A literal transition is one bucket read keyed by (node, word_id); word ids
@@ -75,7 +75,8 @@ struct EdgeSlot {         // 32 B
   uint32_t child_plus;    // copy of nodes[child].plus_child
   uint32_t child_hash;    // copy of nodes[child].hash_fid
   uint32_t child_term;    // copy of nodes[child].term_fid
-  uint32_t pad;
+  uint32_t child_pflags;  // flags of nodes[child].plus_child (0: none) — the walker skips reading
+                          // a '+' child's record that would emit and push nothing (round 5)
 };
 
 struct DictSlot {         // 32 B

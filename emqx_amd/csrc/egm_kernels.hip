@@ -488,6 +488,9 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #ifndef EGM_WALK_PAIRS
 #define EGM_WALK_PAIRS 0     // A/B: the first pass pops two items per lane per iteration
 #endif
+#ifndef EGM_PLUS_SKIP
+#define EGM_PLUS_SKIP 1      // skip a literal child's '+' transition that would do nothing (A/B: 0)
+#endif
 #ifndef EGM_WALK_WORDS
 #define EGM_WALK_WORDS 448   // staged topic word ids per wave (a chunk's topics, [topic][level])
 #endif
@@ -514,8 +517,8 @@ struct alignas(16) WaveLds {
   uint4 stack[STK];
   uint32_t stage_fid[WALK_STAGE];
   uint8_t stage_t[WALK_STAGE];       // topic in chunk of the emit
-  uint32_t words[WALK_WORDS + 1];    // the sub-chunk's word ids, [topic][level] (+1: a leaf's
-                                     // unclamped next-word read, never used)
+  uint32_t words[WALK_WORDS + 2];    // the sub-chunk's word ids, [topic][level] (+2: the unclamped
+                                     // reads of the words at level + 1 and + 2, unused past a leaf)
   uint32_t tinfo[WALK_CHUNK];        // D | tflags << 24 | words at the fixed stride << 31
   uint32_t cnt[WALK_CHUNK];          // ids per topic, whole chunk
   uint32_t fcnt[WALK_CHUNK];         // ids per topic in the current stage / its first slot in the record
@@ -667,6 +670,7 @@ __device__ __forceinline__ uint32_t word_sig(uint32_t p) {
 struct Pend {
   uint4 it;                 // the item
   uint32_t D, nw, nsig;     // its topic's depth, the word at level + 1 and its signature bit
+  uint32_t nsig2;           // the signature bit of the word at level + 2 (the literal child's '+' child)
   bool act, lit, plus, d1;  // d1: a one-word '$' topic (do_match/1's lookup_topic probe)
   uint4 prec, l0, h0, l1, h1;
 };
@@ -693,20 +697,26 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* words
   // the next level's word (used only if level + 1 < D).  From the LDS stage
   // it is read unclamped, so the read does not wait for the topic's depth
   // (a leaf reads the next topic's word 0, or the pad word past the stage).
+  uint32_t w2;
   if (words) {
     const uint32_t raw = words[(meta & LEVEL_MAX) + 1];
+    const uint32_t raw2 = words[(meta & LEVEL_MAX) + 2];
 #if EGM_WORD_SIG
     if (tab.sig_packed) {
       p.nw = word_plain(raw);
       p.nsig = word_sig(raw);
+      p.nsig2 = word_sig(raw2);
       return;
     }
 #endif
     p.nw = raw;
+    w2 = raw2;
   } else {
     p.nw = wid[p.act ? gbase + min((meta & LEVEL_MAX) + 1, p.D - 1) : 0u];
+    w2 = wid[p.act ? gbase + min((meta & LEVEL_MAX) + 2, p.D - 1) : 0u];
   }
   p.nsig = p.nw < WID_MAX ? sig_bit(p.nw) : 0u;
+  p.nsig2 = w2 < WID_MAX ? sig_bit(w2) : 0u;
 }
 
 // Children and emits of one popped item.
@@ -743,7 +753,7 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend
   const uint32_t s1 = m1 ? 0xFFFFFFFFu : 0u;
   uint32_t cz = (p.l0.z & ~s1) | (p.l1.z & s1), cw = (p.l0.w & ~s1) | (p.l1.w & s1);
   uint32_t hx = (p.h0.x & ~s1) | (p.h1.x & s1), hy = (p.h0.y & ~s1) | (p.h1.y & s1);
-  uint32_t hz = (p.h0.z & ~s1) | (p.h1.z & s1);
+  uint32_t hz = (p.h0.z & ~s1) | (p.h1.z & s1), hw = (p.h0.w & ~s1) | (p.h1.w & s1);
   bool found = p.lit && (m0 || m1);
   if (p.lit && !m0 && !z0 && !m1 && !z1) {   // the slots read hold other keys: keep probing
     uint4 lo, hi;
@@ -753,13 +763,28 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend
     hx = hi.x;
     hy = hi.y;
     hz = hi.z;
+    hw = hi.w;
   }
   cw = found ? cw : 0u;
   o.e0 = (cw & F_HASH) != 0;
   o.f0 = hy;
   o.e1 = leaf && (cw & F_TERM) && (mode == MODE_ROUTES || wc || p.d1);
   o.f1 = hz;
-  const uint32_t go0 = (cw & F_PLUS) | ((cw & nsig) ? (cw & F_LIT) : 0u);
+  // the literal child's '+' child (flags from the slot) lands at level + 2
+  // when the child is popped: if it would emit nothing and push nothing
+  // there, the child does not take that transition — no record read, and no
+  // pop at all for a child left with none — and it is counted as created
+  // here (SURVEY §8d V_t counts it)
+  const uint32_t pfl = found ? hw : 0u;
+  const bool leaf2 = level + 2 == D;
+#if EGM_PLUS_SKIP
+  const bool puse = (pfl & F_HASH) || (leaf2 ? (pfl & F_TERM) != 0
+                                            : ((pfl & F_PLUS) || ((pfl & p.nsig2) && (pfl & F_LIT))));
+#else
+  const bool puse = true;
+#endif
+  const bool pskip = !leaf && (cw & F_PLUS) && !puse;
+  const uint32_t go0 = (puse ? (cw & F_PLUS) : 0u) | ((cw & nsig) ? (cw & F_LIT) : 0u);
   o.p0 = !leaf && go0;
   o.c0 = make_uint4(cz, base_meta | (go0 << MF_SHIFT) | (wc << MW_SHIFT), hx, nw);
   // '+' child
@@ -771,7 +796,7 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend
   const uint32_t go1 = (pf & F_PLUS) | ((pf & nsig) ? (pf & F_LIT) : 0u);
   o.p1 = !leaf && go1;
   o.c1 = make_uint4(p.it.z, base_meta | (go1 << MF_SHIFT) | (1u << MW_SHIFT), p.prec.x, nw);
-  o.created = (found ? 1u : 0u) + (p.plus ? 1u : 0u);
+  o.created = (found ? 1u : 0u) + (p.plus ? 1u : 0u) + (pskip ? 1u : 0u);
 }
 
 // lookup_routes(Topic) of a wildcard topic in ROUTES mode (emqx_router.erl:

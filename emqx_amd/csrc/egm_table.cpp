@@ -203,13 +203,24 @@ void HostTable::update_flags(uint32_t n) {
   NodeRec& r = nodes[n];
   r.flags = own_flags(n);
   mark_node(n);
-  if (parent_[n] == NONE || via_[n] >= WID_MAX) return;
+  // a '+' child's flags are also carried by the slot that reaches its parent
+  const uint32_t par = parent_[n];
+  if (par != NONE && via_[n] == WID_PLUS && parent_[par] != NONE && via_[par] < WID_MAX) {
+    mark_edge(edge_slot_[par]);
+    edges[edge_slot_[par]].child_pflags = r.flags;
+  }
+  if (par == NONE || via_[n] >= WID_MAX) return;
   mark_edge(edge_slot_[n]);
   EdgeSlot& s = edges[edge_slot_[n]];
   s.child_flags = r.flags;
   s.child_plus = r.plus_child;
   s.child_hash = r.hash_fid;
   s.child_term = r.term_fid;
+  s.child_pflags = plus_flags(n);
+}
+
+uint32_t HostTable::plus_flags(uint32_t n) const {
+  return nodes[n].plus_child != NONE ? nodes[nodes[n].plus_child].flags : 0u;
 }
 
 // ---- dictionary ----
@@ -287,7 +298,7 @@ uint32_t HostTable::edge_insert(uint32_t parent, uint32_t wid, uint32_t child, u
       if (s.parent == NONE || s.parent == TOMB) {
         if (s.parent == TOMB) --n_edge_tombs_;
         const NodeRec& r = nodes[child];
-        s = EdgeSlot{parent, wid, child, cflags, r.plus_child, r.hash_fid, r.term_fid, 0};
+        s = EdgeSlot{parent, wid, child, cflags, r.plus_child, r.hash_fid, r.term_fid, plus_flags(child)};
         ++n_edges_;
         mark_edge((uint32_t)(b * EDGE_BUCKET + k));
         return (uint32_t)(b * EDGE_BUCKET + k);

@@ -130,6 +130,7 @@ class HostTable {
   void free_node(uint32_t n);
   void update_flags(uint32_t n);
   uint32_t own_flags(uint32_t n) const;
+  uint32_t plus_flags(uint32_t n) const;   // flags of n's '+' child (0: none)
   uint32_t dict_add(const uint8_t* p, uint32_t len);
   void dict_rehash(size_t cap);
   uint32_t edge_find(uint32_t parent, uint32_t wid) const;

@@ -103,3 +103,46 @@ def test_bulk_rejects_bad_ids():
         im.bulk_build(blob, off, np.asarray([7, 7], np.uint32))      # duplicate id
     with pytest.raises(Exception):
         im.bulk_build(blob, off, np.asarray([1, 0xFFFFFFFF], np.uint32))   # NONE: assign-id path only
+
+
+def _check_plus_flags(a):
+    """Every live edge slot carries the flags of its child's '+' child (0: none)."""
+    nodes, e = a["nodes"], a["edges"]
+    live = e[(e[:, 0] != 0xFFFFFFFF) & (e[:, 0] != 0xFFFFFFFE)]
+    pc = nodes[live[:, 2].astype(np.int64), 0]
+    want = np.where(pc != 0xFFFFFFFF, nodes[np.where(pc != 0xFFFFFFFF, pc, 0).astype(np.int64), 3], 0)
+    assert len(live) > 0 and np.array_equal(live[:, 7], want.astype(live.dtype))
+    return int(np.count_nonzero(want))
+
+
+def test_edge_slots_carry_plus_child_flags():
+    """The slot field the walk uses to skip a '+' transition that would do
+    nothing (egm_common.h EdgeSlot::child_pflags) stays equal to the '+'
+    child's flags through inserts and removes without a relayout, after a
+    relayout and after a bulk build."""
+    rng = random.Random(11)
+    words = [b"a", b"b", b"c", b"+", b"d"]
+
+    def filt():
+        ws = [rng.choice(words) for _ in range(rng.randint(1, 6))]
+        if rng.random() < 0.3:
+            ws.append(b"#")
+        return b"/".join(ws)
+
+    fl = list(dict.fromkeys(filt() for _ in range(600)))
+    im = TableImage()
+    for i, f in enumerate(fl):
+        im.insert(f, i)
+    assert _check_plus_flags(im.arrays()) > 0
+    for f in fl[::2]:
+        im.remove(f)
+    more = [x for x in dict.fromkeys(filt() for _ in range(300)) if x not in set(fl[1::2])]
+    for j, f in enumerate(more):
+        im.insert(f, 10_000 + j)
+    _check_plus_flags(im.arrays())
+    im.relayout()
+    _check_plus_flags(im.arrays())
+    bi = TableImage()
+    blob, off = pack_strings(fl)
+    bi.bulk_build(blob, off, None, 4)
+    _check_plus_flags(bi.arrays())
