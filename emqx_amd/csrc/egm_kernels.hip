@@ -839,11 +839,11 @@ __device__ __forceinline__ const uint32_t* topic_words(const MatchWork& w, uint3
 // 64 roots at a time while the stack is short, and the wave pops up to 64
 // items per iteration.
 //
-// Two passes: the first (DEEP = false, a 320-item stack, 16 waves per CU)
+// Two passes: the first (DEEP = false, a 320-item stack, 17 waves per CU)
 // walks the chunks of up to DEEP_MIN levels and hands deeper ones to the
-// second (DEEP = true: a 640-item stack, 10 waves per CU), whose wider stack
+// second (DEEP = true: a 448-item stack, 14 waves per CU), whose wider stack
 // keeps the wave's pops full on deep, wide frontiers (C3: lane occupancy 0.39
-// -> 0.84) where the first pass's room bound would narrow it; a chunk deeper
+// -> 0.80) where the first pass's room bound would narrow it; a chunk deeper
 // than the deep pass takes goes to k_heavy.
 #ifdef EGM_WALK_WPE   // A/B: ask the compiler for this many waves per SIMD (caps VGPRs)
 #define EGM_WALK_ATTR __attribute__((amdgpu_waves_per_eu(EGM_WALK_WPE)))
