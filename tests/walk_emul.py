@@ -45,6 +45,8 @@ class Emul:
                     c = int(s[2])
                     rec = (int(s[4]), int(s[5]), int(s[6]), int(s[3]))
                     assert rec == self.rec(c), "edge slot's copy of the child record is stale"
+                    pc = rec[0]   # the slot also carries the flags of the child's '+' child (the walk's skip)
+                    assert int(s[7]) == (self.rec(pc)[3] if pc != NONE else 0), "edge slot's '+' child flags are stale"
                     return c, rec
                 if int(s[0]) == NONE:
                     return NONE, None
