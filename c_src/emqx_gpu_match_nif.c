@@ -372,7 +372,9 @@ static int get_pairs(ErlNifEnv* env, ERL_NIF_TERM list, egm_sub_pair** out, unsi
    changes since the last call ({FilterId, Sub} pairs; a $share group as
    GroupId bor 16#80000000) in one epoch of the fan-out's table —
    emqx_broker:subscribe/3, unsubscribe/1 and subscriber_down/1
-   (emqx_broker.erl:144-197, 331-345). */
+   (emqx_broker.erl:144-197, 331-345).  Adds and Dels are NET effects: a pair
+   in both lists is refused ({error, einval}, nothing applied); an
+   unsubscribe-then-resubscribe since the last call is the add alone. */
 static ERL_NIF_TERM nif_subs_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   egm_res_t* r;
   egm_sub_pair *add = NULL, *del = NULL;

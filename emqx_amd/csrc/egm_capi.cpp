@@ -945,10 +945,27 @@ void egm_close(egm_ctx* c) {
 
 const char* egm_last_error(egm_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+// A host allocation failure inside an entry point is reported, never thrown
+// across the C ABI (a std::bad_alloc escaping an extern "C" function would
+// terminate the embedding BEAM node).
+extern "C++" {
+template <class F>
+inline int no_throw(egm_ctx* c, const char* what, F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return c->fail(EGM_E_NOMEM, what);
+  } catch (const std::exception& ex) {
+    return c->fail(EGM_E_DEVICE, ex.what());
+  }
+}
+}  // extern "C++"
+
 int egm_table_build(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, const uint32_t* ids) {
   if (!c || (n && (!blob || !valid_offsets(off, n)))) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
+  return no_throw(c, "table build: host allocation", [&] {
   std::string why;
   if (!validate_inserts(c->table, blob, off, n, ids, true, &why)) return c->fail(EGM_E_INVAL, why);
   if (use_bulk_build(n, ids)) {   // parallel: the same image as the insert loop below (egm_bulk.cpp)
@@ -965,6 +982,7 @@ int egm_table_build(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32
   }
   c->table.relayout();
   return commit_locked(c, nullptr);
+  });
 }
 
 int egm_table_apply_delta(egm_ctx* c, const egm_delta* ins, const egm_delta* del) {
@@ -972,6 +990,7 @@ int egm_table_apply_delta(egm_ctx* c, const egm_delta* ins, const egm_delta* del
   if (ins && ins->n && (!ins->blob || !valid_offsets(ins->offsets, ins->n))) return EGM_E_INVAL;
   if (del && del->n && (!del->blob || !valid_offsets(del->offsets, del->n))) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
+  return no_throw(c, "table delta: host allocation", [&] {
   std::string why;
   if (ins && !validate_inserts(c->table, ins->blob, ins->offsets, ins->n, ins->ids, false, &why))
     return c->fail(EGM_E_INVAL, why);   // nothing staged
@@ -985,13 +1004,14 @@ int egm_table_apply_delta(egm_ctx* c, const egm_delta* ins, const egm_delta* del
     for (uint32_t i = 0; i < del->n; ++i)
       c->table.remove(del->blob + del->offsets[i], del->offsets[i + 1] - del->offsets[i]);
   return EGM_OK;
+  });
 }
 
 int egm_table_commit(egm_ctx* c, uint64_t* epoch) {
   if (!c) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
-  return commit_locked(c, epoch);
+  return no_throw(c, "table commit: host allocation", [&] { return commit_locked(c, epoch); });
 }
 
 int egm_table_epoch(egm_ctx* c, uint64_t* epoch) {
@@ -1682,6 +1702,7 @@ int egm_subs_build(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint
   const uint64_t ns = row[n_slots];
   if (ns && !subs) return EGM_E_INVAL;
   if (ns >= (1ull << 40)) return c->fail(EGM_E_INVAL, "subscriber table: at most 2^40 entries (40-bit row starts)");
+  return no_throw(c, "subscriber build: host allocation", [&] {
   // the host keeps the lists: the base of later incremental changes (egm_subs_apply_delta)
   SubsState& S = c->subs;
   // record slots beyond the given filter ids (empty rows): new filters subscribed
@@ -1694,6 +1715,7 @@ int egm_subs_build(egm_ctx* c, const uint64_t* row, uint32_t n_slots, const uint
   else
     S.subs.clear();
   return subs_upload(c, S.row.data(), cap_slots, S.subs.data());
+  });
 }
 
 // The current subscriber list of filter f (host).
@@ -1706,14 +1728,33 @@ static std::vector<uint32_t>* subs_list(SubsState& S, uint32_t f, bool create) {
   return &L;
 }
 
-int egm_subs_apply_delta(egm_ctx* c, const egm_sub_pair* add, uint64_t n_add, const egm_sub_pair* del,
-                         uint64_t n_del) {
-  if (!c || (n_add && !add) || (n_del && !del)) return EGM_E_INVAL;
-  std::lock_guard<std::recursive_mutex> g(c->mu);
+// New filter ids a delta may introduce past the table's current slots.  Filter
+// ids are dense (the table builder assigns them in insertion order), so one
+// delta never legitimately reaches millions of ids past the table; a larger id
+// is a stale or garbage id from the caller, refused before it can size a
+// rebuild (one id near WID_MAX asked for a ~34 GB row vector).
+static constexpr uint64_t SUBS_FID_GROWTH = 1ull << 22;
+
+static int subs_apply_delta(egm_ctx* c, const egm_sub_pair* add, uint64_t n_add, const egm_sub_pair* del,
+                            uint64_t n_del) {
   SubsState& S = c->subs;
   if (!S.built) return c->fail(EGM_E_STATE, "subscriber table: egm_subs_build first");
+  const uint64_t fid_limit = std::max<uint64_t>(c->n_fid_slots, S.row.size() - 1) + SUBS_FID_GROWTH;
   for (uint64_t i = 0; i < n_add; ++i)
-    if (add[i].fid >= WID_MAX) return c->fail(EGM_E_INVAL, "subscriber delta: filter id out of range");
+    if (add[i].fid >= WID_MAX || add[i].fid >= fid_limit)
+      return c->fail(EGM_E_INVAL, "subscriber delta: filter id out of range");
+  // The two lists are NET effects since the caller's last delta, so a pair
+  // may not be in both: adds are applied before removes, and "unsubscribe X,
+  // subscribe X" passed as Adds=[X], Dels=[X] would silently drop X.  Refused
+  // before anything is applied.
+  if (n_add && n_del) {
+    std::unordered_set<uint64_t> adds;
+    adds.reserve(n_add * 2);
+    for (uint64_t i = 0; i < n_add; ++i) adds.insert((uint64_t)add[i].fid << 32 | add[i].sub);
+    for (uint64_t i = 0; i < n_del; ++i)
+      if (adds.count((uint64_t)del[i].fid << 32 | del[i].sub))
+        return c->fail(EGM_E_INVAL, "subscriber delta: a (filter, subscriber) pair is both added and removed");
+  }
   // subscribe: a subscriber is in a filter's bag at most once (an ets bag keeps
   // one copy of an identical object, emqx_broker.erl:144-157)
   for (uint64_t i = 0; i < n_add; ++i) {
@@ -1735,10 +1776,23 @@ int egm_subs_apply_delta(egm_ctx* c, const egm_sub_pair* add, uint64_t n_add, co
   return EGM_OK;
 }
 
+int egm_subs_apply_delta(egm_ctx* c, const egm_sub_pair* add, uint64_t n_add, const egm_sub_pair* del,
+                         uint64_t n_del) {
+  if (!c || (n_add && !add) || (n_del && !del)) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  return no_throw(c, "subscriber delta: host allocation", [&] { return subs_apply_delta(c, add, n_add, del, n_del); });
+}
+
+static int subs_commit(egm_ctx* c, uint64_t* epoch);
+
 int egm_subs_commit(egm_ctx* c, uint64_t* epoch) {
   if (!c) return EGM_E_INVAL;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
+  return no_throw(c, "subscriber commit: host allocation", [&] { return subs_commit(c, epoch); });
+}
+
+static int subs_commit(egm_ctx* c, uint64_t* epoch) {
   SubsState& S = c->subs;
   if (!S.built) return c->fail(EGM_E_STATE, "subscriber table: egm_subs_build first");
   S.last_appended = S.last_patched = 0;
@@ -1750,21 +1804,30 @@ int egm_subs_commit(egm_ctx* c, uint64_t* epoch) {
   // or more superseded entries than live ones
   bool rebuild = false;
   uint64_t append = 0;
-  uint32_t max_f = c->n_fid_slots;
   for (uint32_t f : P) {
     const std::vector<uint32_t>& L = *subs_list(S, f, true);
-    if (f >= c->n_fid_slots) {
-      rebuild = true;
-      max_f = std::max(max_f, f + 1);
-    }
+    if (f >= c->n_fid_slots) rebuild = true;
     if (L.size() >= (1u << 24) - 1) rebuild = true;
     if (L.size() > 3) append += L.size();
   }
   const uint64_t cap_ids = c->sub_ids.cap / 4;
   if (S.tail + append + 16 > cap_ids || S.garbage + append > S.tail / 2 + 65536) rebuild = true;
   if (rebuild) {
-    // flatten: the build's lists with every changed list in place (and new empty slots)
-    const uint32_t n = (uint32_t)std::min<uint64_t>(WID_MAX, (uint64_t)max_f + max_f / 4 + 4096);
+    // flatten: the build's lists with every changed list in place (and new
+    // empty slots).  Sized from the largest LIVE filter id — a non-empty base
+    // row or changed list, or a new id — not from the padded slot count, so
+    // repeated rebuilds under churn do not grow the table.
+    uint64_t hi = 0;
+    for (uint64_t f = S.row.size() - 1; f > 0; --f)
+      if (S.row[f] > S.row[f - 1]) {
+        hi = f;
+        break;
+      }
+    for (const auto& kv : S.lists)
+      if (!kv.second.empty()) hi = std::max<uint64_t>(hi, (uint64_t)kv.first + 1);
+    for (uint32_t f : P)
+      if (f >= c->n_fid_slots) hi = std::max<uint64_t>(hi, (uint64_t)f + 1);
+    const uint32_t n = (uint32_t)std::min<uint64_t>(WID_MAX, hi + hi / 4 + 4096);
     std::vector<uint64_t> row((uint64_t)n + 1, 0);
     for (uint32_t f = 0; f < n; ++f) {
       auto it = S.lists.find(f);
@@ -1841,6 +1904,13 @@ int egm_subs_commit(egm_ctx* c, uint64_t* epoch) {
   S.last_appended = app.size();
   S.last_patched = need.size();
   if (epoch) *epoch = S.epoch;
+  return EGM_OK;
+}
+
+int egm_subs_slots(egm_ctx* c, uint32_t* n_fid_slots) {
+  if (!c || !n_fid_slots) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  *n_fid_slots = c->n_fid_slots;
   return EGM_OK;
 }
 

@@ -422,6 +422,18 @@ def gpu_route(gm, ps: PrefixSlots, d_vpart_rank, stream: int, send):
     return route
 
 
+def _require_torch_stream(stream: int):
+    """The GPU stages launch on `stream` and then read their results (the
+    topic gather below) and drop old buffers on torch's CURRENT stream: the
+    two must be one stream, or the gather could read d_topic before the
+    compaction wrote it and the caching allocator could hand a buffer the
+    kernels still write to someone else.  Checked, not assumed."""
+    import torch
+    cur = torch.cuda.current_stream().cuda_stream
+    if int(stream or 0) != int(cur or 0):
+        raise ValueError(f"prefix stages: stream {stream:#x} is not torch's current stream {cur:#x}")
+
+
 def gpu_match_slot(gm, ps: PrefixSlots, mode: int, stream: int, rows: list, ids: list, topic: Optional[list] = None):
     """match_slot() of PrefixExchange on the GPU: slot g of the received buffer
     matched in place (no copy) with its count read on the device; rows[g]
@@ -431,6 +443,7 @@ def gpu_match_slot(gm, ps: PrefixSlots, mode: int, stream: int, rows: list, ids:
     the rows come in the walk's order (egm_match_device_counted_ordered) and
     the returned indices are gathered through the row -> slot topic map."""
     import torch
+    _require_torch_stream(stream)
 
     def match_slot(recv, g):
         base = recv.data_ptr() + g * ps.slot_bytes
@@ -456,6 +469,7 @@ def gpu_prefix_stages(gm, d_vpart_rank, mode: int, stream: int, ids_per_topic: i
     import torch
 
     def make(ps: PrefixSlots):
+        _require_torch_stream(stream)
         dev = d_vpart_rank.device
         send = torch.zeros(ps.n_ranks * ps.slot_bytes, dtype=torch.uint8, device=dev)
         rows = [torch.zeros(ps.cap_topics + 1, dtype=torch.int64, device=dev) for _ in range(ps.n_ranks)]

@@ -227,7 +227,11 @@ class GpuMatcher:
 
     def match_device_counted(self, d_blob: int, blob_bytes: int, d_off: int, n_max: int, d_n: int, mode: int,
                              stream: int, d_row: int, d_ids: int, ids_cap: int):
-        """egm_match_device over a batch whose topic count (<= n_max) is at d_n on the device."""
+        """egm_match_device over a received prefix slot: d_n points to the
+        slot's 16-B device header {count, bytes, overflow, 0} (the layout
+        egm_prefix_route writes, include/emqx_gpu_match.h), not a bare u32
+        count — the kernels read its count (<= n_max) and match the slot as
+        empty when its overflow word is set."""
         self._check(self.lib.egm_match_device_counted(self.ctx, d_blob, blob_bytes, d_off, n_max, d_n, mode,
                                                       stream or None, d_row, d_ids, ids_cap),
                     "egm_match_device_counted")
@@ -306,6 +310,12 @@ class GpuMatcher:
         ep = C.c_uint64()
         self._check(self.lib.egm_subs_commit(self.ctx, C.byref(ep)), "egm_subs_commit")
         return ep.value
+
+    def subs_slots(self) -> int:
+        """egm_subs_slots: filter-id slots of the device subscriber records."""
+        n = C.c_uint32()
+        self._check(self.lib.egm_subs_slots(self.ctx, C.byref(n)), "egm_subs_slots")
+        return n.value
 
     def subs_last_commit(self) -> dict:
         a, p, e = C.c_uint64(), C.c_uint64(), C.c_uint64()

@@ -144,12 +144,23 @@ def subscribers(n_filters: int, lam=1.0, p_big=0.001, n_big=2000, p_share=0.1, g
     return row, ids
 
 
-def config(name: str, scale: float = 1.0, n_filters=None, n_topics=None):
-    """(filters, topics) for a BASELINE config, optionally scaled down."""
+def config_filters(name: str, scale: float = 1.0, n_filters=None) -> StringSet:
+    """The filter set of a BASELINE config (config()'s first half)."""
     c = CONFIGS[name]
     seed = SEED_BASE + CONFIG_INDEX[name]
     nf = n_filters if n_filters is not None else max(1, int(c["n_filters"] * scale))
+    return filters(nf, c["dmin"], c["dmax"], c["wc"], c["p_plus"], c["p_hash"], seed=seed)
+
+
+def config_topics(name: str, f: StringSet, scale: float = 1.0, n_topics=None) -> StringSet:
+    """The topic batch of a BASELINE config over its filters (config()'s second half)."""
+    c = CONFIGS[name]
+    seed = SEED_BASE + CONFIG_INDEX[name]
     nt = n_topics if n_topics is not None else max(1, int(c["n_topics"] * scale))
-    f = filters(nf, c["dmin"], c["dmax"], c["wc"], c["p_plus"], c["p_hash"], seed=seed)
-    t = topics(nt, f, c["dmin"], c["dmax"], seed=seed)
-    return f, t
+    return topics(nt, f, c["dmin"], c["dmax"], seed=seed)
+
+
+def config(name: str, scale: float = 1.0, n_filters=None, n_topics=None):
+    """(filters, topics) for a BASELINE config, optionally scaled down."""
+    f = config_filters(name, scale, n_filters)
+    return f, config_topics(name, f, scale, n_topics)

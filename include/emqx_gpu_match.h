@@ -264,7 +264,16 @@ int egm_subs_build(egm_ctx* ctx, const uint64_t* row_ptr, uint32_t n_fid_slots, 
    last readers finished), then makes it current: fan-outs already launched
    keep the epoch they started with.  A new filter id past the table, a row of
    2^24 subscribers, or appended rows past the reserve make it a full build
-   (egm_subs_last_commit reports which).  EGM_E_STATE before egm_subs_build. */
+   (egm_subs_last_commit reports which), sized from the largest filter id
+   that still has a subscriber.  EGM_E_STATE before egm_subs_build.
+   Contract of one egm_subs_apply_delta call: `add` and `del` are the NET
+   changes since the caller's previous call, so no (fid, sub) pair may appear
+   in both (adds are applied before removes; "unsubscribe X then subscribe X
+   again" is the add alone, or nothing if X was there) — a pair in both lists
+   is refused with EGM_E_INVAL and nothing is applied.  An added fid must be
+   below the table's slots + 2^22 (filter ids are dense); a larger one is
+   refused with EGM_E_INVAL.  Host allocation failures return EGM_E_NOMEM
+   (no entry point throws). */
 typedef struct egm_sub_pair {
   uint32_t fid;   /* filter id */
   uint32_t sub;   /* subscriber id, or a $share group id | 0x80000000 */
@@ -275,6 +284,10 @@ int egm_subs_commit(egm_ctx* ctx, uint64_t* epoch);
 /* What the last egm_subs_commit did: subscriber entries appended, records
    patched, whether it was a full build, entries now on the device. */
 int egm_subs_last_commit(egm_ctx* ctx, uint64_t* appended, uint64_t* patched, int* rebuilt, uint64_t* entries);
+/* Filter-id slots of the device subscriber records (ids at or past it have no
+   subscribers): the build's ids + a quarter + 4096 spare, re-sized by a full
+   build from the largest filter id that still has a subscriber. */
+int egm_subs_slots(egm_ctx* ctx, uint32_t* n_fid_slots);
 int egm_fanout_batch(egm_ctx* ctx, const egm_result* matched, egm_delivery** out);
 /* Device variant over a device CSR match result.  match_ids_len = entries
    d_match_ids holds: a match row whose total exceeds it (an overflowed match

@@ -35,6 +35,8 @@ def _load():
         lib.ot_match_count.argtypes = [P, P, P, C.c_uint32, C.c_int]
         lib.ot_match_counts.restype = C.c_uint64
         lib.ot_match_counts.argtypes = [P, P, P, C.c_uint32, C.c_int, P]
+        lib.ot_match_sums.restype = C.c_uint64
+        lib.ot_match_sums.argtypes = [P, P, P, C.c_uint32, C.c_int, P, P]
         lib.ot_visited_counts.restype = C.c_uint64
         lib.ot_visited_counts.argtypes = [P, P, P, C.c_uint32, C.c_int, P]
         lib.ot_n_keys.restype = C.c_uint64
@@ -101,6 +103,18 @@ class OracleTrie:
         counts = np.zeros(n, dtype=np.uint32)
         self.lib.ot_match_counts(self.h, _p(blob), _p(off), n, threads, _p(counts))
         return counts
+
+    def match_sums(self, blob, off, threads: int = 1):
+        """Per-topic match counts (u32[n]) and per-row checksums (u64[n]): the
+        sum of a 64-bit mix of each matched id, the mix of
+        tests/test_gpu_scale.py::row_checksums — every row compared as a SET
+        at full size; additive over disjoint filter shards."""
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        n = len(off) - 1
+        counts = np.zeros(n, dtype=np.uint32)
+        sums = np.zeros(n, dtype=np.uint64)
+        self.lib.ot_match_sums(self.h, _p(blob), _p(off), n, threads, _p(counts), _p(sums))
+        return counts, sums
 
     def visited_counts(self, blob, off, threads: int = 1):
         """SURVEY §8d V_t per topic (u64[n]) and its sum: the root plus every

@@ -436,6 +436,49 @@ uint64_t ot_match_counts(void* h, const uint8_t* blob, const uint32_t* off, uint
   return s;
 }
 
+// Per-topic match counts AND an order-independent checksum of each topic's
+// filter-id set: the sum (mod 2^64) of a 64-bit mix of every id in the row —
+// the same mix as tests/test_gpu_scale.py::row_checksums, so a whole batch's
+// rows are compared as sets at full config size without moving the ids.  The
+// sum is additive over disjoint filter shards, so a sharded
+// oracle's rows are checked by summing the shards' checksums.
+static inline uint64_t id_mix(uint32_t id) {
+  uint64_t x = id;
+  x ^= x >> 16;
+  x *= 0x9E3779B97F4A7C15ull;
+  x ^= x >> 29;
+  return x;
+}
+
+uint64_t ot_match_sums(void* h, const uint8_t* blob, const uint32_t* off, uint32_t n, int threads,
+                       uint32_t* counts, uint64_t* sums) {
+  const Oracle* o = (const Oracle*)h;
+  if (threads < 1) threads = 1;
+  std::vector<uint64_t> tot(threads, 0);
+  std::vector<std::thread> th;
+  for (int k = 0; k < threads; ++k) {
+    th.emplace_back([&, k]() {
+      uint32_t a = (uint32_t)((uint64_t)n * k / threads), b = (uint32_t)((uint64_t)n * (k + 1) / threads);
+      uint64_t s = 0;
+      std::vector<uint32_t> tmp;
+      for (uint32_t i = a; i < b; ++i) {
+        tmp.clear();
+        match_one(o, (const char*)blob + off[i], off[i + 1] - off[i], tmp);
+        uint64_t c = 0;
+        for (uint32_t id : tmp) c += id_mix(id);
+        counts[i] = (uint32_t)tmp.size();
+        sums[i] = c;
+        s += tmp.size();
+      }
+      tot[k] = s;
+    });
+  }
+  for (auto& t : th) t.join();
+  uint64_t s = 0;
+  for (auto v : tot) s += v;
+  return s;
+}
+
 // Per-topic V_t (counts may be null) and their sum over n topics.
 uint64_t ot_visited_counts(void* h, const uint8_t* blob, const uint32_t* off, uint32_t n, int threads,
                            uint64_t* counts) {

@@ -295,3 +295,68 @@ def test_broker_subscriber_churn_vs_oracle():
         rounds_checked += 1
     assert rounds_checked == 8
     assert any(not s["rebuilt"] and s["patched"] > 0 for s in stats), stats   # deltas, not rebuilds
+
+
+def test_subs_delta_contract_and_bounded_rebuilds():
+    """(1) full builds forced by superseded entries are sized from
+    the largest live filter id, so repeated rebuilds under churn do not grow
+    the slot table; (2) an added filter id far past the table is refused
+    (EGM_E_INVAL) before it can size a rebuild; (3) a (filter, subscriber)
+    pair in both lists of one delta is refused and nothing is applied.  The
+    deliveries stay exact throughout (emqx_broker:dispatch/2,
+    apps/emqx/src/emqx_broker.erl:283-308)."""
+    import numpy as np
+    from emqx_amd import _lib as L
+    from emqx_amd.engine import GpuMatcher, pack_strings
+    nf = 1000
+    gm = GpuMatcher(0)
+    try:
+        fb, fo = pack_strings([b"a/%d" % i for i in range(nf)])
+        gm.build(fb, fo)
+        lists = {f: [f * 10 + k for k in range(1 + f % 3)] for f in range(nf)}
+        row = np.zeros(nf + 1, np.uint64)
+        row[1:] = np.cumsum([len(lists[f]) for f in range(nf)])
+        gm.subs_build(row, np.concatenate([np.array(lists[f], np.uint32) for f in range(nf)]))
+        slots0 = gm.subs_slots()
+        assert slots0 >= nf
+        tb, to = pack_strings([b"a/5", b"a/7", b"a/999", b"b/1"])
+
+        def check():
+            res = gm.match(tb, to, L.EGM_MODE_ROUTES)
+            drow, dfid, dsub = gm.fanout(res)
+            for i, f in enumerate((5, 7, 999, None)):
+                got = sorted(dsub[int(drow[i]):int(drow[i + 1])].tolist())
+                assert got == (sorted(lists[f]) if f is not None else []), (i, f)
+
+        # a big row re-committed again and again: superseded entries force full builds
+        big = [(5, 100000 + k) for k in range(70000)]
+        gm.subs_apply_delta(add=big)
+        lists[5] += [s for _, s in big]
+        gm.subs_commit()
+        rebuilt = 0
+        for k in range(24):
+            gm.subs_apply_delta(add=[(5, 900000 + k)])
+            lists[5].append(900000 + k)
+            gm.subs_commit()
+            rebuilt += gm.subs_last_commit()["rebuilt"]
+            assert gm.subs_slots() <= slots0, (k, gm.subs_slots(), slots0)
+        assert rebuilt >= 5, rebuilt
+        check()
+        # a garbage filter id: refused, the table unchanged
+        with pytest.raises(L.EgmError) as ei:
+            gm.subs_apply_delta(add=[(7, 1), (0xFFFFFF00, 2)])
+        assert ei.value.code == L.EGM_E_INVAL
+        # the same pair added and removed in one delta: refused, nothing applied
+        with pytest.raises(L.EgmError) as ei:
+            gm.subs_apply_delta(add=[(7, 4242), (999, 1)], delete=[(7, 4242)])
+        assert ei.value.code == L.EGM_E_INVAL
+        gm.subs_commit()
+        check()
+        # a legitimate new filter id just past the slots: a full build that grows the table
+        gm.subs_apply_delta(add=[(slots0 + 10, 77)], delete=[(7, lists[7][0])])
+        lists[7].pop(0)
+        gm.subs_commit()
+        assert gm.subs_last_commit()["rebuilt"] and gm.subs_slots() > slots0 + 10
+        check()
+    finally:
+        gm.close()

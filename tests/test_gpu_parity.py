@@ -580,9 +580,10 @@ def test_fanout_device_exact_and_guarded(gm, monkeypatch, walk_sorted):
 
 @pytest.mark.slow
 def test_full_size_c1_properties(gm):
-    """C1 at full size: 1M filters x 10M topics.  Every one of the 10M row
-    totals against the C++ oracle's count (they were promised
-    but not compared), 200K sampled rows id-exact, determinism across runs."""
+    """C1 at full size: 1M filters x 10M topics.  Every one of the 10M rows
+    against the C++ oracle as a SET — its count and an order-independent
+    checksum of its ids (rows were compared by count) —
+    200K sampled rows id-exact, determinism across runs."""
     f, t = synth.config("c1")
     gm.build(f.blob, f.off)
     a = gm.match(t.blob, t.off, L.EGM_MODE_ROUTES)
@@ -590,13 +591,14 @@ def test_full_size_c1_properties(gm):
     assert np.array_equal(a.row_ptr, b2.row_ptr)
     # every row the same set in both runs: a per-row order-independent checksum
     # (the whole-batch canonical sort of 180M ids took ~20 s of the suite's budget)
-    from tests.test_gpu_scale import row_checksums
-    assert np.array_equal(row_checksums(a.row_ptr, a.ids), row_checksums(b2.row_ptr, b2.ids))
+    from tests.rowsum import row_checksums
+    gsum = row_checksums(a.row_ptr, a.ids)
+    assert np.array_equal(gsum, row_checksums(b2.row_ptr, b2.ids))
     o = OracleTrie(True, 1)
     o.add(f.blob, f.off)
-    want = o.match_counts(t.blob, t.off, threads=16)
+    want, wsum = o.match_sums(t.blob, t.off, threads=16)
     got = np.diff(a.row_ptr).astype(np.uint32)
-    bad = np.nonzero(got != want)[0]
+    bad = np.nonzero((got != want) | (gsum != wsum))[0]
     assert len(bad) == 0, (len(bad), [(int(i), int(got[i]), int(want[i])) for i in bad[:5]])
     rng = np.random.default_rng(5)
     idx = np.sort(rng.choice(t.n, 200_000, replace=False))

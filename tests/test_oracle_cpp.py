@@ -64,3 +64,33 @@ def test_cpp_oracle_random(seed, compact, mode):
     assert o.match_count(tb, to, threads=2) == len(ids)
     c = canonical(row, ids)
     assert len(c) == len(ids)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_cpp_oracle_row_sums(mode):
+    """ot_match_sums: per-row counts and order-independent checksums equal the
+    ones computed from ot_match's id rows (tests/rowsum.py's mix) — the
+    full-size GPU tests compare every row through these."""
+    from tests.rowsum import row_checksums
+    rng = random.Random(11 + mode)
+    filters = list(dict.fromkeys([rand_filter(rng) for _ in range(300)] + [b"$x", b"a/b", b"#"]))
+    o = OracleTrie(True, mode)
+    blob, off = pack_strings(filters)
+    o.add(blob, off)
+    topics = [rand_topic(rng) for _ in range(2000)] + [b"$x", b"a/b"]
+    tb, to = pack_strings(topics)
+    row, ids = o.match(tb, to, threads=2)
+    cnt, sums = o.match_sums(tb, to, threads=3)
+    assert np.array_equal(cnt, np.diff(row).astype(np.uint32))
+    assert np.array_equal(sums, row_checksums(row, ids))
+    assert np.count_nonzero(cnt) > 100
+    # additive over disjoint filter shards
+    half = len(filters) // 2
+    parts = []
+    for lo, hi in ((0, half), (half, len(filters))):
+        p = OracleTrie(True, mode)
+        pb, po = pack_strings(filters[lo:hi])
+        p.add(pb, po, np.arange(lo, hi, dtype=np.uint32))
+        parts.append(p.match_sums(tb, to))
+    assert np.array_equal(parts[0][0] + parts[1][0], cnt)
+    assert np.array_equal(parts[0][1] + parts[1][1], sums)
