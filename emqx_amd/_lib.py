@@ -116,6 +116,7 @@ SIGNATURES = {
     "egm_subs_commit": (C.c_int, [_P, _P]),
     "egm_subs_last_commit": (C.c_int, [_P, _P, _P, _P, _P]),
     "egm_subs_slots": (C.c_int, [_P, _P]),
+    "egm_debug_walk_sort": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint32, _P]),
     "egm_fanout_batch": (C.c_int, [_P, C.POINTER(egm_result), C.POINTER(C.POINTER(egm_delivery))]),
     "egm_fanout_device": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P, _P, C.c_uint64]),
     "egm_fanout_device_compact": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P, _P, C.c_uint64]),

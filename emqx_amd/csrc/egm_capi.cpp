@@ -2066,6 +2066,33 @@ int egm_fanout_batch(egm_ctx* c, const egm_result* m, egm_delivery** out) {
 }
 
 // ------------------------------------------------------------ shard merge --
+int egm_debug_walk_sort(egm_ctx* c, const uint32_t* d_keys, const uint64_t* d_vals, uint32_t n, uint32_t kbits,
+                        uint64_t* d_out) {
+  if (!c || !d_keys || !d_vals || !d_out || !n || n >= (1u << 29) || !kbits || kbits > 32) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (set_device(c)) return EGM_E_DEVICE;
+  DevBuf k1, k2, v1, tmp, st;
+  // a shape whose levels sum to kbits (the scratch size depends only on the bits)
+  const uint32_t shape = kbits <= 15 ? kbits : (kbits <= 30 ? (15u | ((kbits - 15) << 4)) : (15u | (15u << 4) | ((kbits - 30) << 8)));
+  hipError_t e;
+  if ((e = k1.ensure((size_t)n * 4)) != hipSuccess || (e = k2.ensure((size_t)n * 4)) != hipSuccess ||
+      (e = v1.ensure((size_t)n * 8)) != hipSuccess || (e = tmp.ensure(walk_sort_temp_bytes(n, shape))) != hipSuccess ||
+      (e = st.ensure(sizeof(MatchStats))) != hipSuccess)
+    return c->hip_fail(e, "debug sort: scratch");
+  if ((e = hipMemcpyAsync(k1.p, d_keys, (size_t)n * 4, hipMemcpyDeviceToDevice, c->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(v1.p, d_vals, (size_t)n * 8, hipMemcpyDeviceToDevice, c->stream)) != hipSuccess ||
+      (e = hipMemsetAsync(st.p, 0, sizeof(MatchStats), c->stream)) != hipSuccess ||
+      (e = launch_walk_sort(k1.as<uint32_t>(), k2.as<uint32_t>(), v1.as<uint64_t>(), d_out, tmp.p, st.as<MatchStats>(),
+                            n, kbits, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "debug sort: launch");
+  MatchStats hs{};
+  if ((e = hipMemcpyAsync(&hs, st.p, sizeof hs, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+    return c->hip_fail(e, "debug sort: sync");
+  if (hs.guard) return c->fail(EGM_E_DEVICE, "debug sort: look-back guard tripped");
+  return EGM_OK;
+}
+
 int egm_shard_merge(egm_ctx* c, uint32_t n_shards, uint32_t n, const uint32_t* d_counts,
                     const uint32_t* const* d_shard_ids, uint64_t total_ids, void* hip_stream, uint64_t* d_row,
                     uint32_t* d_ids, uint64_t ids_cap) {

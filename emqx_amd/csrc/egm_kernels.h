@@ -130,9 +130,11 @@ constexpr uint32_t DEBUG_INPUT_ORDER = 4u;   // walk in input order (no locality
 constexpr uint32_t DEBUG_FORCE_GUARD = 8u;   // loop guards of 2 iterations: trips the guard (error-path test)
 
 // walk-order key: total bits of a key shape; radix sort scratch bytes for a
-// batch of n topics (hipcub)
+// batch of n topics (the hand-written LSD radix sort, egm_kernels.hip walk_sort)
 uint32_t walk_key_bits(uint32_t shape);
 size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape);
+hipError_t launch_walk_sort(uint32_t* keys, uint32_t* keys_tmp, uint64_t* vals, uint64_t* out, void* tmp,
+                            MatchStats* stats, uint32_t n, uint32_t kbits, hipStream_t s);
 
 struct MatchOut {                 // CSR result (device)
   uint64_t* row_ptr;              // [n + 1]

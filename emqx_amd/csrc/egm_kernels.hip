@@ -18,7 +18,6 @@
 //
 // This is pointer chasing over hashed edges — HBM / latency bound; no MFMA.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -1721,12 +1720,226 @@ uint32_t walk_key_bits(uint32_t shape) {
   return b;
 }
 
+// ------------------------------------------------------- walk-order sort ----
+// LSD radix sort of the batch's (32-bit key, 8-B record) pairs by the key's
+// `kbits` high bits, 8 bits per pass, hand-written for gfx950 (round 6; rounds
+// 2-5 called hipCUB's onesweep).  The order only buys the walk locality — the
+// reference's results are order-free sets (apps/emqx/test/emqx_trie_SUITE.erl:
+// 82,101,118) — but the sort is stable and deterministic, so a batch always
+// walks in the same order.
+//
+//   k_sort_hist   one read of the keys: every pass's 256-bin histogram (LDS
+//                 counts, one global add per bin and block); also zeroes the
+//                 passes' look-back words.
+//   k_sort_pass   per pass, one kernel: a block takes a ticket (its tile of
+//                 SORT_TILE pairs, in dispatch order), ranks its pairs by digit
+//                 with wave ballots (8 per row of 64: the lanes holding the same
+//                 digit; stable: rows in input order, waves in input order),
+//                 publishes its per-digit totals and finds each digit's global
+//                 start by a decoupled look-back over the preceding tiles'
+//                 words {flag:2 | count:30} (agent-scope loads and stores: the
+//                 tiles run on all eight XCDs), then places the pairs sorted in
+//                 LDS and writes each digit's run contiguously.
+// Bytes per pair and pass: 12 read + 12 written (the last pass writes only the
+// records), + 4 read once for the histograms.
+constexpr int SORT_THREADS = 256;
+constexpr int SORT_ITEMS = 15;                                  // pairs per thread: 3840 per tile, 51 KB LDS -> 3 blocks/CU
+constexpr uint32_t SORT_TILE = SORT_THREADS * SORT_ITEMS;
+constexpr uint32_t SORT_MAX_PASSES = 4;
+constexpr uint32_t SORT_HIST_BLOCKS = 1024;
+constexpr uint32_t SORT_AGG = 1u << 30, SORT_PFX = 2u << 30, SORT_CNT = SORT_AGG - 1u;
+constexpr size_t SORT_HEAD = 8192;                              // tickets[4] + hist[4][256], rounded
+constexpr uint32_t SORT_SPIN_LIMIT = 1u << 20;                  // look-back polls before a guard trip
+
+static inline uint32_t sort_passes(uint32_t kbits) { return (kbits + 7) / 8; }
+static inline uint32_t sort_tiles(uint32_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
+static inline size_t sort_vals_bytes(uint32_t n) { return ((size_t)n * 8 + 255) & ~(size_t)255; }
+
 size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape) {
-  size_t b = 0;
-  const int bits = (int)min(walk_key_bits(shape), 32u);
-  hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                     (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)n, 32 - bits, 32);
-  return b;
+  const uint32_t kbits = min(walk_key_bits(shape), 32u);
+  if (!kbits) return 0;
+  return SORT_HEAD + sort_vals_bytes(n) + (size_t)sort_passes(kbits) * sort_tiles(n) * 256 * 4;
+}
+
+__global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ key, uint32_t n, uint32_t begin,
+                                                  uint32_t npass, uint32_t* __restrict__ hist,
+                                                  uint32_t* __restrict__ status, uint64_t status_words) {
+  __shared__ uint32_t h[SORT_MAX_PASSES * 256];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < npass * 256; i += 256) h[i] = 0;
+  const uint64_t g0 = (uint64_t)blockIdx.x * 256 + tid, gs = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = g0; i < status_words; i += gs) status[i] = 0;
+  __syncthreads();
+  auto count = [&](uint32_t k) {
+    for (uint32_t p = 0; p < npass; ++p) atomicAdd(&h[p * 256 + ((k >> (begin + 8 * p)) & 0xFFu)], 1u);
+  };
+  const uint32_t n4 = n / 4;
+  for (uint64_t i = g0; i < n4; i += gs) {
+    const uint4 k = ((const uint4*)key)[i];
+    count(k.x);
+    count(k.y);
+    count(k.z);
+    count(k.w);
+  }
+  for (uint64_t i = (uint64_t)n4 * 4 + g0; i < n; i += gs) count(key[i]);
+  __syncthreads();
+  for (uint32_t i = tid; i < npass * 256; i += 256)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// exclusive scan of one value per thread over a 256-thread block
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t tid, uint32_t* s_wsum) {
+  uint32_t wt;
+  uint32_t x = wave_excl_scan(v, tid & 63, &wt);
+  __syncthreads();
+  if ((tid & 63) == 0) s_wsum[tid >> 6] = wt;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t w = 0; w < SORT_THREADS / 64; ++w)
+    if (w < (tid >> 6)) x += s_wsum[w];
+  return x;
+}
+
+__global__ __launch_bounds__(SORT_THREADS) void k_sort_pass(const uint32_t* __restrict__ kin,
+                                                           const uint64_t* __restrict__ vin,
+                                                           uint32_t* __restrict__ kout, uint64_t* __restrict__ vout,
+                                                           uint32_t n, uint32_t shift,
+                                                           const uint32_t* __restrict__ hist, uint32_t* status,
+                                                           uint32_t* ticket, MatchStats* stats) {
+  __shared__ uint32_t s_key[SORT_TILE];
+  __shared__ uint64_t s_val[SORT_TILE];
+  __shared__ uint32_t s_cnt[SORT_THREADS / 64][256];   // per-wave digit counts, then each wave's offset
+  __shared__ uint32_t s_start[256];                    // the digit's first slot in the sorted tile
+  __shared__ uint32_t s_base[256];                     // the digit's first output position of this tile
+  __shared__ uint32_t s_wsum[SORT_THREADS / 64];
+  __shared__ uint32_t s_tile;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+  for (uint32_t i = tid; i < (SORT_THREADS / 64) * 256; i += SORT_THREADS) (&s_cnt[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint64_t base = (uint64_t)tile * SORT_TILE;
+  // rows of 64 pairs, wave-striped: pair (wave, i, lane) is input pair base + (wave * ITEMS + i) * 64 + lane
+  const uint64_t wbase = base + (uint64_t)wv * 64 * SORT_ITEMS + lane;
+  uint32_t k[SORT_ITEMS], r[SORT_ITEMS];
+  uint64_t v[SORT_ITEMS];
+#pragma unroll
+  for (int i = 0; i < SORT_ITEMS; ++i) {
+    const uint64_t idx = wbase + (uint64_t)i * 64;
+    const bool ok = idx < n;
+    k[i] = ok ? kin[idx] : 0u;
+    v[i] = ok ? vin[idx] : 0ull;
+  }
+  // stable ranks: row by row, a row's lanes of one digit found with 8 ballots
+#pragma unroll
+  for (int i = 0; i < SORT_ITEMS; ++i) {
+    const bool ok = wbase + (uint64_t)i * 64 < n;
+    const uint32_t d = (k[i] >> shift) & 0xFFu;
+    uint64_t m = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t bb = __ballot((d >> b) & 1u);
+      m &= ((d >> b) & 1u) ? bb : ~bb;
+    }
+    const uint32_t below = mbcnt(m);
+    const uint32_t c = s_cnt[wv][d];
+    r[i] = c + below;
+    if (ok && below == 0) s_cnt[wv][d] = c + popc(m);   // the row's lowest lane of the digit adds its count
+  }
+  __syncthreads();
+  const uint32_t d = tid;   // one digit per thread from here
+  uint32_t tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < SORT_THREADS / 64; ++w) {
+    const uint32_t c = s_cnt[w][d];
+    s_cnt[w][d] = tot;
+    tot += c;
+  }
+  uint32_t* my = status + (uint64_t)tile * 256 + d;
+  uint32_t excl = 0;
+  if (tile == 0) {
+    excl = block_excl_scan256(hist[d], tid, s_wsum);   // the digit's first position in the whole output
+  } else {
+    __hip_atomic_store(my, SORT_AGG | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t j = tile - 1;
+    uint32_t spins = 0;
+    for (;;) {
+      const uint32_t x = __hip_atomic_load(status + j * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t f = x & ~SORT_CNT;
+      if (f == 0) {
+        if (++spins > SORT_SPIN_LIMIT) {   // a bug, reported (rows not assembled), never a hang
+          atomicOr(&stats->guard, GUARD_LOOP);
+          break;
+        }
+        continue;
+      }
+      excl += x & SORT_CNT;
+      if (f == SORT_PFX) break;
+      --j;
+    }
+  }
+  __hip_atomic_store(my, SORT_PFX | ((excl + tot) & SORT_CNT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t start = block_excl_scan256(tot, tid, s_wsum);
+  s_start[d] = start;
+  s_base[d] = excl;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < SORT_ITEMS; ++i) {
+    if (wbase + (uint64_t)i * 64 >= n) continue;
+    const uint32_t dg = (k[i] >> shift) & 0xFFu;
+    const uint32_t p = s_start[dg] + s_cnt[wv][dg] + r[i];
+    s_key[p] = k[i];
+    s_val[p] = v[i];
+  }
+  __syncthreads();
+  const uint32_t nt = (uint32_t)min<uint64_t>(SORT_TILE, n - base);
+  for (uint32_t j = tid; j < nt; j += SORT_THREADS) {
+    const uint32_t kk = s_key[j];
+    const uint32_t dg = (kk >> shift) & 0xFFu;
+    const uint64_t dst = (uint64_t)s_base[dg] + (j - s_start[dg]);
+    if (kout) kout[dst] = kk;
+    vout[dst] = s_val[j];
+  }
+}
+
+// Sort (skey, sval) by the key's kbits high bits into w.order (records only).
+static hipError_t walk_sort(const MatchWork& w, uint32_t n, uint32_t kbits, hipStream_t s) {
+  const uint32_t begin = 32 - kbits, npass = sort_passes(kbits), tiles = sort_tiles(n);
+  uint8_t* tmp = (uint8_t*)w.sort_tmp;
+  uint32_t* tickets = (uint32_t*)tmp;
+  uint32_t* hist = tickets + SORT_MAX_PASSES;
+  uint64_t* vtmp = (uint64_t*)(tmp + SORT_HEAD);
+  uint32_t* status = (uint32_t*)(tmp + SORT_HEAD + sort_vals_bytes(n));
+  hipError_t e = hipMemsetAsync(tmp, 0, (SORT_MAX_PASSES + SORT_MAX_PASSES * 256) * 4, s);
+  if (e != hipSuccess) return e;
+  const uint64_t status_words = (uint64_t)npass * tiles * 256;
+  const uint32_t hb = (uint32_t)std::min<uint64_t>(SORT_HIST_BLOCKS, std::max<uint64_t>(1, ((uint64_t)n / 4 + 255) / 256));
+  hipLaunchKernelGGL(k_sort_hist, dim3(hb), dim3(256), 0, s, w.skey, n, begin, npass, hist, status, status_words);
+  for (uint32_t p = 0; p < npass; ++p) {
+    const bool last = p + 1 == npass;
+    const uint32_t* kin = (p & 1) ? w.skey_out : w.skey;
+    uint32_t* kout = last ? nullptr : ((p & 1) ? w.skey : w.skey_out);
+    const uint64_t* vin = (p == 0 || !(p & 1)) ? w.sval : vtmp;
+    uint64_t* vout = last ? w.order : ((p & 1) ? w.sval : vtmp);
+    hipLaunchKernelGGL(k_sort_pass, dim3(tiles), dim3(SORT_THREADS), 0, s, kin, vin, kout, vout, n, begin + 8 * p,
+                       hist + 256 * p, status + (uint64_t)p * tiles * 256, tickets + p, w.stats);
+  }
+  return hipGetLastError();
+}
+
+// Test hook (egm_debug_walk_sort): the walk sort alone over caller-given pairs.
+// keys/vals are overwritten (scratch); tmp holds walk_sort_temp_bytes.
+hipError_t launch_walk_sort(uint32_t* keys, uint32_t* keys_tmp, uint64_t* vals, uint64_t* out, void* tmp,
+                            MatchStats* stats, uint32_t n, uint32_t kbits, hipStream_t s) {
+  if (!n || !kbits || kbits > 32) return hipErrorInvalidValue;
+  MatchWork w{};
+  w.skey = keys;
+  w.skey_out = keys_tmp;
+  w.sval = vals;
+  w.order = out;
+  w.sort_tmp = tmp;
+  w.stats = stats;
+  return walk_sort(w, n, kbits, s);
 }
 
 constexpr uint32_t SORT_MIN_TOPICS = 16384;   // below this the sort's fixed cost outweighs the locality
@@ -1757,8 +1970,7 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
                      off, n, w.wid, w.lv, w.tfl, wo);
   trace(s, "k_tokenise");
   if (sorted) {
-    e = hipcub::DeviceRadixSort::SortPairs(w.sort_tmp, tb, w.skey, w.skey_out, w.sval, w.order, (int)n,
-                                           32 - (int)kbits, 32, s);
+    e = walk_sort(w, n, kbits, s);
     if (e != hipSuccess) return e;
     if (walk_sorted) *walk_sorted = true;
     trace(s, "walk order sort");

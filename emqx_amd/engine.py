@@ -311,6 +311,10 @@ class GpuMatcher:
         self._check(self.lib.egm_subs_commit(self.ctx, C.byref(ep)), "egm_subs_commit")
         return ep.value
 
+    def debug_walk_sort(self, d_keys: int, d_vals: int, n: int, kbits: int, d_out: int):
+        """egm_debug_walk_sort: the walk-order radix sort alone (test hook)."""
+        self._check(self.lib.egm_debug_walk_sort(self.ctx, d_keys, d_vals, n, kbits, d_out), "egm_debug_walk_sort")
+
     def subs_slots(self) -> int:
         """egm_subs_slots: filter-id slots of the device subscriber records."""
         n = C.c_uint32()

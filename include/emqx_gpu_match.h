@@ -246,6 +246,12 @@ int egm_set_timing(egm_ctx* ctx, int enable);
 #define EGM_DEBUG_INPUT_ORDER 4u   /* walk the batch in input order (no locality sort; A/B and tests) */
 #define EGM_DEBUG_FORCE_GUARD 8u   /* loop guards of 2 iterations: trips the walk guard (error-path test) */
 int egm_set_debug(egm_ctx* ctx, uint32_t flags);
+/* Test hook: the walk-order radix sort alone (egm_kernels.hip walk_sort, the
+   hand-written LSD sort every sorted batch runs): d_out[i] = d_vals of the
+   i-th pair in a STABLE sort by the key's kbits (1..32) high bits; n < 2^29.
+   Inputs are not modified.  EGM_E_DEVICE if a look-back guard tripped. */
+int egm_debug_walk_sort(egm_ctx* ctx, const uint32_t* d_keys, const uint64_t* d_vals, uint32_t n, uint32_t kbits,
+                        uint64_t* d_out);
 int egm_get_timing(egm_ctx* ctx, double* walk_ms, uint64_t* walk_launches, double* fanout_ms,
                    uint64_t* fanout_launches);
 
