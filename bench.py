@@ -178,6 +178,56 @@ def host_e2e(gm, t, mode, batch: int = 1_000_000, batches: int = 24, depth: int 
             "path": "host blob -> pinned staging -> H2D -> match -> SDMA D2H into pinned CSR (egm_match_submit/wait)"}
 
 
+def host_batcher_curve(gm, t, mode, sizes=(1024, 4096, 16384, 65536), depth: int = 2, seconds: float = 0.3,
+                       default_size: int = 4096) -> dict:
+    """The drop-in's own operating point: the Erlang
+    batcher (erl/emqx_gpu_batch.erl: batch_size 4096, depth 2, linger 1 ms;
+    emqx_batch.erl:50-81's size + linger policy) commits a batch of topics to
+    submit/3 and answers its callers when wait/2 returns, with at most `depth`
+    tickets in flight.  Saturated (every batch full, the next one committed as
+    soon as a ticket slot frees), per batch size: topics/s and the latency of
+    each batch from its submit to its wait-return (p50 / p99) — what a
+    publisher's match_routes/1 call waits on top of the linger
+    (emqx_broker.erl:200-209, the PUBACK after it, emqx_channel.erl:601-609).
+    Host blob in, host CSR out, through egm_match_submit / egm_match_wait."""
+    out = []
+    pool = min(t.n, 1 << 20)
+    for b in sizes:
+        b = min(b, pool)
+        k = max(2, min(16, pool // b))
+        parts = [t.subset(np.arange(i * b, (i + 1) * b)) for i in range(k)]
+        tk = [gm.submit(parts[i % k].blob, parts[i % k].off, mode) for i in range(depth + 1)]   # slots sized, untimed
+        for x in tk:
+            gm.wait(x, copy=False)
+        lat = []
+        inflight = []
+        done = i = 0
+        t0 = time.perf_counter()
+        while True:
+            running = time.perf_counter() - t0 < seconds or i < 4 * depth
+            if running:   # the next full batch, committed as soon as a ticket slot is free
+                p = parts[i % k]
+                inflight.append((time.perf_counter(), gm.submit(p.blob, p.off, mode)))
+                i += 1
+            if inflight and (len(inflight) == depth or not running):
+                ts, tick = inflight.pop(0)
+                gm.wait(tick, copy=False)
+                lat.append(time.perf_counter() - ts)
+                done += 1
+            if not running and not inflight:
+                break
+        dt = time.perf_counter() - t0
+        lat_ms = np.array(lat) * 1e3
+        out.append({"batch_topics": b, "in_flight": depth, "batches": done, "topics_per_s": b * done / dt,
+                    "latency_ms_p50": float(np.percentile(lat_ms, 50)), "latency_ms_p99": float(np.percentile(lat_ms, 99)),
+                    "latency_ms_max": float(lat_ms.max())})
+    dflt = next((r for r in out if r["batch_topics"] == default_size), None)
+    return {"defaults": {"batch_size": default_size, "depth": depth, "linger_ms": 1}, "at_defaults": dflt,
+            "sweep": out,
+            "what": "saturated batcher: full batches, `depth` tickets in flight; latency = submit -> wait-return "
+                    "of one batch (a caller also waits up to linger_ms for its batch to fill)"}
+
+
 def _heartbeat(period: float = 30.0):
     """Progress on stderr while long host steps (100M-filter generation and
     table build) run inside ctypes calls, so a watchdog sees a live process."""
@@ -812,6 +862,8 @@ def main():
     if _host_leg(args, world, shard):
         log("[rank 0] timing the host-visible path ...")
         host = host_e2e(gm, t, mode)
+        log("[rank 0] timing the batcher's operating points ...")
+        host["batcher"] = host_batcher_curve(gm, t, mode)
     if rank == 0:
         cpu = None
         if args.cpu_baseline == "auto" and world == 1 and f.n > 20_000_000:

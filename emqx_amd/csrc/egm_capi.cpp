@@ -99,8 +99,9 @@ struct PipeSlot {
   uint32_t n = 0;
   int mode = 0;
   uint64_t bytes = 0, maxlen = 0, cap = 0;
+  uint64_t o_off = 0;      // the offsets' place after the blob in h_in and d_in (one H2D copy)
   PinBuf h_in, h_out, h_stats;
-  DevBuf d_blob, d_off, d_row, d_ids, d_flags;
+  DevBuf d_in, d_row, d_ids, d_flags;
   // ev_in: staged input copied in; ev_match: matched (stream s); ev_done: the
   // CSR in h_out (the copier's D2H copies, or the copy-out kernel)
   hipEvent_t ev_in = nullptr, ev_match = nullptr, ev_done = nullptr;
@@ -686,8 +687,8 @@ static int ensure_work(egm_ctx* c, MatchWs& W, uint32_t n, uint64_t blob_bytes, 
   if ((e = W.rec.ensure(rcap * 4)) != hipSuccess) return c->hip_fail(e, "flush records");
   W.rec_cap = W.rec.cap / 4;
   if (W.rec_cap >= (1ull << 34)) return c->fail(EGM_E_INVAL, "batch too large: > 16G u32 of flush records (split it)");
-  if ((e = W.chunks.ensure(((uint64_t)n / WALK_CHUNK + 2) * 16)) != hipSuccess) return c->hip_fail(e, "chunk records");
-  if ((e = W.dir.ensure(((uint64_t)n / WALK_CHUNK + 2) * REC_DIR * 4)) != hipSuccess)
+  if ((e = W.chunks.ensure(walk_chunk_cap(n) * 16)) != hipSuccess) return c->hip_fail(e, "chunk records");
+  if ((e = W.dir.ensure(walk_chunk_cap(n) * REC_DIR * 4)) != hipSuccess)
     return c->hip_fail(e, "chunk directories");
   // heavy topics: their ids (count then fill, one piece per topic)
   const uint64_t tcap = ids_cap + 4096;
@@ -696,7 +697,7 @@ static int ensure_work(egm_ctx* c, MatchWs& W, uint32_t n, uint64_t blob_bytes, 
   W.ids_tmp_cap = W.ids_tmp.cap / 4;
   if ((e = W.pieces.ensure(((uint64_t)n + 4096) * 16)) != hipSuccess) return c->hip_fail(e, "pieces");
   W.pieces_cap = std::min<uint64_t>(W.pieces.cap / 16, 0xFFFFFFF0ull);
-  if ((e = W.deferred.ensure((n / WALK_CHUNK + 2) * 4 * 2)) != hipSuccess) return c->hip_fail(e, "deferred");
+  if ((e = W.deferred.ensure(walk_chunk_cap(n) * 4 * 2)) != hipSuccess) return c->hip_fail(e, "deferred");
   const uint32_t hcap = heavy_stack_items(max_levels);
   if ((e = W.heavy_stack.ensure((uint64_t)c->heavy_waves * hcap * 16)) != hipSuccess)
     return c->hip_fail(e, "heavy stack");
@@ -1217,6 +1218,13 @@ static int pipe_copy_mode() {
   return v;
 }
 static bool pipe_copy_kernel() { return pipe_copy_mode() == PIPE_KERNEL; }
+// EGM_PIPE_COPY set explicitly: every batch takes that copy (A/B), small ones too
+static bool pipe_copy_forced() {
+  static const bool v = getenv("EGM_PIPE_COPY") != nullptr;
+  return v;
+}
+// Batches up to this many topics take the small-batch result path (pipe_launch).
+constexpr uint64_t PIPE_SMALL_TOPICS = 65536;
 
 // EGM_PIPE_TRACE=1: one stderr line per pipeline event with a ms clock
 // (diagnostics of the host pipeline's bubbles).
@@ -1251,13 +1259,32 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   const OutLayout ol = out_layout(n, S.cap);
   if ((e = S.h_out.ensure(ol.total)) != hipSuccess) return c->hip_fail(e, "pipe pinned result");
   if ((e = hipStreamWaitEvent(s, S.ev_in, 0)) != hipSuccess) return c->hip_fail(e, "pipe wait input");
-  r = run_match(c, W, *ep, S.d_blob.as<uint8_t>(), S.d_off.as<uint32_t>(), S.n, S.mode, s, S.d_row.as<uint64_t>(),
-                S.d_ids.as<uint32_t>(), S.cap);
+  r = run_match(c, W, *ep, S.d_in.as<uint8_t>(), (const uint32_t*)(S.d_in.as<uint8_t>() + S.o_off), S.n, S.mode, s,
+                S.d_row.as<uint64_t>(), S.d_ids.as<uint32_t>(), S.cap);
   if (r) {
     ws_done(W, s);
     return r;
   }
   c->last_pending = false;   // this batch's counters travel with the slot
+  if (n <= PIPE_SMALL_TOPICS && !pipe_copy_forced()) {
+    // A small batch (the Erlang batcher's: 4096 by default) is latency-bound,
+    // not bandwidth-bound: its result goes to pinned memory by a copy-out
+    // kernel on the match's own stream — flags read from the workspace, the
+    // counters too — so no D2D copy, no copier-thread hand-off and no SDMA
+    // round trips (round 6: ~330 us -> see DESIGN §6 "small batches").
+    uint8_t* h = (uint8_t*)S.h_out.p;
+    if ((e = launch_copy_out(S.d_row.as<uint64_t>(), (uint32_t)n, S.d_ids.as<uint32_t>(), S.cap, W.tfl.as<uint8_t>(),
+                             h + ol.o_row, h + ol.o_ids, h + ol.o_fl, s, W.stats.as<MatchStats>(),
+                             (MatchStats*)S.h_stats.p)) != hipSuccess ||
+        (e = hipEventRecord(S.ev_match, s)) != hipSuccess || (e = hipEventRecord(S.ev_done, s)) != hipSuccess) {
+      ws_done(W, s);
+      return c->hip_fail(e, "pipe copy-out (small batch)");
+    }
+    ws_done(W, s);
+    std::lock_guard<std::mutex> q(c->cq_mu);
+    S.copied_gen = ++S.launch_gen;
+    return EGM_OK;
+  }
   if ((n && (e = hipMemcpyAsync(S.d_flags.p, W.tfl.p, n, hipMemcpyDeviceToDevice, s)) != hipSuccess) ||
       (e = hipMemcpyAsync(S.h_stats.p, W.stats.p, sizeof(MatchStats), hipMemcpyDeviceToHost, s)) != hipSuccess ||
       (e = hipEventRecord(S.ev_match, s)) != hipSuccess) {
@@ -1464,11 +1491,10 @@ static int submit_locked(egm_ctx* c, std::unique_lock<std::recursive_mutex>& g, 
   S.maxlen = maxlen.load();
   S.cap = std::max<uint64_t>(std::max<uint64_t>((uint64_t)n * 4 + 1024, S.cap),
                              std::max<uint64_t>(c->out_ids.cap / 4, c->pipe_cap_hint));
-  if ((e = S.d_blob.ensure(bytes + 16)) != hipSuccess) return c->hip_fail(e, "pipe blob");
-  if ((e = S.d_off.ensure(((uint64_t)n + 1) * 4)) != hipSuccess) return c->hip_fail(e, "pipe offsets");
-  if ((bytes && (e = hipMemcpyAsync(S.d_blob.p, hin, bytes, hipMemcpyHostToDevice, c->copy_stream)) != hipSuccess) ||
-      (e = hipMemcpyAsync(S.d_off.p, hoff, ((uint64_t)n + 1) * 4, hipMemcpyHostToDevice, c->copy_stream)) !=
-          hipSuccess ||
+  // blob and offsets in one copy (the staging already holds them back to back)
+  S.o_off = o_off;
+  if ((e = S.d_in.ensure(in_sz + 16)) != hipSuccess) return c->hip_fail(e, "pipe input");
+  if ((e = hipMemcpyAsync(S.d_in.p, hin, in_sz, hipMemcpyHostToDevice, c->copy_stream)) != hipSuccess ||
       (e = hipEventRecord(S.ev_in, c->copy_stream)) != hipSuccess)
     return c->hip_fail(e, "pipe H2D");
   int r = pipe_launch(c, S);

@@ -77,6 +77,7 @@ struct MatchWork {                // per-batch device workspace
   uint8_t* tfl;                   // [n] TF_* flags
   uint32_t* cnt;                  // [n] ids of each result row (row = walk position if walk_rows, else topic)
   uint32_t walk_rows;             // rows in walk order (MatchOut::topic set): row k = the k-th topic walked
+  uint32_t ct;                    // topics per chunk (walk_chunk_topics(n): 64, fewer for small batches)
   uint32_t* rec;                  // [rec_cap] flush records (u32), per-wave segments
   uint64_t rec_cap;
   uint32_t rec_grain;             // u32 per record segment
@@ -149,6 +150,22 @@ struct MatchOut {                 // CSR result (device)
 #define EGM_WALK_CHUNK 64   // topics per chunk taken by a walk wave (and deferred to k_heavy)
 #endif
 constexpr int WALK_CHUNK = EGM_WALK_CHUNK;
+// Topics per chunk for a batch of n (a power of two <= WALK_CHUNK): a small
+// batch is split into more, smaller chunks so that it still spreads over the
+// whole GPU (a wave's chunk walk is a chain of dependent reads: at 64 topics
+// per wave a 4096-topic batch walked on 64 waves for 123 us, round 6).
+// Bounded so that n / ct <= max(n / WALK_CHUNK, WALK_MIN_CHUNKS).
+constexpr uint32_t WALK_MIN_CHUNKS = 2048, WALK_MIN_CT = 4;
+inline uint32_t walk_chunk_topics(uint32_t n) {
+  uint32_t ct = WALK_CHUNK;
+  while (ct > WALK_MIN_CT && (uint64_t)n < (uint64_t)ct * WALK_MIN_CHUNKS) ct >>= 1;
+  return ct;
+}
+// chunks of a batch of up to n topics (every batch size <= n): the sizing of chunk arrays
+inline uint64_t walk_chunk_cap(uint64_t n) {
+  const uint64_t a = n / WALK_CHUNK, b = 2 * (uint64_t)WALK_MIN_CHUNKS;
+  return (a > b ? a : b) + 2;
+}
 int walk_grid_blocks(uint32_t n_topics);
 size_t scan_tiles(uint32_t n);
 // items of HBM stack per heavy wave for topics of up to max_levels levels
@@ -162,8 +179,10 @@ uint32_t walk_stage();   // WALK_STAGE: the most emits a flush record holds
 // tail.
 inline uint64_t rec_capacity(uint64_t ids, uint32_t n, uint32_t flush_lim, uint32_t grain) {
   const uint64_t per = flush_lim > 256 ? flush_lim - 256 : 1;
-  const uint64_t chunks = (uint64_t)n / WALK_CHUNK + 2;
-  const uint64_t waves = (uint64_t)walk_grid_blocks(n) + (uint64_t)deep_grid_blocks(n);
+  const uint64_t chunks = walk_chunk_cap(n);
+  // waves of any batch of up to n topics (their chunk counts are bounded by walk_chunk_cap)
+  const uint64_t wc = walk_chunk_cap(n);
+  const uint64_t waves = (wc < 256u * 32u ? wc : 256u * 32u) + (uint64_t)deep_grid_blocks(n);
   constexpr uint64_t over = REC_IDS + EGM_REC_ALIGN - 1;
   return ids + ids * (over + per - 1) / per + chunks * (over + REC_HDR) + waves * (grain + EGM_REC_ALIGN + REC_HDR);
 }
@@ -211,7 +230,8 @@ hipError_t launch_shard_merge(const uint32_t* cnt, uint32_t G, uint32_t n, const
 // Host-visible result copy: row_ptr, the row_ptr[n] ids (<= ids_cap) and the
 // flags of a device CSR into pinned host memory (16-B aligned sections).
 hipError_t launch_copy_out(const uint64_t* row, uint32_t n, const uint32_t* ids, uint64_t ids_cap,
-                           const uint8_t* flags, uint8_t* h_row, uint8_t* h_ids, uint8_t* h_fl, hipStream_t s);
+                           const uint8_t* flags, uint8_t* h_row, uint8_t* h_ids, uint8_t* h_fl, hipStream_t s,
+                           const MatchStats* st = nullptr, MatchStats* h_st = nullptr);
 
 // Prefix partition exchange (egm_common.h prefix_vpart): a rank's
 // topic batch -> n_ranks slots of slot_bytes each, one per destination rank,

@@ -864,7 +864,8 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
   __shared__ WaveLds<STK> L;
   const uint32_t lane = threadIdx.x;
   // the first pass walks every chunk, the deep pass the chunks the first handed on
-  const uint32_t nchunks = DEEP ? uni(*(volatile unsigned int*)&w.stats->n_deep) : (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  const uint32_t ct = w.ct;   // topics per chunk (lanes >= ct hold none)
+  const uint32_t nchunks = DEEP ? uni(*(volatile unsigned int*)&w.stats->n_deep) : (n + ct - 1) / ct;
   uint4 root = ld16(tab.nodes);   // wave-uniform: keep it in SGPRs
   root.x = uni(root.x);
   root.y = uni(root.y);
@@ -877,18 +878,18 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
   // sorted batch: the record of the chunk's j-th topic in walk order, loaded
   // one chunk ahead (a grid stride: the wave's next chunk is c + gridDim.x)
   const uint64_t* ord = w.order;
-  uint64_t rec = (ord && !DEEP) ? ord[min(blockIdx.x * WALK_CHUNK + lane, n - 1)] : 0ull;
+  uint64_t rec = (ord && !DEEP) ? ord[min(blockIdx.x * ct + lane, n - 1)] : 0ull;
   uint32_t deep_c = 0, n_pend = 0;   // chunks for the deep pass not yet handed on
   for (uint32_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
     const uint32_t c = DEEP ? uni(w.deep[ci]) : ci;
-    const uint32_t t0 = c * WALK_CHUNK;
-    const uint32_t nt = min((uint32_t)WALK_CHUNK, n - t0);
+    const uint32_t t0 = c * ct;
+    const uint32_t nt = min(ct, n - t0);
     // ---- topic info (lane j: the chunk's j-th topic in walk order) ----
     uint32_t D = 0, f = 0, my_t = 0;
     bool fixed = false;
     if (ord) {
       const uint64_t r = DEEP ? ord[min(t0 + lane, n - 1)] : rec;
-      if (!DEEP) rec = ord[min((uint64_t)(c + gridDim.x) * WALK_CHUNK + lane, (uint64_t)n - 1)];   // the next chunk's, in flight now
+      if (!DEEP) rec = ord[min((uint64_t)(c + gridDim.x) * ct + lane, (uint64_t)n - 1)];   // the next chunk's, in flight now
       if (lane < nt) {
         my_t = (uint32_t)r;
         D = (uint32_t)(r >> 32) & 0xFFFFFFu;
@@ -1151,7 +1152,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
   root.y = uni(root.y);
   root.z = uni(root.z);
   root.w = uni(root.w);
-  const uint32_t total = w.stats->n_deferred * (uint32_t)WALK_CHUNK;
+  const uint32_t ct = w.ct, total = w.stats->n_deferred * ct;
   uint4* stk = w.heavy_stack + (uint64_t)blockIdx.x * w.heavy_cap;
   const uint32_t cap = w.heavy_cap;
   const uint32_t guard_lim = (w.debug & DEBUG_FORCE_GUARD) ? 2u : (1u << EGM_GUARD_BITS);
@@ -1161,7 +1162,7 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
     if (lane == 0) idx = atomicAdd(&w.stats->heavy_next, 1u);
     idx = uni(__shfl(idx, 0, 64));
     if (idx >= total) break;
-    const uint32_t pos = w.deferred[idx / WALK_CHUNK] * WALK_CHUNK + idx % WALK_CHUNK;   // in walk order
+    const uint32_t pos = w.deferred[idx / ct] * ct + idx % ct;   // in walk order
     if (pos >= n) continue;
     const uint64_t rec = w.order ? w.order[pos] : (uint64_t)pos;
     const uint32_t t = uni((uint32_t)rec);
@@ -1359,6 +1360,37 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__
   if (blockIdx.x == 0 && threadIdx.x == 0) row_ptr[n] = tile_sums[ntiles];
 }
 
+// Small arrays (n <= SCAN_SMALL): the whole scan in one launch of one block
+// — a small batch's scan is three launches' fixed cost otherwise (round 6:
+// 3 x 4.5 us of a 4096-topic batch's ~330 us).
+constexpr uint32_t SCAN_SMALL = 65536;
+__global__ __launch_bounds__(1024) void k_scan_small(const uint32_t* __restrict__ cnt, uint32_t n,
+                                                     uint64_t* __restrict__ row_ptr, uint64_t* __restrict__ copy) {
+  __shared__ uint64_t wsum[16];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t per = (n + 1023) / 1024, i0 = threadIdx.x * per;
+  uint64_t s = 0;
+  for (uint32_t k = 0; k < per; ++k)
+    if (i0 + k < n) s += cnt[i0 + k];
+  uint64_t x = s;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  uint64_t pre = x - s;
+  for (uint32_t k = 0; k < wv; ++k) pre += wsum[k];
+  for (uint32_t k = 0; k < per; ++k) {
+    if (i0 + k < n) {
+      row_ptr[i0 + k] = pre;
+      if (copy) copy[i0 + k] = pre;
+      pre += cnt[i0 + k];
+    }
+  }
+  if (threadIdx.x == 1023) row_ptr[n] = pre;   // the last thread's running sum: the total
+}
+
 // Spilled pieces -> CSR rows, no atomics.  One wave per window of 64 pieces:
 // a wave scan lays the window's ids out as one run [0, tot), and the lanes
 // copy that run with consecutive lanes on consecutive ids (a binary search
@@ -1477,12 +1509,12 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
                                                              const uint64_t* __restrict__ order, uint32_t n,
                                                              const uint64_t* __restrict__ row_ptr,
                                                              uint32_t* __restrict__ topic, uint32_t* __restrict__ ids,
-                                                             uint64_t ids_cap, MatchStats* stats) {
+                                                             uint64_t ids_cap, MatchStats* stats, uint32_t ct) {
   __shared__ uint32_t s_ex[REC_WAVES][64];
   __shared__ uint64_t s_dst[REC_WAVES][64];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool ok = compact_checks(row_ptr, n, ids_cap, stats);
-  const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  const uint32_t nchunks = (n + ct - 1) / ct;
   // every load of one record (out of the slab: header 0, which fails the tag check)
   auto issue = [&](uint64_t o, RecLoad& L) {
     const bool in = o + REC_IDS <= rec_cap;
@@ -1494,8 +1526,8 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
     for (uint32_t k = 0; k < REC_IPL; ++k) L.v[k] = rec[min(oc + REC_IDS + lane + 64u * k, rec_cap - 1)];
   };
   for (uint32_t c = blockIdx.x * REC_WAVES + wave; c < nchunks; c += gridDim.x * REC_WAVES) {
-    const uint32_t t = c * WALK_CHUNK + lane;
-    const bool act = t < n;
+    const uint32_t t = c * ct + lane;
+    const bool act = lane < ct && t < n;
     const uint32_t my_t = act ? (order ? (uint32_t)order[t] : t) : 0u;
     if (topic && act) topic[t] = my_t;   // written even when the rows are not (overflow): the map is the order
     const uint4 ch = chunks[c];
@@ -1563,15 +1595,15 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_burst(const uint32_t* __
                                                               const uint64_t* __restrict__ order, uint32_t n,
                                                               const uint64_t* __restrict__ row_ptr,
                                                               uint32_t* __restrict__ topic, uint32_t* __restrict__ ids,
-                                                              uint64_t ids_cap, MatchStats* stats) {
+                                                              uint64_t ids_cap, MatchStats* stats, uint32_t ct) {
   __shared__ uint32_t s_ex[REC_WAVES][64];
   __shared__ uint64_t s_dst[REC_WAVES][64];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool ok = compact_checks(row_ptr, n, ids_cap, stats);
-  const uint32_t nchunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  const uint32_t nchunks = (n + ct - 1) / ct;
   for (uint32_t c = blockIdx.x * REC_WAVES + wave; c < nchunks; c += gridDim.x * REC_WAVES) {
-    const uint32_t t = c * WALK_CHUNK + lane;
-    const bool act = t < n;
+    const uint32_t t = c * ct + lane;
+    const bool act = lane < ct && t < n;
     const uint32_t my_t = act ? (order ? (uint32_t)order[t] : t) : 0u;
     if (topic && act) topic[t] = my_t;   // written even when the rows are not (overflow): the map is the order
     const uint4 ch = chunks[c];
@@ -1648,7 +1680,7 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_burst(const uint32_t* __
 // ------------------------------------------------------------- launchers ----
 // One wave per block; a grid stride over the chunks beyond 32 waves per CU.
 int walk_grid_blocks(uint32_t n) {
-  const uint32_t chunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  const uint32_t ct = walk_chunk_topics(n), chunks = (n + ct - 1) / ct;
   uint32_t blocks = chunks < 256u * 32u ? chunks : 256u * 32u;
   blocks = (blocks + 7) & ~7u;   // a multiple of the 8 XCDs
   return blocks ? (int)blocks : 1;
@@ -1675,7 +1707,7 @@ static uint32_t deep_waves_per_cu() {
 }
 
 int deep_grid_blocks(uint32_t n) {
-  const uint32_t chunks = (n + WALK_CHUNK - 1) / WALK_CHUNK;
+  const uint32_t ct = walk_chunk_topics(n), chunks = (n + ct - 1) / ct;
   const uint32_t per = 256u * deep_waves_per_cu();
   uint32_t blocks = chunks < per ? chunks : per;
   blocks = (blocks + 7) & ~7u;
@@ -1690,6 +1722,10 @@ size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
 static void scan_counts(const uint32_t* cnt, uint32_t n, uint64_t* tile_sums, uint64_t* row_ptr,
                         hipStream_t s, uint64_t* copy = nullptr) {
+  if (n <= SCAN_SMALL) {
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, cnt, n, row_ptr, copy);
+    return;
+  }
   const uint32_t ntiles = (uint32_t)scan_tiles(n);
   if (ntiles) hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(256), 0, s, cnt, n, tile_sums);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, tile_sums, ntiles);
@@ -1743,13 +1779,23 @@ uint32_t walk_key_bits(uint32_t shape) {
 // Bytes per pair and pass: 12 read + 12 written (the last pass writes only the
 // records), + 4 read once for the histograms.
 constexpr int SORT_THREADS = 256;
-constexpr int SORT_ITEMS = 15;                                  // pairs per thread: 3840 per tile, 51 KB LDS -> 3 blocks/CU
+#ifndef EGM_SORT_ITEMS
+#define EGM_SORT_ITEMS 15                                       // pairs per thread: 3840 per tile, 51 KB LDS -> 3 blocks/CU
+#endif
+#ifndef EGM_SORT_TICKET
+#define EGM_SORT_TICKET 1                                       // 0 (A/B): tile = blockIdx (in-order dispatch assumed)
+#endif
+constexpr int SORT_ITEMS = EGM_SORT_ITEMS;
 constexpr uint32_t SORT_TILE = SORT_THREADS * SORT_ITEMS;
 constexpr uint32_t SORT_MAX_PASSES = 4;
 constexpr uint32_t SORT_HIST_BLOCKS = 1024;
 constexpr uint32_t SORT_AGG = 1u << 30, SORT_PFX = 2u << 30, SORT_CNT = SORT_AGG - 1u;
 constexpr size_t SORT_HEAD = 8192;                              // tickets[4] + hist[4][256], rounded
 constexpr uint32_t SORT_SPIN_LIMIT = 1u << 20;                  // look-back polls before a guard trip
+#ifndef EGM_SORT_LB
+#define EGM_SORT_LB 8                                           // look-back words in flight per digit
+#endif
+constexpr int SORT_LB = EGM_SORT_LB;
 
 static inline uint32_t sort_passes(uint32_t kbits) { return (kbits + 7) / 8; }
 static inline uint32_t sort_tiles(uint32_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
@@ -1764,27 +1810,42 @@ size_t walk_sort_temp_bytes(uint32_t n, uint32_t shape) {
 __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ key, uint32_t n, uint32_t begin,
                                                   uint32_t npass, uint32_t* __restrict__ hist,
                                                   uint32_t* __restrict__ status, uint64_t status_words) {
-  __shared__ uint32_t h[SORT_MAX_PASSES * 256];
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < npass * 256; i += 256) h[i] = 0;
+  // one copy of the histograms per wave: LDS atomics of one wave only contend
+  // with each other (the walk key's top digit is Zipf-skewed)
+  __shared__ uint32_t h[4][SORT_MAX_PASSES * 256];
+  const uint32_t tid = threadIdx.x, wv = tid >> 6;
+  for (uint32_t i = tid; i < 4 * SORT_MAX_PASSES * 256; i += 256) (&h[0][0])[i] = 0;
   const uint64_t g0 = (uint64_t)blockIdx.x * 256 + tid, gs = (uint64_t)gridDim.x * 256;
   for (uint64_t i = g0; i < status_words; i += gs) status[i] = 0;
   __syncthreads();
+  uint32_t* hw = h[wv];
   auto count = [&](uint32_t k) {
-    for (uint32_t p = 0; p < npass; ++p) atomicAdd(&h[p * 256 + ((k >> (begin + 8 * p)) & 0xFFu)], 1u);
+    for (uint32_t p = 0; p < npass; ++p) atomicAdd(&hw[p * 256 + ((k >> (begin + 8 * p)) & 0xFFu)], 1u);
   };
   const uint32_t n4 = n / 4;
-  for (uint64_t i = g0; i < n4; i += gs) {
-    const uint4 k = ((const uint4*)key)[i];
-    count(k.x);
-    count(k.y);
-    count(k.z);
-    count(k.w);
+  constexpr int HU = 8;   // loads in flight per thread (the loop is latency-bound otherwise)
+  for (uint64_t i0 = g0; i0 < n4; i0 += gs * HU) {
+    uint4 k[HU];
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const uint64_t i = i0 + gs * u;
+      k[u] = ((const uint4*)key)[i < n4 ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      if (i0 + gs * u >= n4) break;
+      count(k[u].x);
+      count(k[u].y);
+      count(k[u].z);
+      count(k[u].w);
+    }
   }
   for (uint64_t i = (uint64_t)n4 * 4 + g0; i < n; i += gs) count(key[i]);
   __syncthreads();
-  for (uint32_t i = tid; i < npass * 256; i += 256)
-    if (h[i]) atomicAdd(&hist[i], h[i]);
+  for (uint32_t i = tid; i < npass * 256; i += 256) {
+    const uint32_t c = h[0][i] + h[1][i] + h[2][i] + h[3][i];
+    if (c) atomicAdd(&hist[i], c);
+  }
 }
 
 // exclusive scan of one value per thread over a 256-thread block
@@ -1814,7 +1875,11 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_pass(const uint32_t* __re
   __shared__ uint32_t s_wsum[SORT_THREADS / 64];
   __shared__ uint32_t s_tile;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+#if EGM_SORT_TICKET
   if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+#else
+  if (tid == 0) s_tile = blockIdx.x;
+#endif
   for (uint32_t i = tid; i < (SORT_THREADS / 64) * 256; i += SORT_THREADS) (&s_cnt[0][0])[i] = 0;
   __syncthreads();
   const uint32_t tile = s_tile;
@@ -1861,21 +1926,38 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_pass(const uint32_t* __re
     excl = block_excl_scan256(hist[d], tid, s_wsum);   // the digit's first position in the whole output
   } else {
     __hip_atomic_store(my, SORT_AGG | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t j = tile - 1;
+    // windowed look-back: SORT_LB predecessors' words in flight at once, summed
+    // nearest first up to the first inclusive prefix (tile 0 always publishes
+    // one); a word not yet published ends the window and is polled again
+    int64_t j = (int64_t)tile - 1;
     uint32_t spins = 0;
     for (;;) {
-      const uint32_t x = __hip_atomic_load(status + j * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t f = x & ~SORT_CNT;
-      if (f == 0) {
-        if (++spins > SORT_SPIN_LIMIT) {   // a bug, reported (rows not assembled), never a hang
-          atomicOr(&stats->guard, GUARD_LOOP);
-          break;
-        }
-        continue;
+      uint32_t x[SORT_LB];
+#pragma unroll
+      for (int q = 0; q < SORT_LB; ++q) {
+        const int64_t jj = j - q;
+        x[q] = __hip_atomic_load(status + (uint64_t)(jj > 0 ? jj : 0) * 256 + d, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
       }
-      excl += x & SORT_CNT;
-      if (f == SORT_PFX) break;
-      --j;
+      uint32_t used = 0;
+      bool stop = false, done = false;
+#pragma unroll
+      for (int q = 0; q < SORT_LB; ++q) {
+        const uint32_t f = x[q] & ~SORT_CNT;
+        if (stop || f == 0) {
+          stop = true;
+          continue;
+        }
+        excl += x[q] & SORT_CNT;
+        ++used;
+        if (f == SORT_PFX) done = stop = true;
+      }
+      if (done) break;
+      j -= used;
+      if (!used && ++spins > SORT_SPIN_LIMIT) {   // a bug, reported (rows not assembled), never a hang
+        atomicOr(&stats->guard, GUARD_LOOP);
+        break;
+      }
     }
   }
   __hip_atomic_store(my, SORT_PFX | ((excl + tot) & SORT_CNT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1896,9 +1978,17 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_pass(const uint32_t* __re
   for (uint32_t j = tid; j < nt; j += SORT_THREADS) {
     const uint32_t kk = s_key[j];
     const uint32_t dg = (kk >> shift) & 0xFFu;
+#if defined(EGM_SORT_AB) && EGM_SORT_AB == 2   // measurement only: every tile's output contiguous (not a sort)
+    const uint64_t dst = base + j + (dg & 0u);
+#else
     const uint64_t dst = (uint64_t)s_base[dg] + (j - s_start[dg]);
+#endif
+#if defined(EGM_SORT_AB) && EGM_SORT_AB == 1   // measurement only: no output stores
+    if (kk == 0x7FFFFFF1u && s_val[j] == 0x7FFFFFF1ull) vout[0] = dst;
+#else
     if (kout) kout[dst] = kk;
     vout[dst] = s_val[j];
+#endif
   }
 }
 
@@ -1955,6 +2045,7 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
   }
   MatchWork w = w_in;
   w.walk_rows = out.topic != nullptr;
+  w.ct = walk_chunk_topics(n);
   const uint32_t kbits = min(walk_key_bits(w.key_shape), 32u);
   // (fixed-stride word offsets t * FIX_WORDS stay 32-bit below 2^29 topics)
   const bool sorted = kbits && w.order && n >= SORT_MIN_TOPICS && n < (1u << 29) && !(w.debug & DEBUG_INPUT_ORDER);
@@ -1997,13 +2088,13 @@ hipError_t launch_match(const DevTable& tab, const uint8_t* blob, const uint32_t
 #define EGM_REC_ROWS 1   // 1: k_rec_burst; 0: k_rec_rows (A/B)
 #endif
   const uint32_t rblocks = (uint32_t)std::min<uint64_t>(
-      65536, std::max<uint64_t>(1, (((uint64_t)n + 63) / 64 + REC_WAVES - 1) / REC_WAVES));
+      65536, std::max<uint64_t>(1, (((uint64_t)n + w.ct - 1) / w.ct + REC_WAVES - 1) / REC_WAVES));
 #if EGM_REC_ROWS
   hipLaunchKernelGGL(k_rec_burst, dim3(rblocks), dim3(64 * REC_WAVES), 0, s, w.rec, w.rec_cap, w.chunks, w.dir,
-                     w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats);
+                     w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats, w.ct);
 #else   // A/B: one record at a time, the next in flight
   hipLaunchKernelGGL(k_rec_rows, dim3(rblocks), dim3(64 * REC_WAVES), 0, s, w.rec, w.rec_cap, w.chunks, w.dir,
-                     w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats);
+                     w.order, n, out.row_ptr, out.topic, out.ids, out.ids_cap, w.stats, w.ct);
 #endif
   trace(s, "k_rec_rows");
   hipLaunchKernelGGL(k_compact, dim3(cblocks), dim3(64 * COMPACT_WAVES), 0, s, w.pieces, w.ids_tmp, n, out.row_ptr,
@@ -2446,21 +2537,24 @@ __device__ __forceinline__ void seg_copy16(const uint8_t* __restrict__ src, uint
 __global__ __launch_bounds__(256) void k_copy_out(const uint64_t* __restrict__ row, uint32_t n,
                                                   const uint32_t* __restrict__ ids, uint64_t ids_cap,
                                                   const uint8_t* __restrict__ flags, uint8_t* __restrict__ h_row,
-                                                  uint8_t* __restrict__ h_ids, uint8_t* __restrict__ h_fl) {
+                                                  uint8_t* __restrict__ h_ids, uint8_t* __restrict__ h_fl,
+                                                  const MatchStats* __restrict__ st, MatchStats* __restrict__ h_st) {
   const uint64_t gtid = (uint64_t)blockIdx.x * 256 + threadIdx.x, gsize = (uint64_t)gridDim.x * 256;
   const uint64_t nid = min(row[n], ids_cap);   // an overflowed batch is rerun: its copy is discarded
   seg_copy16((const uint8_t*)ids, h_ids, nid * 4, 4, gtid, gsize);
   seg_copy16((const uint8_t*)row, h_row, ((uint64_t)n + 1) * 8, 8, gtid, gsize);
   seg_copy16(flags, h_fl, n, 1, gtid, gsize);
+  if (st && gtid < sizeof(MatchStats) / 4) ((uint32_t*)h_st)[gtid] = ((const uint32_t*)st)[gtid];
 }
 
 hipError_t launch_copy_out(const uint64_t* row, uint32_t n, const uint32_t* ids, uint64_t ids_cap,
-                           const uint8_t* flags, uint8_t* h_row, uint8_t* h_ids, uint8_t* h_fl, hipStream_t s) {
+                           const uint8_t* flags, uint8_t* h_row, uint8_t* h_ids, uint8_t* h_fl, hipStream_t s,
+                           const MatchStats* st, MatchStats* h_st) {
   // one 256-thread block per CU is enough for the PCIe link (tools/d2hbench: 54 GB/s at 256 blocks) and
   // leaves the CUs' other wave slots to the next batch's match on the other stream (1 024 blocks held
   // them all for the copy's ~4 ms: r4a/r4b host_e2e 146 M topics/s)
   hipLaunchKernelGGL(k_copy_out, dim3(EGM_COPY_OUT_BLOCKS), dim3(256), 0, s, row, n, ids, ids_cap, flags, h_row, h_ids,
-                     h_fl);
+                     h_fl, st, h_st);
   return hipGetLastError();
 }
 

@@ -90,6 +90,10 @@ for step in "$@"; do
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "pmc_tcc_$v" 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$R/gpurun_out/${TAG}_pmc_tcc_$v" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "pmc_sq2_$v" 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_SMEM -d "$R/gpurun_out/${TAG}_pmc_sq2_$v" -o run --output-format csv -- $B --steps 3 --warmup 0 --cpu-baseline off --host-e2e off --pipelined off ;;
     host) run host 600 python tools/bench_host.py ;;
+    batcher) run batcher 600 python tools/bench_batcher.py ;;
+    btrace)   # one small batch at a time: host pipeline stamps, then the device timeline
+      EGM_PIPE_TRACE=1 run btrace 300 python tools/batch_trace.py 4096 200
+      run btrace_k 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$R/gpurun_out/${TAG}_btrace_k" -o run --output-format csv -- python tools/batch_trace.py 4096 200 ;;
     host_ptrace) EGM_PIPE_TRACE=1 run host_ptrace 600 python tools/bench_host.py ;;   # pipeline events on stderr
     host_hip) EGM_PIPE_COPY=hip run host_hip 600 python tools/bench_host.py ;;   # A/B: hipMemcpyAsync (blit kernel)
     host_k) EGM_PIPE_COPY=kernel run host_k 600 python tools/bench_host.py ;;   # A/B: the copy-out kernel
@@ -134,6 +138,11 @@ for step in "$@"; do
     abx_*)   # A/B variant, second sample (own log/prof names)
       v=${step#abx_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "abx_$v" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_profx_$v" -o run --output-format csv -- $B --steps 10 --warmup 2 --cpu-baseline off --host-e2e off ;;
+    sort)   # the walk-order sort alone (tools/sort_bench.py) under rocprof stats
+      run sort 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_sort" -o run --output-format csv -- python $R/tools/sort_bench.py ;;
+    sort_*)   # the same on variant V
+      v=${step#sort_}
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_sort_$v" -o run --output-format csv -- python $R/tools/sort_bench.py ;;
     ab_*)   # A/B variant built by tools/build_variant.py: C2 bench under rocprof stats
       v=${step#ab_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_$v" -o run --output-format csv -- $B --steps 10 --warmup 2 --cpu-baseline off --host-e2e off ;;
