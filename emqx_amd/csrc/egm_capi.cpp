@@ -289,6 +289,8 @@ struct egm_ctx {
   hipStream_t copy_stream = nullptr;   // pipeline host->device copies
   hipStream_t d2h_stream = nullptr;    // pipeline device->host copies (PCIe is full duplex)
   hipStream_t d2h_stream2 = nullptr;   // ... the second half of the ids
+  hipStream_t small_streams[MATCH_WORKSPACES] = {};   // small pipeline batches, round robin: they run side by side
+  uint32_t small_rr = 0;
   // The copier thread (round 4): it waits for each launched batch's match
   // (ev_match; the stats, copied before it in stream order, hold the exact id
   // total) and enqueues the result's D2H as DMA copies of exactly that size.
@@ -934,6 +936,12 @@ void egm_close(egm_ctx* c) {
     set_device(c);
     if (c->d2h_stream) hipStreamSynchronize(c->d2h_stream);
     if (c->d2h_stream2) hipStreamSynchronize(c->d2h_stream2);
+    for (auto& ss : c->small_streams)
+      if (ss) {
+        hipStreamSynchronize(ss);
+        hipStreamDestroy(ss);
+        ss = nullptr;
+      }
     c->pipe.clear();
     if (c->copy_stream) hipStreamDestroy(c->copy_stream);
     if (c->d2h_stream) hipStreamDestroy(c->d2h_stream);
@@ -1224,7 +1232,8 @@ static bool pipe_copy_forced() {
   return v;
 }
 // Batches up to this many topics take the small-batch result path (pipe_launch).
-constexpr uint64_t PIPE_SMALL_TOPICS = 65536;
+constexpr uint64_t PIPE_SMALL_TOPICS = 16384;   // (65536 measured: the copy-out on the match's
+                                                 // stream then costs more than the SDMA path's overlap)
 
 // EGM_PIPE_TRACE=1: one stderr line per pipeline event with a ms clock
 // (diagnostics of the host pipeline's bubbles).
@@ -1247,6 +1256,16 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   hipError_t e;
   hipStream_t s = c->stream;
   const uint64_t n = S.n;
+  const bool small = n <= PIPE_SMALL_TOPICS && !pipe_copy_forced();
+  if (small) {
+    // a small batch fills a fraction of the GPU: consecutive ones run side by
+    // side, each on its own stream and workspace (pick_ws orders a workspace
+    // last used on another stream after that use)
+    hipStream_t& ss = c->small_streams[c->small_rr++ % MATCH_WORKSPACES];
+    if (!ss && (e = hipStreamCreateWithFlags(&ss, hipStreamNonBlocking)) != hipSuccess)
+      return c->hip_fail(e, "small-batch stream");
+    s = ss;
+  }
   std::shared_ptr<Epoch> ep = c->cur;
   S.epoch = ep->id;
   MatchWs& W = pick_ws(c, s);
@@ -1266,7 +1285,7 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
     return r;
   }
   c->last_pending = false;   // this batch's counters travel with the slot
-  if (n <= PIPE_SMALL_TOPICS && !pipe_copy_forced()) {
+  if (small) {
     // A small batch (the Erlang batcher's: 4096 by default) is latency-bound,
     // not bandwidth-bound: its result goes to pinned memory by a copy-out
     // kernel on the match's own stream — flags read from the workspace, the
