@@ -902,7 +902,9 @@ def main():
                       "deferred_chunks": st["deferred_chunks"], "walk_iters": wc["iters"],
                       "walk_popped": wc["popped"], "walk_bounded_pops": wc["bounded"],
                       "walk_lane_occupancy": wc["lane_occupancy"], "walk_bucket_reads": wc["lit_probes"],
-                      "walk_plus_record_reads": wc["plus_reads"]},
+                      "walk_plus_record_reads": wc["plus_reads"],
+                      "walk_second_bucket_reads": wc.get("slow_probes"),
+                      "walk_iters_with_second_read": wc.get("slow_iters")},
             "fanout": ({"deliveries_per_step": deliveries, "subscriber_entries": sub_entries,
                         "fanout_ms": tim["fanout_ms"] / max(1, tim["fanout_launches"]),
                         "deliveries_per_s": deliveries * (1 if shard else world) * args.steps / elapsed,

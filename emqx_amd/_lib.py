@@ -108,6 +108,7 @@ SIGNATURES = {
     "egm_last_stats": (C.c_int, [_P, _u64p, _u64p, _u32p, _u32p, _u32p]),
     "egm_last_guard": (C.c_int, [_P, _u32p]),
     "egm_last_walk_counters": (C.c_int, [_P, _u64p, _u64p, _u64p, _u64p, _u64p]),
+    "egm_last_walk_probes": (C.c_int, [_P, _u64p, _u64p]),
     "egm_set_timing": (C.c_int, [_P, C.c_int]),
     "egm_set_debug": (C.c_int, [_P, C.c_uint32]),
     "egm_get_timing": (C.c_int, [_P, C.POINTER(C.c_double), _u64p, C.POINTER(C.c_double), _u64p]),

@@ -427,7 +427,7 @@ int HostTable::bulk_build(const uint8_t* blob, const uint32_t* off, uint32_t n, 
   phase("node records");
   // ---- 4. edge table at relayout's size, edges in child order ----
   size_t nb = 16;
-  while (nb * EDGE_BUCKET < (size_t)n_lit * 2) nb <<= 1;
+  while (nb * EDGE_BUCKET < (size_t)n_lit * EDGE_SPREAD) nb <<= 1;
   edges.assign(nb * EDGE_BUCKET, EdgeSlot{NONE, 0, 0, 0, NONE, NONE, NONE, 0});
   n_edges_ = n_lit;
   n_edge_tombs_ = 0;

@@ -1154,6 +1154,16 @@ int egm_last_walk_counters(egm_ctx* c, uint64_t* iters, uint64_t* popped, uint64
   return EGM_OK;
 }
 
+int egm_last_walk_probes(egm_ctx* c, uint64_t* slow_lanes, uint64_t* slow_iters) {
+  if (!c) return EGM_E_INVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  int r = sync_last(c);
+  if (r) return r;
+  if (slow_lanes) *slow_lanes = c->last.slow_lanes;
+  if (slow_iters) *slow_iters = c->last.slow_iters;
+  return EGM_OK;
+}
+
 int egm_last_stats(egm_ctx* c, uint64_t* n_ids, uint64_t* visited, uint32_t* n_def, uint32_t* overflow,
                    uint32_t* n_error) {
   if (!c) return EGM_E_INVAL;

@@ -56,7 +56,15 @@ constexpr uint8_t TF_HEAVY    = 4;   // matched by the overflow (heavy) kernel
 constexpr uint8_t TF_ERROR    = 8;   // could not be matched (see egm_last_error)
 constexpr uint8_t TF_SKIP     = 16;  // padding past a device-side topic count (egm_match_device_counted): no walk
 
-constexpr int EDGE_BUCKET = 4;       // slots per 64 B bucket
+constexpr int EDGE_BUCKET = 4;       // slots per 128 B bucket (a walker reads its first 64 B: two slots)
+#ifndef EGM_EDGE_SPREAD
+#define EGM_EDGE_SPREAD 2
+#endif
+// Edge slots per literal edge, at least: the table's slot load stays in
+// (1/(2·SPREAD), 1/SPREAD].  A probe whose key is not in its bucket's first
+// two slots (or, for an absent key, whose first two slots are both taken)
+// costs the walking wave a second dependent round trip.
+constexpr uint32_t EDGE_SPREAD = EGM_EDGE_SPREAD;
 
 struct NodeRec {          // 16 B, one dwordx4 load
   uint32_t plus_child;    // node reached by '+', or NONE

@@ -31,14 +31,14 @@ struct MatchStats {               // device-side counters, zeroed per batch
   unsigned int errors;            // topics the heavy kernel could not walk (never for legal topics)
   unsigned int guard;             // GUARD_* bits: a kernel invariant failed (a bug, never a capacity
                                   // problem; reported instead of hanging the GPU, rows not assembled)
-  unsigned int pad_;
+  unsigned int slow_lanes;        // walk literal probes that needed a second bucket read (instrumentation)
   unsigned long long iters;       // walk iterations (instrumentation)
   unsigned long long popped;      // items popped by the walk (lane occupancy = popped / (iters * 64))
   unsigned long long bounded;     // walk iterations whose pop was cut by the stack-room bound (DFS regime)
   unsigned long long lit_probes;  // walk pops that read an edge bucket (instrumentation)
   unsigned long long plus_reads;  // walk pops that read a '+' child's record (instrumentation)
   unsigned int n_deep;            // chunks handed to the deep pass of the walk (more than DEEP_MIN levels)
-  unsigned int pad2_;
+  unsigned int slow_iters;        // walk iterations in which some lane needed a second bucket read
   unsigned long long rec_cursor;  // flush-record slab u32 reserved (per-wave segments, incl. slack)
 };
 

@@ -487,6 +487,9 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #ifndef EGM_WALK_PAIRS
 #define EGM_WALK_PAIRS 0     // A/B: the first pass pops two items per lane per iteration
 #endif
+#ifndef EGM_PROBE4
+#define EGM_PROBE4 0         // A/B: a literal probe reads all four slots of its bucket (two lines) at once
+#endif
 #ifndef EGM_PLUS_SKIP
 #define EGM_PLUS_SKIP 1      // skip a literal child's '+' transition that would do nothing (A/B: 0)
 #endif
@@ -672,6 +675,9 @@ struct Pend {
   uint32_t nsig2;           // the signature bit of the word at level + 2 (the literal child's '+' child)
   bool act, lit, plus, d1;  // d1: a one-word '$' topic (do_match/1's lookup_topic probe)
   uint4 prec, l0, h0, l1, h1;
+#if EGM_PROBE4
+  uint4 l2, h2, l3, h3;     // A/B: the bucket's second line (slots 2-3) read in the same round
+#endif
 };
 
 // Branch-free on purpose: every lane issues its loads unconditionally (an
@@ -693,6 +699,12 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* words
   p.h0 = ld16(bp + 16);
   p.l1 = ld16(bp + 32);
   p.h1 = ld16(bp + 48);
+#if EGM_PROBE4
+  p.l2 = ld16(bp + 64);
+  p.h2 = ld16(bp + 80);
+  p.l3 = ld16(bp + 96);
+  p.h3 = ld16(bp + 112);
+#endif
   // the next level's word (used only if level + 1 < D).  From the LDS stage
   // it is read unclamped, so the read does not wait for the topic's depth
   // (a leaf reads the next topic's word 0, or the pad word past the stage).
@@ -724,6 +736,7 @@ struct Out {
   bool e0, e1, e2, e3;
   uint4 c0, c1;             // children to push
   bool p0, p1;
+  bool slow;                // the literal probe needed another bucket read (instrumentation)
   uint32_t created;         // states created (SURVEY §8d V_t)
 };
 
@@ -754,9 +767,30 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend
   uint32_t hx = (p.h0.x & ~s1) | (p.h1.x & s1), hy = (p.h0.y & ~s1) | (p.h1.y & s1);
   uint32_t hz = (p.h0.z & ~s1) | (p.h1.z & s1), hw = (p.h0.w & ~s1) | (p.h1.w & s1);
   bool found = p.lit && (m0 || m1);
-  if (p.lit && !m0 && !z0 && !m1 && !z1) {   // the slots read hold other keys: keep probing
+#if EGM_PROBE4
+  const bool q = !m0 && !z0 && !m1 && !z1;   // slots 2-3 (already loaded) are next
+  const bool m2 = q && p.l2.x == node && p.l2.y == p.it.w, z2 = p.l2.x == NONE;
+  const bool m3 = q && !m2 && !z2 && p.l3.x == node && p.l3.y == p.it.w, z3 = p.l3.x == NONE;
+  {
+    const uint32_t s2 = m2 ? 0xFFFFFFFFu : 0u, s3 = m3 ? 0xFFFFFFFFu : 0u, k = s2 | s3;
+    cz = (cz & ~k) | (p.l2.z & s2) | (p.l3.z & s3);
+    cw = (cw & ~k) | (p.l2.w & s2) | (p.l3.w & s3);
+    hx = (hx & ~k) | (p.h2.x & s2) | (p.h3.x & s3);
+    hy = (hy & ~k) | (p.h2.y & s2) | (p.h3.y & s3);
+    hz = (hz & ~k) | (p.h2.z & s2) | (p.h3.z & s3);
+    hw = (hw & ~k) | (p.h2.w & s2) | (p.h3.w & s3);
+  }
+  found = found || (p.lit && (m2 || m3));
+  const bool slow = p.lit && q && !m2 && !z2 && !m3 && !z3;
+  constexpr int K0 = 4;
+#else
+  const bool slow = p.lit && !m0 && !z0 && !m1 && !z1;
+  constexpr int K0 = 2;
+#endif
+  o.slow = slow;
+  if (slow) {   // the slots read hold other keys: keep probing
     uint4 lo, hi;
-    found = edge_probe_from(tab, edge_bucket(node, p.it.w, tab.edge_mask), 2, node, p.it.w, &lo, &hi);
+    found = edge_probe_from(tab, edge_bucket(node, p.it.w, tab.edge_mask), K0, node, p.it.w, &lo, &hi);
     cz = lo.z;
     cw = lo.w;
     hx = hi.x;
@@ -873,6 +907,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
   root.w = uni(root.w);
   uint32_t created = 0;
   unsigned long long iters = 0, popped = 0, bounded = 0, lit_probes = 0, plus_reads = 0;
+  uint32_t slow_lanes = 0, slow_iters = 0;
   RecCursor rc{0, 0, 0, 0, 0};
   const uint32_t guard_lim = (w.debug & DEBUG_FORCE_GUARD) ? 2u : (1u << EGM_GUARD_BITS);
   // sorted batch: the record of the chunk's j-th topic in walk order, loaded
@@ -1056,6 +1091,11 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
           Out o;
           finish(tab, mode, q, o);
           created += o.created;
+          {
+            const uint32_t ns = popc(__ballot(o.slow));
+            slow_lanes += ns;
+            slow_iters += ns ? 1u : 0u;
+          }
           const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
           const uint32_t m0 = popc(c0b), nc = m0 + popc(c1b);
           if (sp + nc > STK) {   // guard only: the pop bound keeps sp + pushes <= STK
@@ -1120,6 +1160,10 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
     if (bounded) atomicAdd(&w.stats->bounded, bounded);
     atomicAdd(&w.stats->lit_probes, lit_probes);
     atomicAdd(&w.stats->plus_reads, plus_reads);
+    if (slow_lanes) {
+      atomicAdd(&w.stats->slow_lanes, slow_lanes);
+      atomicAdd(&w.stats->slow_iters, slow_iters);
+    }
   }
 }
 

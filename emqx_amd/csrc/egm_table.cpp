@@ -286,9 +286,9 @@ uint32_t HostTable::edge_find(uint32_t parent, uint32_t wid) const {
 
 uint32_t HostTable::edge_insert(uint32_t parent, uint32_t wid, uint32_t child, uint32_t cflags) {
   size_t nb = edges.size() / EDGE_BUCKET;
-  if ((n_edges_ + n_edge_tombs_ + 1) * 2 > nb * EDGE_BUCKET) {
+  if ((n_edges_ + n_edge_tombs_ + 1) * EDGE_SPREAD > nb * EDGE_BUCKET) {
     size_t want = nb;
-    while ((n_edges_ + 1) * 2 > want * EDGE_BUCKET / 2) want *= 2;  // rehash to <= 25% load
+    while ((n_edges_ + 1) * EDGE_SPREAD > want * EDGE_BUCKET / 2) want *= 2;  // rehash to <= half the max load
     edge_rehash(want);
   }
   uint32_t m = edge_mask(), b = edge_bucket(parent, wid, m);
@@ -540,7 +540,7 @@ void HostTable::relayout() {
   nodes.reserve(room);
 
   size_t nb = 16;
-  while (nb * EDGE_BUCKET < (size_t)n_edges_ * 2) nb <<= 1;  // 25-50 % slot load
+  while (nb * EDGE_BUCKET < (size_t)n_edges_ * EDGE_SPREAD) nb <<= 1;  // slot load in (1/(2 SPREAD), 1/SPREAD]
   std::vector<EdgeSlot> old;
   old.swap(edges);
   edges.assign(nb * EDGE_BUCKET, EdgeSlot{NONE, 0, 0, 0, NONE, NONE, NONE, 0});

@@ -275,8 +275,10 @@ class GpuMatcher:
         self._check(self.lib.egm_last_walk_counters(self.ctx, C.byref(a), C.byref(b), C.byref(c), C.byref(d),
                                                     C.byref(e)), "egm_last_walk_counters")
         occ = b.value / max(1, a.value * 64)
+        sl, si = C.c_uint64(), C.c_uint64()
+        self._check(self.lib.egm_last_walk_probes(self.ctx, C.byref(sl), C.byref(si)), "egm_last_walk_probes")
         return {"iters": a.value, "popped": b.value, "bounded": c.value, "lane_occupancy": occ,
-                "lit_probes": d.value, "plus_reads": e.value}
+                "lit_probes": d.value, "plus_reads": e.value, "slow_probes": sl.value, "slow_iters": si.value}
 
     def set_debug(self, flags: int):
         self._check(self.lib.egm_set_debug(self.ctx, flags), "egm_set_debug")

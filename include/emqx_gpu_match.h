@@ -235,6 +235,9 @@ int egm_last_guard(egm_ctx* ctx, uint32_t* guard);
    line reads).  Any pointer may be NULL. */
 int egm_last_walk_counters(egm_ctx* ctx, uint64_t* iters, uint64_t* popped, uint64_t* bounded, uint64_t* lit_probes,
                            uint64_t* plus_reads);
+/* Instrumentation: the last batch's literal probes that needed a second
+   (dependent) bucket read, and the walk iterations in which any lane did. */
+int egm_last_walk_probes(egm_ctx* ctx, uint64_t* slow_lanes, uint64_t* slow_iters);
 /* Enable per-kernel timing with HIP events on the launch stream (0/1) and read
    the accumulated walk-kernel time (ms) and launch count. */
 int egm_set_timing(egm_ctx* ctx, int enable);
