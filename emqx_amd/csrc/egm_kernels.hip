@@ -467,6 +467,7 @@ constexpr uint32_t ML_BITS = 17;
 constexpr uint32_t MT_SHIFT = 17;
 constexpr uint32_t MF_SHIFT = 24;
 constexpr uint32_t MW_SHIFT = 28;
+constexpr uint32_t M_CONT = 1u << 29;   // a literal probe continued: z = the next 64-B edge line to read
 constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #ifndef EGM_GUARD_BITS
 #define EGM_GUARD_BITS 22   // loop guards: iterations a wave may spend in one loop before reporting a bug
@@ -486,6 +487,10 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #endif
 #ifndef EGM_WALK_PAIRS
 #define EGM_WALK_PAIRS 0     // A/B: the first pass pops two items per lane per iteration
+#endif
+#ifndef EGM_PROBE_CONT
+#define EGM_PROBE_CONT 1     // a literal probe whose first line holds other keys is continued as a stack item
+                             // (1: the first pass; 2: both passes; 0: off — A/B)
 #endif
 #ifndef EGM_PROBE4
 #define EGM_PROBE4 0         // A/B: a literal probe reads all four slots of its bucket (two lines) at once
@@ -675,6 +680,7 @@ struct Pend {
   uint32_t nsig2;           // the signature bit of the word at level + 2 (the literal child's '+' child)
   bool act, lit, plus, d1;  // d1: a one-word '$' topic (do_match/1's lookup_topic probe)
   uint4 prec, l0, h0, l1, h1;
+  uint32_t line;            // the 64-B edge line read (its two slots are l0/h0, l1/h1)
 #if EGM_PROBE4
   uint4 l2, h2, l3, h3;     // A/B: the bucket's second line (slots 2-3) read in the same round
 #endif
@@ -686,15 +692,19 @@ struct Pend {
 // the copy it inserts there waits for the load.  The next level's word comes
 // from the LDS word stage (k_walk: `words` = the topic's staged words) or
 // from HBM (k_heavy: `words` = null, `wid` + `gbase`).
+template <bool CONT>
 __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* words, const uint32_t* __restrict__ wid,
                                       uint32_t gbase, Pend& p) {
   const uint32_t meta = p.it.y;
   const uint32_t fl = (meta >> MF_SHIFT) & 0xFu;
   p.plus = p.act && (fl & F_PLUS);
   p.lit = p.act && (fl & F_LIT) && p.it.w < WID_MAX;
-  const uint32_t bkt = edge_bucket(p.it.x, p.it.w, tab.edge_mask);
+  // the 64-B edge line to read: a bucket's first (two slots), or where a
+  // continued probe goes on (M_CONT: its z; such an item takes no '+')
+  const uint32_t line = (CONT && (meta & M_CONT)) ? p.it.z : 2u * edge_bucket(p.it.x, p.it.w, tab.edge_mask);
+  p.line = line;
   p.prec = ld16(tab.nodes + (p.plus ? p.it.z : 0u));
-  const uint8_t* bp = (const uint8_t*)(tab.edges + (size_t)(p.lit ? bkt : 0u) * EDGE_BUCKET);
+  const uint8_t* bp = (const uint8_t*)tab.edges + (size_t)(p.lit ? line : 0u) * 64;
   p.l0 = ld16(bp);   // the bucket's first two slots: one 64-B line
   p.h0 = ld16(bp + 16);
   p.l1 = ld16(bp + 32);
@@ -743,6 +753,7 @@ struct Out {
 // Straight-line on purpose: every field is computed unconditionally and
 // selected by the lane's flags (conditionally assigned fields became phis
 // whose copies cost a score of VGPRs).
+template <bool CONT>
 __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend& p, Out& o) {
   const uint32_t meta = p.it.y;
   const uint32_t level = meta & LEVEL_MAX;
@@ -788,7 +799,7 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend
   constexpr int K0 = 2;
 #endif
   o.slow = slow;
-  if (slow) {   // the slots read hold other keys: keep probing
+  if (!CONT && slow) {   // the slots read hold other keys: keep probing
     uint4 lo, hi;
     found = edge_probe_from(tab, edge_bucket(node, p.it.w, tab.edge_mask), K0, node, p.it.w, &lo, &hi);
     cz = lo.z;
@@ -820,6 +831,16 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend
   const uint32_t go0 = (puse ? (cw & F_PLUS) : 0u) | ((cw & nsig) ? (cw & F_LIT) : 0u);
   o.p0 = !leaf && go0;
   o.c0 = make_uint4(cz, base_meta | (go0 << MF_SHIFT) | (wc << MW_SHIFT), hx, nw);
+  if (CONT && slow) {
+    // both slots of the line hold other keys: rather than a second dependent
+    // read here, which the whole wave would wait for (82 % of C2's
+    // iterations had such a lane, round 6), the probe goes back on the stack
+    // as an item that reads the next line (same level, literal transition
+    // only) and is popped with the next iteration's items
+    const uint32_t nl = (p.line + 1) & (2u * (tab.edge_mask + 1u) - 1u);
+    o.p0 = true;
+    o.c0 = make_uint4(node, (meta & ~(0xFu << MF_SHIFT)) | (F_LIT << MF_SHIFT) | M_CONT, nl, p.it.w);
+  }
   // '+' child
   const uint32_t pf = p.plus ? p.prec.w : 0u;
   o.e2 = (pf & F_HASH) != 0;
@@ -895,6 +916,9 @@ template <bool DEEP>
 __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const uint32_t* __restrict__ off, uint32_t n,
                                                            int mode, MatchWork w) {
   constexpr uint32_t STK = DEEP ? WALK_STACK_DEEP : WALK_STACK;
+  // probe continuations in the first pass only: the deep pass (C3) measured
+  // 53.8 -> 55.2 ms with them, the first pass (C2) 8.20 -> 6.23 ms (round 6)
+  constexpr bool PROBE_CONT = EGM_PROBE_CONT != 0 && (!DEEP || EGM_PROBE_CONT > 1);
   __shared__ WaveLds<STK> L;
   const uint32_t lane = threadIdx.x;
   // the first pass walks every chunk, the deep pass the chunks the first handed on
@@ -1072,14 +1096,14 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
         const uint32_t ti = L.tinfo[tt];
         p.D = ti & 0xFFFFFFu;
         p.d1 = p.D == 1 && ((ti >> 24) & TF_DOLLAR);   // TF_DOLLAR < 0x80: the fixed-stride bit is not read
-        issue(tab, L.words + (tt & (S - 1)) * dmax, nullptr, 0, p);
+        issue<PROBE_CONT>(tab, L.words + (tt & (S - 1)) * dmax, nullptr, 0, p);
         uint32_t ttb = 0;
         if (PAIRS) {
           ttb = (pb.it.y >> MT_SHIFT) & 0x7Fu;
           const uint32_t tib = L.tinfo[ttb];
           pb.D = tib & 0xFFFFFFu;
           pb.d1 = pb.D == 1 && ((tib >> 24) & TF_DOLLAR);
-          issue(tab, L.words + (ttb & (S - 1)) * dmax, nullptr, 0, pb);
+          issue<PROBE_CONT>(tab, L.words + (ttb & (S - 1)) * dmax, nullptr, 0, pb);
           lit_probes += popc(__ballot(pb.lit));
           plus_reads += popc(__ballot(pb.plus));
         }
@@ -1089,7 +1113,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
         // ---- consume: children -> stack, emits -> stage ----
         auto consume = [&](const Pend& q, uint32_t qt) -> bool {
           Out o;
-          finish(tab, mode, q, o);
+          finish<PROBE_CONT>(tab, mode, q, o);
           created += o.created;
           {
             const uint32_t ns = popc(__ballot(o.slow));
@@ -1275,10 +1299,10 @@ __global__ __launch_bounds__(64) void k_heavy(DevTable tab, const uint32_t* __re
         p.it = ld16_l2(stk + (p.act ? bi + lane : 0u));
         p.D = D;
         p.d1 = D == 1 && (tf & TF_DOLLAR);
-        issue(tab, nullptr, words, tb, p);
+        issue<false>(tab, nullptr, words, tb, p);
         sp = bi;
         Out o;
-        finish(tab, mode, p, o);
+        finish<false>(tab, mode, p, o);
         if (pass == 0) created += o.created;
         const uint64_t c0b = __ballot(o.p0), c1b = __ballot(o.p1);
         const uint32_t m0 = popc(c0b);
