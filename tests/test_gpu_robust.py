@@ -84,10 +84,14 @@ def test_batches_on_two_streams(gm):
     d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
     n, cap = t.n, len(want.ids) + 1024
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    # the outputs are zeroed on torch's stream before any match is launched: the
+    # side streams do not wait for that stream, so a zero-fill still queued there
+    # could land after a match wrote its rows (a race of the test, not the library)
+    bufs = [(torch.zeros(n + 1, dtype=torch.int64, device=dev), torch.zeros(cap, dtype=torch.int32, device=dev))
+            for _ in range(4)]
+    torch.cuda.synchronize()
     outs = []
-    for s in (s1, s2, s1, s2):   # back to back on alternating streams, no host sync in between
-        r = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-        i = torch.zeros(cap, dtype=torch.int32, device=dev)
+    for s, (r, i) in zip((s1, s2, s1, s2), bufs):   # back to back on alternating streams, no host sync in between
         gm.match_device(d_blob.data_ptr(), int(t.off[-1]), d_off.data_ptr(), n, L.EGM_MODE_ROUTES,
                         s.cuda_stream, r.data_ptr(), i.data_ptr(), cap)
         outs.append((s, r, i))
