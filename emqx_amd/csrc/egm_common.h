@@ -7,7 +7,7 @@
 // word-level trie flattened into three HBM arrays:
 //
 //   nodes[]  16 B  {plus_child, hash_fid, term_fid, flags}
-//   edges[]  128 B buckets of four 32 B slots {parent, word_id, child, flags,
+//   edges[]  64 B buckets of two 32 B slots {parent, word_id, child, flags,
 //            child's plus_child, hash_fid, term_fid, flags of the child's '+' child}
 //   dict[]   32 B slots {hash64, word_id, len, inline bytes[16]}  (+ blob for long words)
 //
@@ -56,7 +56,17 @@ constexpr uint8_t TF_HEAVY    = 4;   // matched by the overflow (heavy) kernel
 constexpr uint8_t TF_ERROR    = 8;   // could not be matched (see egm_last_error)
 constexpr uint8_t TF_SKIP     = 16;  // padding past a device-side topic count (egm_match_device_counted): no walk
 
-constexpr int EDGE_BUCKET = 4;       // slots per 128 B bucket (a walker reads its first 64 B: two slots)
+#ifndef EGM_EDGE_BUCKET
+#define EGM_EDGE_BUCKET 2
+#endif
+// Slots per bucket, the unit a key is hashed to (a walker reads one 64-B line
+// = two slots at a time, starting at the key's bucket, then the next lines).
+// Round 6: 2 (a key's home is any 64-B line) instead of 4 (a 128-B bucket,
+// homes on every other line): at the same table size and slot load, fewer
+// keys sit past their home line — C2 probes that read a second line 56.3 M ->
+// 22.8 M per batch, k_walk 6.27 -> 5.86 ms; C3 166 M -> 60 M, 53.7 -> 48.9 ms.
+constexpr int EDGE_BUCKET = EGM_EDGE_BUCKET;
+static_assert(EDGE_BUCKET == 2 || EDGE_BUCKET == 4, "a bucket is one or two 64-B lines");
 #ifndef EGM_EDGE_SPREAD
 #define EGM_EDGE_SPREAD 2
 #endif
@@ -74,7 +84,7 @@ struct NodeRec {          // 16 B, one dwordx4 load
 };
 
 // A literal edge carries a copy of its child's record, so a literal
-// transition is a single 128 B bucket read (four 32 B slots).
+// transition is a single 64-B line read (a bucket of two 32 B slots).
 struct EdgeSlot {         // 32 B
   uint32_t parent;        // NONE = empty, TOMB = deleted
   uint32_t wid;

@@ -701,7 +701,7 @@ __device__ __forceinline__ void issue(const DevTable& tab, const uint32_t* words
   p.lit = p.act && (fl & F_LIT) && p.it.w < WID_MAX;
   // the 64-B edge line to read: a bucket's first (two slots), or where a
   // continued probe goes on (M_CONT: its z; such an item takes no '+')
-  const uint32_t line = (CONT && (meta & M_CONT)) ? p.it.z : 2u * edge_bucket(p.it.x, p.it.w, tab.edge_mask);
+  const uint32_t line = (CONT && (meta & M_CONT)) ? p.it.z : (EDGE_BUCKET / 2) * edge_bucket(p.it.x, p.it.w, tab.edge_mask);
   p.line = line;
   p.prec = ld16(tab.nodes + (p.plus ? p.it.z : 0u));
   const uint8_t* bp = (const uint8_t*)tab.edges + (size_t)(p.lit ? line : 0u) * 64;
@@ -837,7 +837,7 @@ __device__ __forceinline__ void finish(const DevTable& tab, int mode, const Pend
     // iterations had such a lane, round 6), the probe goes back on the stack
     // as an item that reads the next line (same level, literal transition
     // only) and is popped with the next iteration's items
-    const uint32_t nl = (p.line + 1) & (2u * (tab.edge_mask + 1u) - 1u);
+    const uint32_t nl = (p.line + 1) & ((EDGE_BUCKET / 2) * (tab.edge_mask + 1u) - 1u);
     o.p0 = true;
     o.c0 = make_uint4(node, (meta & ~(0xFu << MF_SHIFT)) | (F_LIT << MF_SHIFT) | M_CONT, nl, p.it.w);
   }

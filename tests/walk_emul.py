@@ -38,9 +38,10 @@ class Emul:
         """-> (child, record tuple (plus, hash, term, flags)) or (NONE, None)."""
         a = self.a
         b = self.img.edge_bucket(node, w, a["edge_mask"])
+        nk = len(a["edges"]) // (int(a["edge_mask"]) + 1)   # slots per bucket
         while True:
-            for k in range(4):
-                s = a["edges"][b * 4 + k]
+            for k in range(nk):
+                s = a["edges"][b * nk + k]
                 if int(s[0]) == node and int(s[1]) == w:
                     c = int(s[2])
                     rec = (int(s[4]), int(s[5]), int(s[6]), int(s[3]))

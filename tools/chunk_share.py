@@ -74,10 +74,11 @@ def main():
 
     def edge(node, w):
         b = img.edge_bucket(node, w, emask)
+        nk = len(edges) // (int(emask) + 1)   # slots per bucket
         probes = 0
         while True:
-            for k in range(4):
-                s = edges[b * 4 + k]
+            for k in range(nk):
+                s = edges[b * nk + k]
                 if int(s[0]) == node and int(s[1]) == w:
                     return int(s[2]), int(s[3]), int(s[4]), b
                 if int(s[0]) == NONE:
