@@ -1656,18 +1656,34 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
 #ifndef EGM_REC_BURST
 #define EGM_REC_BURST 8
 #endif
+#ifndef EGM_REC_BITMAP
+#define EGM_REC_BITMAP 1   // ids placed through a bitmap of run starts (A/B: 0, the LDS search)
+#endif
+#ifndef EGM_REC_WPE
+#define EGM_REC_WPE 4      // waves per SIMD k_rec_burst is compiled for (caps its VGPRs at 128)
+#endif
 constexpr uint32_t REC_BURST = EGM_REC_BURST;
-__global__ __launch_bounds__(64 * REC_WAVES) void k_rec_burst(const uint32_t* __restrict__ rec, uint64_t rec_cap,
+__global__ __launch_bounds__(64 * REC_WAVES) __attribute__((amdgpu_waves_per_eu(EGM_REC_WPE))) void k_rec_burst(const uint32_t* __restrict__ rec, uint64_t rec_cap,
                                                               const uint4* __restrict__ chunks,
                                                               const uint32_t* __restrict__ dir,
                                                               const uint64_t* __restrict__ order, uint32_t n,
                                                               const uint64_t* __restrict__ row_ptr,
                                                               uint32_t* __restrict__ topic, uint32_t* __restrict__ ids,
                                                               uint64_t ids_cap, MatchStats* stats, uint32_t ct) {
+#if EGM_REC_BITMAP
+  __shared__ uint64_t s_bm[REC_WAVES][REC_IPL];   // the record's run starts (bit q: an id position where a topic's run begins)
+  __shared__ uint64_t s_dst[REC_WAVES][64];       // the r-th run: its topic's next id in HBM minus the run's start
+#else
   __shared__ uint32_t s_ex[REC_WAVES][64];
   __shared__ uint64_t s_dst[REC_WAVES][64];
+#endif
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool ok = compact_checks(row_ptr, n, ids_cap, stats);
+#if EGM_REC_BITMAP
+  if (lane < REC_IPL) s_bm[wave][lane] = 0ull;
+  wave_sync();
+  const uint64_t lmask = (2ull << lane) - 1ull;   // positions <= lane of a 64-position word (lane 63: all)
+#endif
   const uint32_t nchunks = (n + ct - 1) / ct;
   for (uint32_t c = blockIdx.x * REC_WAVES + wave; c < nchunks; c += gridDim.x * REC_WAVES) {
     const uint32_t t = c * ct + lane;
@@ -1724,6 +1740,34 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_burst(const uint32_t* __
           break;
         }
         chain = off[b] + rec_size(tot);
+#if EGM_REC_BITMAP
+        // round 6: each non-empty topic marks where its run starts; an id's run
+        // is then the count of starts at or before it (popcounts of the bitmap)
+        // instead of a 6-step LDS search per id (k_rec_burst's VALU: 407M per C2 batch)
+        {
+          const bool ne = cr[b] != 0;
+          const uint64_t bal = __ballot(ne);
+          if (ne) {
+            s_dst[wave][mbcnt(bal)] = dst - ex;   // mod 2^64: id q of the run goes to (dst - ex) + q
+            atomicOr((unsigned long long*)&s_bm[wave][ex >> 6], 1ull << (ex & 63u));
+          }
+          dst += cr[b];
+          wave_sync();
+          uint64_t wk[REC_IPL];
+#pragma unroll
+          for (uint32_t k = 0; k < REC_IPL; ++k) wk[k] = uni64(s_bm[wave][k]);
+          if (lane < REC_IPL) s_bm[wave][lane] = 0ull;   // for the next record (a wave's LDS operations stay in order)
+          uint32_t pre = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < REC_IPL; ++k) {
+            const uint32_t q = lane + 64u * k;
+            const uint32_t r = pre + popc(wk[k] & lmask);   // runs that start at or before q (>= 1 below tot)
+            pre += popc(wk[k]);
+            if (q < tot) ids[s_dst[wave][r - 1] + q] = v[b][k];
+          }
+          wave_sync();
+        }
+#else
         s_ex[wave][lane] = ex;
         s_dst[wave][lane] = dst;
         dst += cr[b];
@@ -1740,6 +1784,7 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_burst(const uint32_t* __
           }
         }
         wave_sync();
+#endif
       }
     }
   }
