@@ -203,13 +203,14 @@ static ERL_NIF_TERM nif_apply_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM
   return enif_make_tuple2(env, ATOM_OK, enif_make_uint64(env, epoch));
 }
 
-/* Rows of a CSR as [[Id]] (shared by match_batch and wait). */
+/* Rows of a CSR as [[Id]] (shared by match_batch and wait); either result
+   form — wait/2's batches are submitted packed (EGM_RESULT_PACKED). */
 static ERL_NIF_TERM rows_term(ErlNifEnv* env, const egm_result* res) {
   ERL_NIF_TERM rows = enif_make_list(env, 0);
   for (uint32_t i = res->n_topics; i-- > 0;) {
     ERL_NIF_TERM row = enif_make_list(env, 0);
-    for (uint64_t k = res->row_ptr[i + 1]; k-- > res->row_ptr[i];)
-      row = enif_make_list_cell(env, enif_make_uint(env, res->ids[k]), row);
+    for (uint64_t k = egm_result_row(res, i + 1); k-- > egm_result_row(res, i);)
+      row = enif_make_list_cell(env, enif_make_uint(env, egm_result_id(res, k)), row);
     rows = enif_make_list_cell(env, row, rows);
   }
   return rows;
@@ -249,7 +250,7 @@ static ERL_NIF_TERM nif_submit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
       (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES) || !pack_list(env, argv[1], &blob, &off, &n))
     return enif_make_badarg(env);
   uint64_t ticket = 0;
-  int rc = egm_match_submit(r->ctx, blob, off, n, mode, &ticket);
+  int rc = egm_match_submit(r->ctx, blob, off, n, mode | EGM_RESULT_PACKED, &ticket);
   free(blob);
   free(off);
   if (rc) return error_tuple(env, r->ctx, rc);

@@ -22,6 +22,7 @@ EGM_E_NOTFOUND = -6
 
 EGM_MODE_TRIE = 0
 EGM_MODE_ROUTES = 1
+EGM_RESULT_PACKED = 0x100   # mode flag: the packed host result (u32 rows, 3-byte ids)
 EGM_RMODE_MATCH = 0
 EGM_RMODE_DISPATCH = 1
 
@@ -57,7 +58,8 @@ class egm_delta(C.Structure):
 class egm_result(C.Structure):
     _fields_ = [("n_topics", C.c_uint32), ("n_ids", C.c_uint64), ("counts", _u32p), ("row_ptr", _u64p),
                 ("ids", _u32p), ("flags", _u8p), ("epoch", C.c_uint64), ("visited", C.c_uint64),
-                ("n_heavy", C.c_uint32), ("n_error", C.c_uint32)]
+                ("n_heavy", C.c_uint32), ("n_error", C.c_uint32),
+                ("id_bytes", C.c_uint32), ("row32", _u32p), ("ids24", _u8p)]
 
 
 class egm_delivery(C.Structure):

@@ -24,7 +24,7 @@ LIB = os.path.join(HERE, "libemqx_gpu_match.so")
 SYNTH = os.path.join(HERE, "libegm_synth.so")
 ORACLE = os.path.join(ROOT, "oracle", "liboracle_trie.so")
 
-HEADERS = [os.path.join(CSRC, f) for f in ("egm_common.h", "egm_table.h", "egm_kernels.h", "egm_dma.h")] + [
+HEADERS = [os.path.join(CSRC, f) for f in ("egm_common.h", "egm_table.h", "egm_kernels.h", "egm_dma.h", "egm_pack.h")] + [
     os.path.join(ROOT, "include", "emqx_gpu_match.h")]
 
 
@@ -53,12 +53,13 @@ def _run(cmd, verbose):
 def build_lib(verbose=False, force=False) -> str:
     os.makedirs(BUILD, exist_ok=True)
     objs = []
-    hip_src = os.path.join(CSRC, "egm_kernels.hip")
-    o = os.path.join(BUILD, "egm_kernels.o")
-    if force or _stale(o, [hip_src] + HEADERS):
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result", "-Wno-unused-value",
-              "-c", hip_src, "-o", o], verbose)
-    objs.append(o)
+    for name in ("egm_kernels.hip", "egm_pack.hip"):
+        hip_src = os.path.join(CSRC, name)
+        o = os.path.join(BUILD, name.replace(".hip", ".o"))
+        if force or _stale(o, [hip_src] + HEADERS):
+            _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result",
+                  "-Wno-unused-value", "-c", hip_src, "-o", o], verbose)
+        objs.append(o)
     for name in ("egm_table.cpp", "egm_bulk.cpp", "egm_capi.cpp", "egm_retain.cpp", "egm_dma.cpp"):
         src = os.path.join(CSRC, name)
         o = os.path.join(BUILD, name.replace(".cpp", ".o"))

@@ -24,6 +24,7 @@
 #include "../../include/emqx_gpu_match.h"
 #include "egm_alloc.h"
 #include "egm_dma.h"
+#include "egm_pack.h"
 #include "egm_kernels.h"
 #include "egm_table.h"
 
@@ -98,10 +99,12 @@ struct PipeSlot {
   uint32_t gen = 0;        // bumped at every submit: part of the ticket, so a stale ticket is refused
   uint32_t n = 0;
   int mode = 0;
+  bool want_packed = false;   // submitted with EGM_RESULT_PACKED
+  bool packed = false;        // this launch's result is packed (egm_pack.h): row32 + 3-byte ids
   uint64_t bytes = 0, maxlen = 0, cap = 0;
   uint64_t o_off = 0;      // the offsets' place after the blob in h_in and d_in (one H2D copy)
   PinBuf h_in, h_out, h_stats;
-  DevBuf d_in, d_row, d_ids, d_flags;
+  DevBuf d_in, d_row, d_ids, d_flags, d_row32, d_pk;
   // ev_in: staged input copied in; ev_match: matched (stream s); ev_done: the
   // CSR in h_out (the copier's D2H copies, or the copy-out kernel)
   hipEvent_t ev_in = nullptr, ev_match = nullptr, ev_done = nullptr;
@@ -209,6 +212,7 @@ struct Epoch {
   int slot = 0;
   uint64_t id = 0;
   uint64_t n_filters = 0, n_nodes = 0, n_edges = 0, n_words = 0, bytes = 0;
+  uint64_t fid_end = 0;   // every filter id of the epoch is below this (packed results: < 2^24)
 };
 
 struct CommitStats {
@@ -608,6 +612,7 @@ static int commit_locked(egm_ctx* c, uint64_t* epoch) {
   ep->n_nodes = t.n_nodes_live();
   ep->n_edges = t.n_edges();
   ep->n_words = t.n_words();
+  ep->fid_end = t.next_fid();
   ep->bytes = S.bytes();
   ep->id = c->next_epoch++;
   c->cur = ep;
@@ -1262,6 +1267,13 @@ static void ptrace(const char* what, const void* slot, uint64_t gen) {
 // Enqueue one staged batch of slot S: H2D on the copy stream, the match on
 // the context stream once the input is in, then the batch's flags and
 // counters copied out in stream order (the next batch reuses the workspace).
+// Packed parts' copy sizes rounded up to EGM_PIPE_ALIGN bytes (A/B; the
+// device and pinned buffers keep that much slack).
+#ifndef EGM_PIPE_ALIGN
+#define EGM_PIPE_ALIGN 1
+#endif
+static uint64_t pipe_round(uint64_t b) { return (b + EGM_PIPE_ALIGN - 1) / EGM_PIPE_ALIGN * EGM_PIPE_ALIGN; }
+
 static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   hipError_t e;
   hipStream_t s = c->stream;
@@ -1282,7 +1294,7 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   int r = ensure_work(c, W, S.n, S.bytes, S.cap, S.maxlen + 1);
   if (r) return r;
   if ((e = S.d_row.ensure((n + 1) * 8)) != hipSuccess) return c->hip_fail(e, "pipe row");
-  if ((e = S.d_ids.ensure((S.cap + 1) * 4)) != hipSuccess) return c->hip_fail(e, "pipe ids");
+  if ((e = S.d_ids.ensure((S.cap + 4) * 4)) != hipSuccess) return c->hip_fail(e, "pipe ids");   // (+4: the packer reads groups of 4)
   if ((e = S.d_flags.ensure(n + 8)) != hipSuccess) return c->hip_fail(e, "pipe flags");
   if ((e = S.h_stats.ensure(sizeof(MatchStats))) != hipSuccess) return c->hip_fail(e, "pipe stats");
   const OutLayout ol = out_layout(n, S.cap);
@@ -1295,6 +1307,18 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
     return r;
   }
   c->last_pending = false;   // this batch's counters travel with the slot
+  // the packed form (EGM_RESULT_PACKED, egm_pack.h): large batches on the copier's path whose
+  // epoch's filter ids fit 24 bits; the packer runs on the match's stream, before ev_match
+  S.packed = S.want_packed && !small && !pipe_copy_kernel() && ep->fid_end <= (1ull << 24) && S.cap < (1ull << 31);
+  if (S.packed) {
+    if ((e = S.d_row32.ensure(pipe_round((n + 1) * 4))) != hipSuccess ||
+        (e = S.d_pk.ensure(pipe_round(S.cap * 3 + 16))) != hipSuccess ||
+        (e = launch_pack_result(S.d_row.as<uint64_t>(), (uint32_t)n, S.d_ids.as<uint32_t>(), S.cap,
+                                S.d_row32.as<uint32_t>(), S.d_pk.as<uint8_t>(), s)) != hipSuccess) {
+      ws_done(W, s);
+      return c->hip_fail(e, "pipe pack");
+    }
+  }
   if (small) {
     // A small batch (the Erlang batcher's: 4096 by default) is latency-bound,
     // not bandwidth-bound: its result goes to pinned memory by a copy-out
@@ -1369,26 +1393,31 @@ static void copier_main(egm_ctx* c) {
     const MatchStats st = *(const MatchStats*)S.h_stats.p;   // copied before ev_match, in stream order
     bool failed = e != hipSuccess;   // the match itself failed: nothing is copied, the waiter reports EGM_E_DEVICE
     if (e == hipSuccess && !st.overflow && !st.guard && dma) {
-      const uint64_t n = S.n, nids = std::min<uint64_t>(st.total_ids, S.cap), half = (nids / 2 + 3) & ~3ull;
-      const uint64_t h1 = std::min(half, nids);
+      const uint64_t n = S.n, nids = std::min<uint64_t>(st.total_ids, S.cap);
+      // the ids in two halves (two SDMA queues), then row starts and flags; packed: 3 bytes per id, u32 rows
+      const uint64_t ib0 = nids * (S.packed ? 3 : 4), ib = S.packed ? pipe_round(ib0) : ib0;
+      const uint64_t h1 = std::min<uint64_t>((ib / 2 + 15) & ~15ull, ib);
       const OutLayout ol = out_layout(n, S.cap);
       uint8_t* h = (uint8_t*)S.h_out.p;
-      const DmaPart parts[4] = {{h + ol.o_ids, S.d_ids.p, h1 * 4},
-                                {h + ol.o_ids + h1 * 4, (const uint8_t*)S.d_ids.p + h1 * 4, (nids - h1) * 4},
-                                {h + ol.o_row, S.d_row.p, (n + 1) * 8},
+      const uint8_t* di = S.packed ? S.d_pk.as<uint8_t>() : S.d_ids.as<uint8_t>();
+      const uint64_t rb = S.packed ? pipe_round((n + 1) * 4) : (n + 1) * 8;
+      const DmaPart parts[4] = {{h + ol.o_ids, di, h1},
+                                {h + ol.o_ids + h1, di + h1, ib - h1},
+                                {h + ol.o_row, S.packed ? S.d_row32.p : S.d_row.p, rb},
                                 {h + ol.o_fl, S.d_flags.p, n}};
       failed = !dma_copy_d2h(dma, parts, 4);
     } else if (e == hipSuccess && !st.overflow && !st.guard) {
-      const uint64_t n = S.n, nids = std::min<uint64_t>(st.total_ids, S.cap), half = (nids / 2 + 3) & ~3ull;
+      const uint64_t n = S.n, nids = std::min<uint64_t>(st.total_ids, S.cap);
+      const uint64_t ib = nids * (S.packed ? 3 : 4), h1 = std::min<uint64_t>((ib / 2 + 15) & ~15ull, ib);
       const OutLayout ol = out_layout(n, S.cap);
       uint8_t* h = (uint8_t*)S.h_out.p;
-      hipMemcpyAsync(h + ol.o_row, S.d_row.p, (n + 1) * 8, hipMemcpyDeviceToHost, c->d2h_stream);
+      const uint8_t* di = S.packed ? S.d_pk.as<uint8_t>() : S.d_ids.as<uint8_t>();
+      hipMemcpyAsync(h + ol.o_row, S.packed ? S.d_row32.p : S.d_row.p, (n + 1) * (S.packed ? 4 : 8),
+                     hipMemcpyDeviceToHost, c->d2h_stream);
       if (n) hipMemcpyAsync(h + ol.o_fl, S.d_flags.p, n, hipMemcpyDeviceToHost, c->d2h_stream);
-      const uint64_t h1 = std::min(half, nids);
-      if (h1) hipMemcpyAsync(h + ol.o_ids, S.d_ids.p, h1 * 4, hipMemcpyDeviceToHost, c->d2h_stream);
-      if (nids > h1) {
-        hipMemcpyAsync(h + ol.o_ids + h1 * 4, (const uint8_t*)S.d_ids.p + h1 * 4, (nids - h1) * 4,
-                       hipMemcpyDeviceToHost, c->d2h_stream2);
+      if (h1) hipMemcpyAsync(h + ol.o_ids, di, h1, hipMemcpyDeviceToHost, c->d2h_stream);
+      if (ib > h1) {
+        hipMemcpyAsync(h + ol.o_ids + h1, di + h1, ib - h1, hipMemcpyDeviceToHost, c->d2h_stream2);
         hipEventRecord(join, c->d2h_stream2);
         hipStreamWaitEvent(c->d2h_stream, join, 0);
       }
@@ -1515,7 +1544,8 @@ static int submit_locked(egm_ctx* c, std::unique_lock<std::recursive_mutex>& g, 
     }
   });
   S.n = n;
-  S.mode = mode;
+  S.mode = mode & ~EGM_RESULT_PACKED;
+  S.want_packed = (mode & EGM_RESULT_PACKED) != 0;
   S.bytes = bytes;
   S.maxlen = maxlen.load();
   S.cap = std::max<uint64_t>(std::max<uint64_t>((uint64_t)n * 4 + 1024, S.cap),
@@ -1537,8 +1567,13 @@ static int submit_locked(egm_ctx* c, std::unique_lock<std::recursive_mutex>& g, 
   return EGM_OK;
 }
 
+static bool pipe_mode_ok(int mode) {   // EGM_MODE_TRIE / EGM_MODE_ROUTES, optionally | EGM_RESULT_PACKED
+  const int m = mode & ~EGM_RESULT_PACKED;
+  return m == EGM_MODE_TRIE || m == EGM_MODE_ROUTES;
+}
+
 int egm_match_submit(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, int mode, uint64_t* ticket) {
-  if (!c || !ticket || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES)) return EGM_E_INVAL;
+  if (!c || !ticket || !pipe_mode_ok(mode)) return EGM_E_INVAL;
   if (n && (!off || !valid_offsets(off, n) || (!blob && off[n] > off[0]))) return EGM_E_INVAL;
   ptrace("submit-enter", nullptr, n);
   std::unique_lock<std::recursive_mutex> g(c->mu);
@@ -1614,8 +1649,15 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   res->n_topics = S.n;
   res->n_ids = nids;
   res->counts = (uint32_t*)(h + ol.o_cnt);
-  res->row_ptr = (uint64_t*)(h + ol.o_row);
-  res->ids = (uint32_t*)(h + ol.o_ids);
+  if (S.packed) {   // row starts as u32, ids as 3 bytes (egm_result_row / egm_result_id)
+    res->id_bytes = 3;
+    res->row32 = (const uint32_t*)(h + ol.o_row);
+    res->ids24 = h + ol.o_ids;
+  } else {
+    res->id_bytes = 4;
+    res->row_ptr = (uint64_t*)(h + ol.o_row);
+    res->ids = (uint32_t*)(h + ol.o_ids);
+  }
   res->flags = (uint8_t*)(h + ol.o_fl);
   res->epoch = S.epoch;
   res->visited = st.visited;
@@ -1626,12 +1668,13 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   std::atomic<uint32_t> heavy_n{0};
   {
     const uint64_t* rp = res->row_ptr;
+    const uint32_t* r32 = res->row32;
     uint32_t* cn = res->counts;
     const uint8_t* fl = res->flags;
     par_for(n, 1u << 17, [&](size_t lo, size_t hi) {
       uint32_t h = 0;
       for (size_t i = lo; i < hi; ++i) {
-        cn[i] = (uint32_t)(rp[i + 1] - rp[i]);
+        cn[i] = r32 ? r32[i + 1] - r32[i] : (uint32_t)(rp[i + 1] - rp[i]);
         h += (fl[i] & TF_HEAVY) ? 1u : 0u;
       }
       heavy_n += h;
@@ -1639,7 +1682,7 @@ int egm_match_wait(egm_ctx* c, uint64_t ticket, egm_result** out) {
   }
   const uint32_t heavy = heavy_n.load();
   g.lock();
-  if (res->row_ptr[n] != nids) return done(c->fail(EGM_E_DEVICE, "row_ptr total mismatch"));
+  if (egm_result_row(res, (uint32_t)n) != nids) return done(c->fail(EGM_E_DEVICE, "row_ptr total mismatch"));
   res->n_heavy = heavy;
   hdr->magic = RES_PIPE;
   hdr->owner = c;
@@ -1680,7 +1723,7 @@ int egm_match_cancel(egm_ctx* c, uint64_t ticket) {
 // "pipeline full": they take extra slots, then wait for one to be released.
 int egm_match_batch(egm_ctx* c, const uint8_t* blob, const uint32_t* off, uint32_t n, int mode,
                     egm_result** out) {
-  if (!c || !out || (mode != EGM_MODE_TRIE && mode != EGM_MODE_ROUTES)) return EGM_E_INVAL;
+  if (!c || !out || !pipe_mode_ok(mode)) return EGM_E_INVAL;
   *out = nullptr;
   if (n && (!off || !valid_offsets(off, n) || (!blob && off[n] > off[0]))) return EGM_E_INVAL;
   uint64_t t = 0;
@@ -2072,6 +2115,8 @@ int egm_fanout_device_compact(egm_ctx* c, const uint64_t* d_mrow, const uint32_t
 int egm_fanout_batch(egm_ctx* c, const egm_result* m, egm_delivery** out) {
   if (!c || !m || !out) return EGM_E_INVAL;
   *out = nullptr;
+  if (!m->row_ptr || (m->n_ids && !m->ids))   // a packed result (EGM_RESULT_PACKED) is not taken here
+    return c->fail(EGM_E_INVAL, "egm_fanout_batch takes the plain result form (match without EGM_RESULT_PACKED)");
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (set_device(c)) return EGM_E_DEVICE;
   hipStream_t s = c->stream;

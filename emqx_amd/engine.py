@@ -47,6 +47,7 @@ class MatchResult:
     visited: int
     n_heavy: int
     n_error: int
+    id_bytes: int = 4     # 3: the batch crossed PCIe in the packed form (EGM_RESULT_PACKED)
 
     def row(self, i: int) -> np.ndarray:
         return self.ids[self.row_ptr[i]: self.row_ptr[i + 1]]
@@ -54,6 +55,23 @@ class MatchResult:
     @property
     def counts(self) -> np.ndarray:
         return np.diff(self.row_ptr).astype(np.uint32)
+
+
+def _result_of(r) -> "MatchResult":
+    """Copy an egm_result out of the library's memory, either form: plain
+    (u64 row_ptr, u32 ids) or packed (u32 row32, 3-byte ids24; EGM_RESULT_PACKED)."""
+    n, nid = int(r.n_topics), int(r.n_ids)
+    if int(r.id_bytes) == 3:
+        row = np.ctypeslib.as_array(r.row32, shape=(n + 1,)).astype(np.uint64)
+        b = np.ctypeslib.as_array(r.ids24, shape=(3 * nid,)) if nid else np.zeros(0, np.uint8)
+        b = b.reshape(nid, 3).astype(np.uint32)
+        ids = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
+    else:
+        row = np.ctypeslib.as_array(r.row_ptr, shape=(n + 1,)).copy()
+        ids = np.ctypeslib.as_array(r.ids, shape=(nid,)).copy() if nid else np.zeros(0, np.uint32)
+    fl = np.ctypeslib.as_array(r.flags, shape=(n,)).copy() if n else np.zeros(0, np.uint8)
+    return MatchResult(row, ids.astype(np.uint32), fl, int(r.epoch), int(r.visited), int(r.n_heavy), int(r.n_error),
+                       int(r.id_bytes))
 
 
 class GpuMatcher:
@@ -170,17 +188,13 @@ class GpuMatcher:
                 self.lib.egm_result_free(res)
             self._check(rc, "egm_match_batch")
         try:
-            r = res.contents
-            nid = int(r.n_ids)
-            row = np.ctypeslib.as_array(r.row_ptr, shape=(n + 1,)).copy()
-            ids = np.ctypeslib.as_array(r.ids, shape=(nid,)).copy() if nid else np.zeros(0, np.uint32)
-            fl = np.ctypeslib.as_array(r.flags, shape=(n,)).copy() if n else np.zeros(0, np.uint8)
-            return MatchResult(row, ids, fl, int(r.epoch), int(r.visited), int(r.n_heavy), int(r.n_error))
+            return _result_of(res.contents)
         finally:
             self.lib.egm_result_free(res)
 
     def submit(self, blob: np.ndarray, off: np.ndarray, mode: int = L.EGM_MODE_TRIE) -> int:
-        """Queue a host batch on the pipeline (staged in pinned memory at once)."""
+        """Queue a host batch on the pipeline (staged in pinned memory at once).
+        mode may carry L.EGM_RESULT_PACKED (the packed result form)."""
         off = np.ascontiguousarray(off, dtype=np.uint32)
         t = C.c_uint64()
         self._check(self.lib.egm_match_submit(self.ctx, _ptr(blob), _ptr(off), len(off) - 1, mode, C.byref(t)),
@@ -199,12 +213,7 @@ class GpuMatcher:
         try:
             if not copy:
                 return None
-            r = res.contents
-            n, nid = int(r.n_topics), int(r.n_ids)
-            row = np.ctypeslib.as_array(r.row_ptr, shape=(n + 1,)).copy()
-            ids = np.ctypeslib.as_array(r.ids, shape=(nid,)).copy() if nid else np.zeros(0, np.uint32)
-            fl = np.ctypeslib.as_array(r.flags, shape=(n,)).copy() if n else np.zeros(0, np.uint8)
-            return MatchResult(row, ids, fl, int(r.epoch), int(r.visited), int(r.n_heavy), int(r.n_error))
+            return _result_of(res.contents)
         finally:
             self.lib.egm_result_free(res)
 

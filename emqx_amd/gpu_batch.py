@@ -314,7 +314,7 @@ class BatchServer:
         try:
             extra = self.overlay.filters() if self.overlay is not None else []   # before the submit (step 2)
             blob, off = pack_strings(list(topics))
-            t = nif.submit(blob, off, L.EGM_MODE_TRIE)
+            t = nif.submit(blob, off, L.EGM_MODE_TRIE | L.EGM_RESULT_PACKED)   # as the NIF's submit/3
             res = nif.wait(t)
             out = []
             for k, tp in enumerate(topics):

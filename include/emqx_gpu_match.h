@@ -89,7 +89,30 @@ typedef struct egm_result {
   uint64_t visited;    /* NFA states expanded (instrumentation)                     */
   uint32_t n_heavy;    /* topics routed through the heavy kernel                    */
   uint32_t n_error;    /* topics flagged EGM_TF_ERROR                               */
+  /* The packed form (a pipeline batch submitted with EGM_RESULT_PACKED, when
+     every filter id of its epoch is below 2^24; round 6): id_bytes == 3,
+     row_ptr and ids are NULL, row32 holds the row starts as u32 and ids24 the
+     ids as 3-byte little-endian values — 3 bytes per id and 4 per row start
+     cross PCIe instead of 4 and 8.  Otherwise id_bytes == 4 and row32/ids24
+     are NULL.  Read either form with egm_result_row()/egm_result_id(). */
+  uint32_t id_bytes;
+  const uint32_t* row32;  /* [n_topics+1] (packed form)                             */
+  const uint8_t* ids24;   /* [3 * n_ids]  (packed form)                             */
 } egm_result;
+
+/* mode flag of egm_match_submit / egm_match_batch: the packed result form */
+#define EGM_RESULT_PACKED 0x100
+
+static inline uint64_t egm_result_row(const egm_result* r, uint32_t i) {
+  return r->row32 ? (uint64_t)r->row32[i] : r->row_ptr[i];
+}
+static inline uint32_t egm_result_id(const egm_result* r, uint64_t k) {
+  if (r->ids24) {
+    const uint8_t* p = r->ids24 + 3 * k;
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+  }
+  return r->ids[k];
+}
 
 typedef struct egm_delivery {
   uint32_t n_topics;
@@ -170,7 +193,13 @@ int egm_match_batch(egm_ctx* ctx, const uint8_t* topics_blob, const uint32_t* to
    egm_match_batch is submit + wait on a slot of its own: concurrent callers
    never see "pipeline full" (extra slots up to 16, then they queue for one).
    A walk guard trip (a kernel invariant failed, egm_last_guard) makes wait
-   return EGM_E_DEVICE; only a capacity overflow is retried. */
+   return EGM_E_DEVICE; only a capacity overflow is retried.
+   mode may carry EGM_RESULT_PACKED: a batch of more than 16 384 topics then
+   returns the packed form (egm_result.id_bytes == 3) when its epoch's filter
+   ids all fit 24 bits — the host path is bound by the PCIe link, and the
+   packed form moves ~28 % fewer bytes.  Smaller batches, and tables with
+   larger filter ids, return the plain form; read both with egm_result_row()
+   and egm_result_id(). */
 int egm_match_submit(egm_ctx* ctx, const uint8_t* topics_blob, const uint32_t* topic_offsets, uint32_t n_topics,
                      int mode, uint64_t* ticket);
 int egm_match_wait(egm_ctx* ctx, uint64_t ticket, egm_result** out);

@@ -20,9 +20,43 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def header_functions():
+    """The library's entry points the header declares (its static inline
+    helpers, egm_result_row/egm_result_id, are header-only)."""
     src = open(os.path.join(ROOT, "include", "emqx_gpu_match.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(egm_[a-z_]+)\s*\(", src)))
+    inline = set(re.findall(r"static\s+inline\s+[\w\s\*]+?\b(egm_[a-z_0-9]+)\s*\(", src))
+    return sorted(set(re.findall(r"\b(egm_[a-z_0-9]+)\s*\(", src)) - inline)
+
+
+def test_packed_result_helpers_decode_both_forms(tmp_path):
+    """egm_result_row / egm_result_id (include/emqx_gpu_match.h) read the plain
+    and the packed (EGM_RESULT_PACKED: u32 rows, 3-byte ids) result forms alike."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc missing")
+    c = tmp_path / "t.c"
+    c.write_text(r"""
+#include <stdio.h>
+#include "emqx_gpu_match.h"
+int main(void) {
+  uint64_t row[3] = {0, 2, 3};
+  uint32_t ids[3] = {7, 0xFFFFFE, 65536};
+  uint32_t row32[3] = {0, 2, 3};
+  uint8_t pk[9] = {7, 0, 0, 0xFE, 0xFF, 0xFF, 0, 0, 1};
+  egm_result a = {0}, b = {0};
+  a.n_topics = b.n_topics = 2; a.n_ids = b.n_ids = 3;
+  a.row_ptr = row; a.ids = ids; a.id_bytes = 4;
+  b.row32 = row32; b.ids24 = pk; b.id_bytes = 3;
+  for (uint32_t i = 0; i <= 2; ++i) if (egm_result_row(&a, i) != egm_result_row(&b, i)) return 1;
+  for (uint64_t k = 0; k < 3; ++k) if (egm_result_id(&a, k) != egm_result_id(&b, k)) return 2;
+  return 0;
+}
+""")
+    exe = tmp_path / "t"
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{os.path.join(ROOT, 'include')}", str(c), "-o", str(exe)],
+                   check=True)
+    assert subprocess.run([str(exe)]).returncode == 0
 
 
 def test_library_exports_every_header_symbol():

@@ -267,6 +267,43 @@ def test_pipeline_deep_in_flight_exact(gm):
         m.close()
 
 
+def test_pipeline_packed_results_exact(gm):
+    """EGM_RESULT_PACKED (round 6, egm_pack.hip): batches past the small-batch
+    size come back as u32 rows + 3-byte ids, several in flight, every one equal
+    to the plain form; a small batch, and a table whose filter ids reach 2^24,
+    come back plain (id_bytes 4) — equal too."""
+    f, t = synth.config("c2", n_filters=200_000, n_topics=120_000)
+    gm.build(f.blob, f.off)
+    parts = [t.subset(np.arange(k * 30_000, (k + 1) * 30_000)) for k in range(4)]
+    want = [gm.match(p.blob, p.off, L.EGM_MODE_ROUTES) for p in parts]
+    assert want[0].id_bytes == 4 and int(want[0].row_ptr[-1]) > 5 * 30_000
+    from collections import deque
+    inflight = deque()
+    for r in range(8):
+        j = r % 4
+        inflight.append((j, gm.submit(parts[j].blob, parts[j].off, L.EGM_MODE_ROUTES | L.EGM_RESULT_PACKED)))
+        while len(inflight) >= 3 or (r == 7 and inflight):
+            jj, tk = inflight.popleft()
+            got = gm.wait(tk)
+            assert got.id_bytes == 3
+            assert np.array_equal(got.row_ptr, want[jj].row_ptr)
+            assert np.array_equal(got.ids, want[jj].ids)   # the same device rows, only narrowed
+            assert np.array_equal(got.flags, want[jj].flags)
+    small = t.subset(np.arange(0, 4_096))
+    ws = gm.match(small.blob, small.off, L.EGM_MODE_ROUTES)
+    gs = gm.wait(gm.submit(small.blob, small.off, L.EGM_MODE_ROUTES | L.EGM_RESULT_PACKED))
+    assert gs.id_bytes == 4 and np.array_equal(gs.row_ptr, ws.row_ptr)
+    assert np.array_equal(canonical(gs.row_ptr, gs.ids), canonical(ws.row_ptr, ws.ids))
+    # filter ids past 24 bits: the plain form
+    ids = np.arange(f.n, dtype=np.uint32) + np.uint32((1 << 24) - 1000)
+    gm.build(f.blob, f.off, ids)
+    wl = gm.match(parts[0].blob, parts[0].off, L.EGM_MODE_ROUTES)
+    gl = gm.wait(gm.submit(parts[0].blob, parts[0].off, L.EGM_MODE_ROUTES | L.EGM_RESULT_PACKED))
+    assert gl.id_bytes == 4 and int(wl.ids.max()) >= (1 << 24) - 1000
+    assert np.array_equal(gl.row_ptr, wl.row_ptr)
+    assert np.array_equal(canonical(gl.row_ptr, gl.ids), canonical(wl.row_ptr, wl.ids))
+
+
 def test_pipeline_tickets_are_generational_and_cancellable(gm):
     """a ticket carries a generation (a stale or repeated ticket is
     refused, never answered with another batch's result) and can be given up

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--filters", type=int, default=None)
     ap.add_argument("--batch", type=int, default=1_000_000)
     ap.add_argument("--batches", type=int, default=40)
+    ap.add_argument("--packed", action="store_true", help="EGM_RESULT_PACKED: u32 rows + 3-byte ids (the NIF's form)")
     a = ap.parse_args()
     from emqx_amd import _lib as L
     from emqx_amd import synth
@@ -35,7 +36,7 @@ def main():
     halves = [t.subset(np.arange(0, a.batch)), t.subset(np.arange(a.batch, 2 * a.batch))]
     gm = GpuMatcher(0, max_batch=a.batch)
     gm.build(f.blob, f.off)
-    mode = L.EGM_MODE_ROUTES
+    mode = L.EGM_MODE_ROUTES | (L.EGM_RESULT_PACKED if a.packed else 0)
     # warm up: create and size the pipeline slots the deepest phase uses
     tk = [gm.submit(halves[k % 2].blob, halves[k % 2].off, mode) for k in range(4)]
     for x in tk:
@@ -63,12 +64,13 @@ def main():
         dt = time.perf_counter() - t0
         out[f"in_flight_{depth}"] = {"topics_per_s": a.batch * a.batches / dt, "ms_per_batch": dt / a.batches * 1e3,
                                      "ids_per_batch": ids / a.batches,
-                                     "result_bytes_per_batch": ids / a.batches * 4 + (a.batch + 1) * 8 + a.batch,
+                                     "result_bytes_per_batch": (ids / a.batches * 3 + (a.batch + 1) * 4 + a.batch) if a.packed
+                                     else (ids / a.batches * 4 + (a.batch + 1) * 8 + a.batch),
                                      "input_bytes_per_batch": int(halves[0].off[-1]) + 4 * (a.batch + 1),
                                      "submit_ms": t_sub / a.batches * 1e3, "wait_ms": t_wait / a.batches * 1e3}
     gm.close()
     line = {"what": "host_e2e: host topic blob -> host CSR (egm_match_submit/egm_match_wait, pinned staging)",
-            "config": a.config, "filters": f.n, "batch": a.batch, "batches": a.batches, **out}
+            "config": a.config, "filters": f.n, "batch": a.batch, "batches": a.batches, "packed": a.packed, **out}
     print(json.dumps(line), flush=True)
 
 

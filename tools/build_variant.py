@@ -19,9 +19,11 @@ tag, flags = sys.argv[1], sys.argv[2:]
 out = os.path.join(B.HERE, f"libemqx_gpu_match_{tag}.so")
 bdir = f"/tmp/egm_var_{tag}"
 os.makedirs(bdir, exist_ok=True)
-objs = [os.path.join(bdir, "egm_kernels.o")]
-B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
-        "-Wno-unused-value", *flags, "-c", os.path.join(B.CSRC, "egm_kernels.hip"), "-o", objs[0]], True)
+objs = []
+for name in ("egm_kernels.hip", "egm_pack.hip"):
+    objs.append(os.path.join(bdir, name.replace(".hip", ".o")))
+    B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
+            "-Wno-unused-value", *flags, "-c", os.path.join(B.CSRC, name), "-o", objs[-1]], True)
 for name in ("egm_table.cpp", "egm_bulk.cpp", "egm_capi.cpp", "egm_retain.cpp", "egm_dma.cpp"):
     o = os.path.join(bdir, name.replace(".cpp", ".o"))
     B._run(["g++", "-O3", "-fPIC", "-std=c++17", "-pthread", "-D__HIP_PLATFORM_AMD__", f"-I{B.ROCM}/include", *flags,

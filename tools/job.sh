@@ -95,6 +95,11 @@ for step in "$@"; do
       EGM_PIPE_TRACE=1 run btrace 300 python tools/batch_trace.py 4096 200
       run btrace_k 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$R/gpurun_out/${TAG}_btrace_k" -o run --output-format csv -- python tools/batch_trace.py 4096 200 ;;
     host_ptrace) EGM_PIPE_TRACE=1 run host_ptrace 600 python tools/bench_host.py ;;   # pipeline events on stderr
+    hostpk) run hostpk 600 python tools/bench_host.py --packed ;;   # the packed result form (EGM_RESULT_PACKED)
+    hostpk_ptrace) EGM_PIPE_TRACE=1 run hostpk_ptrace 600 python tools/bench_host.py --packed --batches 12 ;;
+    hostpk_*)  # the packed host path on variant V
+      v=${step#hostpk_}
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 python tools/bench_host.py --packed ;;
     host_hip) EGM_PIPE_COPY=hip run host_hip 600 python tools/bench_host.py ;;   # A/B: hipMemcpyAsync (blit kernel)
     host_k) EGM_PIPE_COPY=kernel run host_k 600 python tools/bench_host.py ;;   # A/B: the copy-out kernel
     host_trace)   # the host path's timeline: kernels and copies (no counters)
