@@ -1267,13 +1267,6 @@ static void ptrace(const char* what, const void* slot, uint64_t gen) {
 // Enqueue one staged batch of slot S: H2D on the copy stream, the match on
 // the context stream once the input is in, then the batch's flags and
 // counters copied out in stream order (the next batch reuses the workspace).
-// Packed parts' copy sizes rounded up to EGM_PIPE_ALIGN bytes (A/B; the
-// device and pinned buffers keep that much slack).
-#ifndef EGM_PIPE_ALIGN
-#define EGM_PIPE_ALIGN 1
-#endif
-static uint64_t pipe_round(uint64_t b) { return (b + EGM_PIPE_ALIGN - 1) / EGM_PIPE_ALIGN * EGM_PIPE_ALIGN; }
-
 static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   hipError_t e;
   hipStream_t s = c->stream;
@@ -1311,8 +1304,7 @@ static int pipe_launch(egm_ctx* c, PipeSlot& S) {
   // epoch's filter ids fit 24 bits; the packer runs on the match's stream, before ev_match
   S.packed = S.want_packed && !small && !pipe_copy_kernel() && ep->fid_end <= (1ull << 24) && S.cap < (1ull << 31);
   if (S.packed) {
-    if ((e = S.d_row32.ensure(pipe_round((n + 1) * 4))) != hipSuccess ||
-        (e = S.d_pk.ensure(pipe_round(S.cap * 3 + 16))) != hipSuccess ||
+    if ((e = S.d_row32.ensure((n + 1) * 4)) != hipSuccess || (e = S.d_pk.ensure(S.cap * 3 + 16)) != hipSuccess ||
         (e = launch_pack_result(S.d_row.as<uint64_t>(), (uint32_t)n, S.d_ids.as<uint32_t>(), S.cap,
                                 S.d_row32.as<uint32_t>(), S.d_pk.as<uint8_t>(), s)) != hipSuccess) {
       ws_done(W, s);
@@ -1395,12 +1387,11 @@ static void copier_main(egm_ctx* c) {
     if (e == hipSuccess && !st.overflow && !st.guard && dma) {
       const uint64_t n = S.n, nids = std::min<uint64_t>(st.total_ids, S.cap);
       // the ids in two halves (two SDMA queues), then row starts and flags; packed: 3 bytes per id, u32 rows
-      const uint64_t ib0 = nids * (S.packed ? 3 : 4), ib = S.packed ? pipe_round(ib0) : ib0;
-      const uint64_t h1 = std::min<uint64_t>((ib / 2 + 15) & ~15ull, ib);
+      const uint64_t ib = nids * (S.packed ? 3 : 4), h1 = std::min<uint64_t>((ib / 2 + 15) & ~15ull, ib);
       const OutLayout ol = out_layout(n, S.cap);
       uint8_t* h = (uint8_t*)S.h_out.p;
       const uint8_t* di = S.packed ? S.d_pk.as<uint8_t>() : S.d_ids.as<uint8_t>();
-      const uint64_t rb = S.packed ? pipe_round((n + 1) * 4) : (n + 1) * 8;
+      const uint64_t rb = (n + 1) * (S.packed ? 4 : 8);
       const DmaPart parts[4] = {{h + ol.o_ids, di, h1},
                                 {h + ol.o_ids + h1, di + h1, ib - h1},
                                 {h + ol.o_row, S.packed ? S.d_row32.p : S.d_row.p, rb},
