@@ -110,6 +110,8 @@ for step in "$@"; do
     s2) run s2 400 python $R/bench.py --steps 20 --warmup 3 --streams 2 --cpu-baseline off --host-e2e off --x-orders "a86,0" ;;
     orders4) run orders4 500 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off --x-orders "a86,68a8,8a86,a86,68a8,8a86,9a8" ;;
     orders5) run orders5 600 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off --x-orders "8a86,a886,88a6,8a95,6a88,7a87,8a86,7a96,8b75" ;;
+    orders7) run orders7 600 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off --x-orders "7764,4444,5542,4453,3355,7764,6622" ;;   # 16-bit keys: 2 sort passes (round 6)
+    orders8) run orders8 600 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off --x-orders "7764,8888,6a88,8a86,7764,9887,7864" ;;   # 32-bit keys: 4 sort passes (round 6)
     orders6) run orders6 600 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off --x-orders "8a86,a86,6864,8862,6666,7764,8a86" ;;   # 24-bit keys: 3 sort passes
     orders) run orders 400 python $R/bench.py --steps 10 --warmup 2 --cpu-baseline off --host-e2e off --x-orders "a86,0,a86/128,a86" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
