@@ -39,6 +39,10 @@ run() {
   local rc=$?
   echo "[$(date +%T)] $name rc=$rc"
   tail -n 4 "$log"
+  # a device fault surfaces as an ordinary Python exception (exit 1): stop there too
+  if grep -q -E "illegal memory access|hipErrorIllegalAddress|Memory access fault|HSA_STATUS_ERROR" "$log"; then
+    echo "FATAL: $name hit a GPU fault — stopping"; exit 99
+  fi
   case $rc in
     0|1|2|3|4|5) return 0 ;;
     *) echo "FATAL: $name exited $rc — stopping"; exit $rc ;;
