@@ -44,6 +44,88 @@ SHARD_THRESHOLD = 1024        # ?SHARD, emqx_broker_helper.erl:54
 STRATEGIES = ("random", "round_robin", "sticky", "hash", "hash_clientid", "hash_topic")
 
 
+class SharedSub:
+    """``emqx_shared_sub``'s member pick and its ack/nack redispatch
+    (apps/emqx/src/emqx_shared_sub.erl:120-134 ``dispatch/4``, :150-194
+    ``dispatch_per_qos``/``dispatch_with_ack``, :239-290 ``pick``/``do_pick``,
+    :390-397 ``is_active_sub``) over a group's member list; no GPU involved.
+
+    phash2 (ERTS) is replaced by crc32 and ``rand`` by a seeded
+    ``random.Random``: the member a hash or random pick chooses is not the
+    reference's (parity-unpinned); the retry chain is: a fresh pick
+    excludes the members that failed this delivery, a member that nacks (its
+    queue was full), is down or times out is added to them, and once every
+    member has failed one is picked from all of them and sent without an ack
+    (``retry``).  ``{error, no_subscribers}`` only for a group with no member.
+    """
+
+    def __init__(self, strategy: str = "random", seed: int = 0):
+        if strategy not in STRATEGIES:
+            raise ValueError(strategy)
+        self.strategy = strategy
+        self._rng = random.Random(seed)
+        self._rr: Dict[Tuple[bytes, bytes], int] = {}
+        self._sticky: Dict[Tuple[bytes, bytes], int] = {}
+
+    def _nth(self, key, strategy: str, source_topic: bytes, clientid: bytes, subs: List[int]) -> int:
+        """pick_subscriber/6 + do_pick_subscriber/6 (:268-290)."""
+        n = len(subs)
+        if n == 1:
+            return subs[0]
+        if strategy == "random":
+            return subs[self._rng.randrange(n)]
+        if strategy == "round_robin":
+            i = self._rr.get(key)
+            i = self._rng.randrange(n) if i is None else (i + 1) % n
+            self._rr[key] = i
+            return subs[i]
+        if strategy in ("hash", "hash_clientid"):
+            return subs[zlib.crc32(clientid) % n]
+        return subs[zlib.crc32(source_topic) % n]   # hash_topic
+
+    def _do_pick(self, key, strategy, source_topic, clientid, members, failed):
+        """do_pick/6 (:255-266): None = no subscriber; (type, member)."""
+        if not members:
+            return None
+        rest = [m for m in members if m not in failed]
+        if not rest:   # all of them failed: pick one anyway, sent without an ack
+            return "retry", self._nth(key, strategy, source_topic, clientid, members)
+        return "fresh", self._nth(key, strategy, source_topic, clientid, rest)
+
+    def pick(self, group: bytes, topic: bytes, members: List[int], source_topic: bytes = b"",
+             clientid: bytes = b"", failed: Sequence[int] = (), alive=lambda m: True):
+        """pick/6 (:239-253): (type, member) or None."""
+        key = (group, topic)
+        if self.strategy == "sticky":
+            cur = self._sticky.get(key)
+            if cur is not None and alive(cur) and cur not in failed:   # is_active_sub/2 (:390-391)
+                return "fresh", cur
+            got = self._do_pick(key, "random", source_topic, clientid, members,
+                                list(failed) + ([cur] if cur is not None else []))
+            if got is not None:
+                self._sticky[key] = got[1]
+            return got
+        return self._do_pick(key, self.strategy, source_topic, clientid, members, failed)
+
+    def dispatch(self, group: bytes, topic: bytes, members: List[int], source_topic: bytes = b"",
+                 clientid: bytes = b"", qos: int = 0, ack_enabled: bool = False,
+                 respond=lambda m: "ack", alive=lambda m: True):
+        """dispatch/4 (:123-134): -> (("ok", 1) | ("error", "no_subscribers"),
+        the member delivered to or None, the members that failed on the way).
+        ``respond(member)`` is the member session's answer to a delivery that
+        needs an ack (QoS 1/2 with ``shared_dispatch_ack_enabled``): "ack", or
+        "nack" / "down" / "timeout" (:173-190)."""
+        failed: List[int] = []
+        while True:
+            got = self.pick(group, topic, members, source_topic, clientid, failed, alive)
+            if got is None:
+                return ("error", "no_subscribers"), None, failed
+            typ, m = got
+            if qos == 0 or typ == "retry" or not ack_enabled or respond(m) == "ack":   # dispatch_per_qos/4
+                return ("ok", 1), m, failed
+            failed.append(m)   # "Failed to dispatch to this sub, try next"
+
+
 class Broker:
     def __init__(self, router: Optional[Router] = None, device: int = 0, node: str = "local",
                  shared_strategy: str = "random", seed: int = 0, shards: int = 32):
@@ -58,9 +140,7 @@ class Broker:
         self.group_ids: Dict[bytes, int] = {}
         self.group_names: List[bytes] = []
         self.clientid: Dict[int, bytes] = {}
-        self._rng = random.Random(seed)
-        self._rr: Dict[Tuple[bytes, bytes], int] = {}
-        self._sticky: Dict[Tuple[bytes, bytes], int] = {}
+        self.share = SharedSub(shared_strategy, seed)
         self._shards = shards
         # the GPU subscriber table (egm_subs_*): built once, then kept by deltas
         self._built = False
@@ -292,34 +372,26 @@ class Broker:
 
     def _pick(self, group: bytes, flt: bytes, source_topic: bytes, clientid: bytes,
               members: Optional[List[int]] = None) -> Optional[int]:
-        """``pick/6`` + ``do_pick_subscriber/6`` (emqx_shared_sub.erl:239-290).
-
-        phash2 (ERTS) is replaced by crc32: the member a hash strategy picks is
-        therefore not the reference's (parity is at (filter, group) level,
-        SURVEY §8c); each strategy keeps its reference behaviour otherwise.
-        """
+        """One member of a group for a delivery without an ack (SharedSub.pick,
+        emqx_shared_sub.erl:239-290): ``publish_result`` passes the group's
+        live members (the DOWNs of dead ones already processed)."""
         mem = self.shared.get((group, flt)) if members is None else members
-        if not mem:
-            return None
-        n = len(mem)
-        key = (group, flt)
-        s = self.strategy
-        if n == 1:
-            return mem[0]
-        if s == "random":
-            return mem[self._rng.randrange(n)]
-        if s == "round_robin":
-            i = self._rr.get(key)
-            i = self._rng.randrange(n) if i is None else (i + 1) % n
-            self._rr[key] = i
-            return mem[i]
-        if s == "sticky":
-            cur = self._sticky.get(key)
-            if cur in mem:
-                return cur
-            cur = mem[self._rng.randrange(n)]
-            self._sticky[key] = cur
-            return cur
-        if s in ("hash", "hash_clientid"):
-            return mem[zlib.crc32(clientid) % n]
-        return mem[zlib.crc32(source_topic) % n]   # hash_topic
+        got = self.share.pick(group, flt, mem or [], source_topic, clientid, (), lambda m: m not in self.dead)
+        return None if got is None else got[1]
+
+    def dispatch_shared(self, group: bytes, flt: bytes, source_topic: bytes, clientid: bytes = b"", qos: int = 0,
+                        ack_enabled: bool = False, respond=None):
+        """``emqx_shared_sub:dispatch/3`` for one (filter, group) entry of the
+        fan-out, with the ack/nack redispatch (SharedSub.dispatch) over the
+        group's members as ?TAB holds them — a member whose process is gone
+        but not yet cleaned up answers an ack-requiring delivery with DOWN.
+        ``respond(member)`` overrides the live members' answers (default: ack)."""
+        members = self.shared.get((group, flt), [])
+
+        def answer(m):
+            if m in self.dead:
+                return "down"
+            return respond(m) if respond is not None else "ack"
+
+        return self.share.dispatch(group, flt, members, source_topic, clientid, qos, ack_enabled, answer,
+                                   lambda m: m not in self.dead)

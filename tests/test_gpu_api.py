@@ -149,6 +149,26 @@ def test_publish_result_share_and_forward():
     assert br.metrics["messages.dropped"] == 0   # a shared group's miss is not a drop
 
 
+def test_shared_dispatch_redispatches_on_nack_and_down():
+    """emqx_shared_sub:dispatch/4 through the broker mirror (Broker.dispatch_shared):
+    a (filter, group) entry from the GPU fan-out, a member that nacks or whose
+    process is down (not yet cleaned up) skipped for a QoS 1 delivery with
+    shared_dispatch_ack_enabled, {ok, 1} while the group has members."""
+    br = Broker(shared_strategy="round_robin")
+    for m in (20, 21, 22):
+        br.subscribe(b"$share/g/q/+", m)
+    got = br.publish_result(b"q/1")
+    assert got == [("share", b"q/+", ("ok", 1))]
+    br.kill(21)
+    for _ in range(6):
+        res, m, failed = br.dispatch_shared(b"g", b"q/+", b"q/1", qos=1, ack_enabled=True,
+                                            respond=lambda x: "nack" if x == 22 else "ack")
+        assert res == ("ok", 1) and m == 20 and set(failed) <= {21, 22}
+    res, m, failed = br.dispatch_shared(b"g", b"q/+", b"q/1", qos=0)
+    assert res == ("ok", 1) and m in (20, 21, 22) and failed == []   # QoS 0: a plain send, even to 21
+    assert br.dispatch_shared(b"none", b"q/+", b"q/1") == (("error", "no_subscribers"), None, [])
+
+
 def test_publish_result_random_vs_oracle():
     rng = random.Random(17)
     br = Broker(shared_strategy="random")
