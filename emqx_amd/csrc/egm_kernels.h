@@ -171,14 +171,16 @@ size_t scan_tiles(uint32_t n);
 // items of HBM stack per heavy wave for topics of up to max_levels levels
 uint32_t heavy_stack_items(uint64_t max_levels);
 int deep_grid_blocks(uint32_t n_topics);
-uint32_t walk_stage();   // WALK_STAGE: the most emits a flush record holds
+uint32_t walk_stage();       // the most emits a flush record holds (the larger pass's stage)
+uint32_t walk_stage_min();   // the smaller pass's stage: records of either pass hold more than this - 256
 // Record slab u32 for a batch of up to `ids` matched ids: every record carries
 // REC_IDS + EGM_REC_ALIGN - 1 u32 beyond its entries and holds at least flush_lim - 256 + 1 of
 // them (a flush is due once the next step could overfill the stage; the last
 // record of a chunk can be shorter: one per chunk), plus every wave's segment
 // tail.
 inline uint64_t rec_capacity(uint64_t ids, uint32_t n, uint32_t flush_lim, uint32_t grain) {
-  const uint64_t per = flush_lim > 256 ? flush_lim - 256 : 1;
+  const uint32_t fl = flush_lim < walk_stage_min() ? flush_lim : walk_stage_min();   // the shorter pass's records
+  const uint64_t per = fl > 256 ? fl - 256 : 1;
   const uint64_t chunks = walk_chunk_cap(n);
   // waves of any batch of up to n topics (their chunk counts are bounded by walk_chunk_cap)
   const uint64_t wc = walk_chunk_cap(n);

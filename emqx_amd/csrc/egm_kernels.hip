@@ -483,7 +483,12 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #define EGM_WALK_DEEP_MIN 12   // a chunk with a deeper topic is walked by the deep pass
 #endif
 #ifndef EGM_WALK_STAGE
-#define EGM_WALK_STAGE 320   // staged emits per flush record (5 B each in LDS; >= 4 emits x 64 lanes)
+#define EGM_WALK_STAGE 448   // staged emits per flush record, first pass (5 B each in LDS; >= 4 emits x 64 lanes;
+                             // 320 until round 6: the first pass is VGPR-bound at 16 waves per CU, so LDS had
+                             // room for longer records — fewer, longer runs for k_rec_burst)
+#endif
+#ifndef EGM_WALK_STAGE_DEEP
+#define EGM_WALK_STAGE_DEEP 320   // the deep pass's stage (LDS-bound: 448 would cost it a wave per CU)
 #endif
 #ifndef EGM_WALK_PAIRS
 #define EGM_WALK_PAIRS 0     // A/B: the first pass pops two items per lane per iteration
@@ -505,6 +510,9 @@ constexpr uint32_t WALK_STACK = EGM_WALK_STACK;
 constexpr uint32_t WALK_STACK_DEEP = EGM_WALK_STACK_DEEP;
 constexpr uint32_t DEEP_MIN = EGM_WALK_DEEP_MIN;
 constexpr uint32_t WALK_STAGE = EGM_WALK_STAGE;
+constexpr uint32_t WALK_STAGE_DEEP = EGM_WALK_STAGE_DEEP;
+constexpr uint32_t WALK_STAGE_MAX = WALK_STAGE > WALK_STAGE_DEEP ? WALK_STAGE : WALK_STAGE_DEEP;   // record readers
+constexpr uint32_t WALK_STAGE_MIN = WALK_STAGE < WALK_STAGE_DEEP ? WALK_STAGE : WALK_STAGE_DEEP;   // record sizing
 constexpr uint32_t WALK_WORDS = EGM_WALK_WORDS;
 // The pop bound (below) keeps room >= dmax after every iteration and a refill
 // fills the stack to at most 64 items, so the stack cannot overflow while
@@ -514,16 +522,17 @@ __host__ __device__ constexpr uint32_t light_dmax(uint32_t stack) {
   return (stack - 64) < WALK_WORDS ? (stack - 64) : WALK_WORDS;
 }
 static_assert(WALK_CHUNK == 64, "one topic per lane in the chunk prologue");
-static_assert(WALK_STAGE >= 256, "a step stages up to 4 emits x 64 lanes");
-static_assert(WALK_STAGE <= 0xFFFF, "a record's entry count and per-topic counts are 16-bit");
+static_assert(WALK_STAGE_MIN >= 256, "a step stages up to 4 emits x 64 lanes");
+static_assert(WALK_STAGE_MAX <= 0xFFFF, "a record's entry count and per-topic counts are 16-bit");
 static_assert(light_dmax(WALK_STACK) >= DEEP_MIN, "the first pass must take the chunks it does not hand on");
 static_assert(light_dmax(WALK_STACK_DEEP) >= 16, "stack too small");
 
-template <uint32_t STK>
+template <uint32_t STK, uint32_t STG>
 struct alignas(16) WaveLds {
+  static constexpr uint32_t STAGE = STG;
   uint4 stack[STK];
-  uint32_t stage_fid[WALK_STAGE];
-  uint8_t stage_t[WALK_STAGE];       // topic in chunk of the emit
+  uint32_t stage_fid[STG];
+  uint8_t stage_t[STG];              // topic in chunk of the emit
   uint32_t words[WALK_WORDS + 2];    // the sub-chunk's word ids, [topic][level] (+2: the unclamped
                                      // reads of the words at level + 1 and + 2, unused past a leaf)
   uint32_t tinfo[WALK_CHUNK];        // D | tflags << 24 | words at the fixed stride << 31
@@ -570,7 +579,7 @@ __device__ __forceinline__ void st_u32(uint32_t* p, uint32_t v) {
 template <class LDS>
 __device__ __forceinline__ void flush_stage(LDS& L, uint32_t nstage, uint32_t lane, const MatchWork& w,
                                             RecCursor& rc) {
-  constexpr uint32_t NQ = (WALK_STAGE + 63) / 64;
+  constexpr uint32_t NQ = (LDS::STAGE + 63) / 64;
   uint32_t fv[NQ], pv[NQ];   // fid; topic | rank inside the flush << 8
 #pragma unroll
   for (uint32_t r = 0; r < NQ; ++r) {
@@ -919,7 +928,8 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
   // probe continuations in the first pass only: the deep pass (C3) measured
   // 53.8 -> 55.2 ms with them, the first pass (C2) 8.20 -> 6.23 ms (round 6)
   constexpr bool PROBE_CONT = EGM_PROBE_CONT != 0 && (!DEEP || EGM_PROBE_CONT > 1);
-  __shared__ WaveLds<STK> L;
+  constexpr uint32_t STG = DEEP ? WALK_STAGE_DEEP : WALK_STAGE;
+  __shared__ WaveLds<STK, STG> L;
   const uint32_t lane = threadIdx.x;
   // the first pass walks every chunk, the deep pass the chunks the first handed on
   const uint32_t ct = w.ct;   // topics per chunk (lanes >= ct hold none)
@@ -990,7 +1000,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
     while (S > 1 && S * dmax > WALK_WORDS) S >>= 1;
     uint32_t nstage = 0;
     rc.nrec = 0;
-    const uint32_t flim = w.flush_lim;
+    const uint32_t flim = min(w.flush_lim, STG);   // this pass's stage (the host's limit is the larger one's)
     wave_sync();
     for (uint32_t sub = 0; sub < nt; sub += S) {
       const uint32_t end = min(sub + S, nt);
@@ -1565,7 +1575,7 @@ __global__ __launch_bounds__(64 * COMPACT_WAVES) void k_compact(const uint4* __r
 // contiguous run (measurement only) take 0.93 ms and no stores 0.46 ms: the
 // runs of ~5 ids per topic and record are what costs.
 constexpr int REC_WAVES = 4;
-constexpr uint32_t REC_IPL = (WALK_STAGE + 63) / 64;   // a record's ids, all loaded in one round
+constexpr uint32_t REC_IPL = (WALK_STAGE_MAX + 63) / 64;   // a record's ids, all loaded in one round
 struct RecLoad {
   uint64_t off;
   uint32_t hdr, cr;
@@ -1610,7 +1620,7 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
       if (next_dir) issue((uint64_t)(uint32_t)__shfl((int)roff, (int)(r + 1), 64) << 2, B);   // in flight now
       uint32_t tot;
       const uint32_t ex = wave_excl_scan(A.cr, lane, &tot);
-      if ((A.hdr & 0xFFFF0000u) != REC_TAG || (A.hdr & 0xFFFFu) != tot || tot > WALK_STAGE) {
+      if ((A.hdr & 0xFFFF0000u) != REC_TAG || (A.hdr & 0xFFFFu) != tot || tot > WALK_STAGE_MAX) {
         if (lane == 0) atomicOr(&stats->guard, GUARD_STACK);   // a broken directory or chain: a bug, reported
         break;
       }
@@ -1734,7 +1744,7 @@ __global__ __launch_bounds__(64 * REC_WAVES) __attribute__((amdgpu_waves_per_eu(
         }
         uint32_t tot;
         const uint32_t ex = wave_excl_scan(cr[b], lane, &tot);
-        if ((hdr[b] & 0xFFFF0000u) != REC_TAG || (hdr[b] & 0xFFFFu) != tot || tot > WALK_STAGE) {
+        if ((hdr[b] & 0xFFFF0000u) != REC_TAG || (hdr[b] & 0xFFFFu) != tot || tot > WALK_STAGE_MAX) {
           if (lane == 0) atomicOr(&stats->guard, GUARD_STACK);   // a broken directory or chain: a bug, reported
           broken = true;
           break;
@@ -1829,7 +1839,8 @@ int deep_grid_blocks(uint32_t n) {
 
 uint32_t heavy_stack_items(uint64_t max_levels) { return (uint32_t)(max_levels + 256); }
 
-uint32_t walk_stage() { return WALK_STAGE; }
+uint32_t walk_stage() { return WALK_STAGE_MAX; }
+uint32_t walk_stage_min() { return WALK_STAGE_MIN; }
 
 size_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 

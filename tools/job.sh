@@ -149,6 +149,9 @@ for step in "$@"; do
     abnp_*)   # A/B variant, single-stream steps only (rocprof averages over the timed launches alone)
       v=${step#abnp_}; v=${v%%.*}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_profnp_${step#abnp_}" -o run --output-format csv -- $B --steps 20 --warmup 3 --cpu-baseline off --host-e2e off --pipelined off ;;
+    c3np_*)   # C3 on variant V under rocprof stats (single-stream steps)
+      v=${step#c3np_}; v=${v%%.*}
+      EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "$step" 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_profc3_${step#c3np_}" -o run --output-format csv -- $B --config c3 --steps 5 --warmup 2 --cpu-baseline off --host-e2e off --pipelined off ;;
     abx_*)   # A/B variant, second sample (own log/prof names)
       v=${step#abx_}
       EGM_LIB=$R/emqx_amd/libemqx_gpu_match_$v.so run "abx_$v" 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_profx_$v" -o run --output-format csv -- $B --steps 10 --warmup 2 --cpu-baseline off --host-e2e off ;;
