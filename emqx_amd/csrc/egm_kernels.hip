@@ -483,9 +483,10 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #define EGM_WALK_DEEP_MIN 12   // a chunk with a deeper topic is walked by the deep pass
 #endif
 #ifndef EGM_WALK_STAGE
-#define EGM_WALK_STAGE 448   // staged emits per flush record, first pass (5 B each in LDS; >= 4 emits x 64 lanes;
+#define EGM_WALK_STAGE 480   // staged emits per flush record, first pass (5 B each in LDS; >= 4 emits x 64 lanes;
                              // 320 until round 6: the first pass is VGPR-bound at 16 waves per CU, so LDS had
-                             // room for longer records — fewer, longer runs for k_rec_burst)
+                             // room for longer records — fewer, longer runs for k_rec_burst; 448 / 480 / 512
+                             // with stack 304: 8.49 / 8.39 / 8.38 ms per step, profiles/r6_walk_stage_ab.jsonl)
 #endif
 #ifndef EGM_WALK_STAGE_DEEP
 #define EGM_WALK_STAGE_DEEP 320   // the deep pass's stage (LDS-bound: 448 would cost it a wave per CU)
@@ -1664,7 +1665,7 @@ __global__ __launch_bounds__(64 * REC_WAVES) void k_rec_rows(const uint32_t* __r
 // direct form keeps each chunk open for ~11 dependent rounds: 4.1 GB written
 // per C2 batch for 1.99 GB of ids, PMC r5g).
 #ifndef EGM_REC_BURST
-#define EGM_REC_BURST 8
+#define EGM_REC_BURST 7   // a C2 chunk's ids come in ~7 records of 480 (burst 8 at 8 ids per lane spills 44 B)
 #endif
 #ifndef EGM_REC_BITMAP
 #define EGM_REC_BITMAP 1   // ids placed through a bitmap of run starts (A/B: 0, the LDS search)
