@@ -39,7 +39,8 @@ constexpr int TOK_BLOCK = 256;
 #endif
 constexpr int TOK_LDS = EGM_TOK_LDS;
 #ifndef EGM_TOK_WORDS
-#define EGM_TOK_WORDS 2560   // words per tokenise block (7 B of LDS each; 40 KB per block -> 4 blocks per CU;
+#define EGM_TOK_WORDS 2560   // words per tokenise block (5 B of LDS each; 31.4 KB per block -> 5 blocks per CU,
+                             // 4 with round 5's 7 B: C2 0.892 -> 0.877 ms, C3 2.63 -> 2.58, gpurun_out r6al;
                              // 2048 made C3's segments of 128 depth-16 topics retry as two of 64)
 #endif
 constexpr int TOK_WORDS = EGM_TOK_WORDS;
@@ -249,11 +250,10 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
                                                         uint32_t* __restrict__ wid, uint32_t* __restrict__ lv,
                                                         uint8_t* __restrict__ tfl, WalkOrderOut wo) {
   __shared__ __attribute__((aligned(16))) uint32_t sw[TOK_LDS / 4 + 1];   // +1: lds_word reads one word past
-  __shared__ uint32_t wpos[TOK_WORDS];   // start | len << 16 (LDS byte index)
-  __shared__ uint16_t wlv[TOK_WORDS];    // level of the word in its topic (a segment holds < 2^16 words)
+  __shared__ uint32_t wpos[TOK_WORDS];   // start | len << 16 (LDS byte index); then the word's id (sorted batch)
   __shared__ uint8_t wtop[TOK_WORDS];    // topic within the segment
   __shared__ uint32_t tg[TOK_BLOCK];     // wid index of the topic's word 0 (a word's is tg + its level)
-  __shared__ uint32_t kw[TOK_BLOCK][KEY_LEVELS];   // the topic's first word ids (walk-order key)
+  __shared__ uint32_t tex[TOK_BLOCK];    // the topic's first word in the segment (a word's level is i - tex)
   __shared__ uint32_t tflag[TOK_BLOCK];   // TF_* flags | levels << 8
   __shared__ uint32_t wsum[TOK_BLOCK / 64];
   const uint32_t blk0 = blockIdx.x * TOK_BLOCK;
@@ -357,20 +357,17 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
           const uint32_t p = q + (__builtin_ctz(m) >> 3);
           m &= m - 1;
           wpos[ex + l] = ws | ((p - ws) << 16);
-          wlv[ex + l] = (uint16_t)l;
           wtop[ex + l] = (uint8_t)tid;
           ++l;
           ws = p + 1;
         }
       }
       wpos[ex + l] = ws | ((ts + len - ws) << 16);
-      wlv[ex + l] = (uint16_t)l;
+      tex[tid] = ex;
       wtop[ex + l] = (uint8_t)tid;
       tg[tid] = g;
       lv[t] = D;
     }
-#pragma unroll
-    for (uint32_t k = 0; k < KEY_LEVELS; ++k) kw[tid][k] = 0;
     __syncthreads();
 
     // ---- pass 3: hash + dictionary probe, lane per word ----
@@ -412,12 +409,12 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
         if (wo.key) {
           // sorted batch: a topic of <= FIX_WORDS levels is read only at the
           // fixed stride (its record's fixed bit), so wid[] is not written
-          const uint32_t tt = wtop[i], l = wlv[i];
-          if (l < KEY_LEVELS) kw[tt][l] = res[u];
+          const uint32_t tt = wtop[i], l = i - tex[tt];
+          wpos[i] = res[u];   // only this lane reads word i's position; the key reads the id back
           if ((tflag[tt] >> 8) <= FIX_WORDS) wo.wfix[(uint64_t)(t0 + tt) * FIX_WORDS + l] = res[u];
           else wid[tg[tt] + l] = res[u];
         } else {
-          wid[tg[wtop[i]] + wlv[i]] = res[u];
+          wid[tg[wtop[i]] + i - tex[wtop[i]]] = res[u];
         }
       }
     }
@@ -427,7 +424,7 @@ __global__ __launch_bounds__(TOK_BLOCK) void k_tokenise(DevTable tab, const uint
       if (wo.key) {
         uint32_t w4[KEY_LEVELS];
 #pragma unroll
-        for (uint32_t k = 0; k < KEY_LEVELS; ++k) w4[k] = kw[tid][k];
+        for (uint32_t k = 0; k < KEY_LEVELS; ++k) w4[k] = k < D ? wpos[tex[tid] + k] : 0u;
         wo.key[t] = (tflag[tid] & TF_SKIP) ? 0xFFFFFFFFu : walk_key(w4, D, wo.shape);   // padding sorts last
         wo.val[t] = sort_val(t, D, tflag[tid] & 0xFFu, D <= FIX_WORDS);
       }
