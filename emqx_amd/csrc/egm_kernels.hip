@@ -474,7 +474,7 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #define EGM_WALK_STACK 320   // items (16 B) per wave: chunks of up to DEEP_MIN levels
 #endif
 #ifndef EGM_WALK_STACK_DEEP
-#define EGM_WALK_STACK_DEEP 448   // items per wave of the deep pass (deeper chunks: C3's wide frontiers; 640 until r5)
+#define EGM_WALK_STACK_DEEP 504   // items per wave of the deep pass (deeper chunks: C3's wide frontiers; 640 until r5, 448 x 16 B until r6)
 #endif
 #ifndef EGM_WALK_DEEP_MIN
 #define EGM_WALK_DEEP_MIN 12   // a chunk with a deeper topic is walked by the deep pass
@@ -504,6 +504,17 @@ constexpr uint32_t LEVEL_MAX = (1u << ML_BITS) - 1;
 #ifndef EGM_WALK_WORDS
 #define EGM_WALK_WORDS 448   // staged topic word ids per wave (a chunk's topics, [topic][level])
 #endif
+#ifndef EGM_WALK_ITEM12
+#define EGM_WALK_ITEM12 0        // the first pass keeps 12 B per stack item (A/B)
+#endif
+#ifndef EGM_WALK_ITEM12_DEEP
+#define EGM_WALK_ITEM12_DEEP 1   // the deep pass keeps 12 B per stack item, the word re-read from the word stage:
+                                 // 504 items in 10 240 B, 16 waves per CU instead of 14 at 16 B x 448 (C3 deep
+                                 // walk 48.8 -> 45.4 ms, profiles/r6_walk_deep_item12_ab.jsonl)
+#endif
+#ifndef EGM_WALK_WORDS_DEEP
+#define EGM_WALK_WORDS_DEEP 448   // the deep pass's word stage (sub-chunks of S topics, S * dmax <= it)
+#endif
 constexpr uint32_t WALK_STACK = EGM_WALK_STACK;
 constexpr uint32_t WALK_STACK_DEEP = EGM_WALK_STACK_DEEP;
 constexpr uint32_t DEEP_MIN = EGM_WALK_DEEP_MIN;
@@ -512,26 +523,29 @@ constexpr uint32_t WALK_STAGE_DEEP = EGM_WALK_STAGE_DEEP;
 constexpr uint32_t WALK_STAGE_MAX = WALK_STAGE > WALK_STAGE_DEEP ? WALK_STAGE : WALK_STAGE_DEEP;   // record readers
 constexpr uint32_t WALK_STAGE_MIN = WALK_STAGE < WALK_STAGE_DEEP ? WALK_STAGE : WALK_STAGE_DEEP;   // record sizing
 constexpr uint32_t WALK_WORDS = EGM_WALK_WORDS;
+constexpr uint32_t WALK_WORDS_DEEP = EGM_WALK_WORDS_DEEP;
 // The pop bound (below) keeps room >= dmax after every iteration and a refill
 // fills the stack to at most 64 items, so the stack cannot overflow while
 // 64 + dmax <= the stack; the words of one topic must fit the word stage.
 // A chunk with a deeper topic goes to k_heavy before any of it is walked.
-__host__ __device__ constexpr uint32_t light_dmax(uint32_t stack) {
-  return (stack - 64) < WALK_WORDS ? (stack - 64) : WALK_WORDS;
+__host__ __device__ constexpr uint32_t light_dmax(uint32_t stack, uint32_t words) {
+  return (stack - 64) < words ? (stack - 64) : words;
 }
 static_assert(WALK_CHUNK == 64, "one topic per lane in the chunk prologue");
 static_assert(WALK_STAGE_MIN >= 256, "a step stages up to 4 emits x 64 lanes");
 static_assert(WALK_STAGE_MAX <= 0xFFFF, "a record's entry count and per-topic counts are 16-bit");
-static_assert(light_dmax(WALK_STACK) >= DEEP_MIN, "the first pass must take the chunks it does not hand on");
-static_assert(light_dmax(WALK_STACK_DEEP) >= 16, "stack too small");
+static_assert(light_dmax(WALK_STACK, WALK_WORDS) >= DEEP_MIN, "the first pass must take the chunks it does not hand on");
+static_assert(light_dmax(WALK_STACK_DEEP, WALK_WORDS_DEEP) >= 16, "stack too small");
 
-template <uint32_t STK, uint32_t STG>
+template <uint32_t STK, uint32_t STG, uint32_t WRD, bool N12>
 struct alignas(16) WaveLds {
   static constexpr uint32_t STAGE = STG;
-  uint4 stack[STK];
+  uint4 stack[N12 ? 1 : STK];        // items {node, meta, plus_child, word}
+  uint2 sxy[N12 ? STK : 1];          // 12-B items: {node, meta} ...
+  uint32_t sz[N12 ? STK : 1];        // ... and plus_child; the word is words[slot][level]
   uint32_t stage_fid[STG];
   uint8_t stage_t[STG];              // topic in chunk of the emit
-  uint32_t words[WALK_WORDS + 2];    // the sub-chunk's word ids, [topic][level] (+2: the unclamped
+  uint32_t words[WRD + 2];           // the sub-chunk's word ids, [topic][level] (+2: the unclamped
                                      // reads of the words at level + 1 and + 2, unused past a leaf)
   uint32_t tinfo[WALK_CHUNK];        // D | tflags << 24 | words at the fixed stride << 31
   uint32_t cnt[WALK_CHUNK];          // ids per topic, whole chunk
@@ -902,7 +916,7 @@ __device__ __forceinline__ const uint32_t* topic_words(const MatchWork& w, uint3
 //
 // Two passes: the first (DEEP = false, a 320-item stack, 17 waves per CU)
 // walks the chunks of up to DEEP_MIN levels and hands deeper ones to the
-// second (DEEP = true: a 448-item stack, 14 waves per CU), whose wider stack
+// second (DEEP = true: a 504-item stack of 12-B items, 16 waves per CU), whose wider stack
 // keeps the wave's pops full on deep, wide frontiers (C3: lane occupancy 0.39
 // -> 0.80) where the first pass's room bound would narrow it; a chunk deeper
 // than the deep pass takes goes to k_heavy.
@@ -927,7 +941,26 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
   // 53.8 -> 55.2 ms with them, the first pass (C2) 8.20 -> 6.23 ms (round 6)
   constexpr bool PROBE_CONT = EGM_PROBE_CONT != 0 && (!DEEP || EGM_PROBE_CONT > 1);
   constexpr uint32_t STG = DEEP ? WALK_STAGE_DEEP : WALK_STAGE;
-  __shared__ WaveLds<STK, STG> L;
+  constexpr uint32_t WRD = DEEP ? WALK_WORDS_DEEP : WALK_WORDS;
+  // (a continued probe keeps its line in z and its word is the one at its level: it fits 12 B too)
+  constexpr bool N12 = DEEP ? EGM_WALK_ITEM12_DEEP != 0 : EGM_WALK_ITEM12 != 0;
+  __shared__ WaveLds<STK, STG, WRD, N12> L;
+  auto st_put = [&](uint32_t i, const uint4& v) {
+    if constexpr (N12) {
+      L.sxy[i] = make_uint2(v.x, v.y);
+      L.sz[i] = v.z;
+    } else {
+      L.stack[i] = v;
+    }
+  };
+  auto st_get = [&](uint32_t i) -> uint4 {
+    if constexpr (N12) {
+      const uint2 a = L.sxy[i];
+      return make_uint4(a.x, a.y, L.sz[i], 0u);
+    } else {
+      return L.stack[i];
+    }
+  };
   const uint32_t lane = threadIdx.x;
   // the first pass walks every chunk, the deep pass the chunks the first handed on
   const uint32_t ct = w.ct;   // topics per chunk (lanes >= ct hold none)
@@ -975,7 +1008,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, d, 64));
     dmax = uni(dmax);
-    if (dmax > light_dmax(WALK_STACK_DEEP) || (w.debug & DEBUG_FORCE_HEAVY)) {   // the whole chunk goes to k_heavy
+    if (dmax > light_dmax(WALK_STACK_DEEP, WALK_WORDS_DEEP) || (w.debug & DEBUG_FORCE_HEAVY)) {   // the whole chunk goes to k_heavy
       if (lane == 0) {
         const uint32_t d = atomicAdd(&w.stats->n_deferred, 1u);
         w.deferred[d] = c;
@@ -995,7 +1028,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
     // only words at a variable offset need off[] (read by other lanes with a shuffle)
     const uint32_t gb = lane < nt ? (fixed ? my_t : off[my_t] + my_t) : 0u;
     uint32_t S = WALK_CHUNK;
-    while (S > 1 && S * dmax > WALK_WORDS) S >>= 1;
+    while (S > 1 && S * dmax > WRD) S >>= 1;
     uint32_t nstage = 0;
     rc.nrec = 0;
     const uint32_t flim = min(w.flush_lim, STG);   // this pass's stage (the host's limit is the larger one's)
@@ -1058,7 +1091,7 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
             }
           }
           const uint64_t b = __ballot(has);
-          if (has) L.stack[sp + mbcnt(b)] = it;
+          if (has) st_put(sp + mbcnt(b), it);
           sp += popc(b);
           const uint64_t be = __ballot(em);
           if (em) {
@@ -1094,16 +1127,20 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
         popped += take;
         Pend p, pb;
         p.act = lane < take_a;
-        p.it = L.stack[min(bi + lane, STK - 1)];   // unconditional: see issue()
+        p.it = st_get(min(bi + lane, STK - 1));   // unconditional: see issue()
         if (PAIRS) {
           pb.act = lane < take_b;
-          pb.it = L.stack[min(bi + 64 + lane, STK - 1)];
+          pb.it = st_get(min(bi + 64 + lane, STK - 1));
         }
         sp = bi;
         const uint32_t tt = (p.it.y >> MT_SHIFT) & 0x7Fu;
         const uint32_t ti = L.tinfo[tt];
         p.D = ti & 0xFFFFFFu;
         p.d1 = p.D == 1 && ((ti >> 24) & TF_DOLLAR);   // TF_DOLLAR < 0x80: the fixed-stride bit is not read
+        if constexpr (N12) {   // the item's word: its topic's staged word at its level
+          const uint32_t raw = L.words[(tt & (S - 1)) * dmax + min(p.it.y & LEVEL_MAX, dmax - 1)];
+          p.it.w = (EGM_WORD_SIG && tab.sig_packed) ? word_plain(raw) : raw;
+        }
         issue<PROBE_CONT>(tab, L.words + (tt & (S - 1)) * dmax, nullptr, 0, p);
         uint32_t ttb = 0;
         if (PAIRS) {
@@ -1134,8 +1171,8 @@ __global__ __launch_bounds__(64) EGM_WALK_ATTR void k_walk(DevTable tab, const u
             if (lane == 0) atomicOr(&w.stats->guard, GUARD_STACK);
             return false;
           }
-          if (o.p0) L.stack[sp + mbcnt(c0b)] = o.c0;
-          if (o.p1) L.stack[sp + m0 + mbcnt(c1b)] = o.c1;
+          if (o.p0) st_put(sp + mbcnt(c0b), o.c0);
+          if (o.p1) st_put(sp + m0 + mbcnt(c1b), o.c1);
           sp += nc;
           const uint64_t b0 = __ballot(o.e0), b1 = __ballot(o.e1), b2 = __ballot(o.e2), b3 = __ballot(o.e3);
           const uint32_t n0 = popc(b0), n1 = n0 + popc(b1), n2 = n1 + popc(b2), ne = n2 + popc(b3);
@@ -1808,20 +1845,33 @@ int walk_grid_blocks(uint32_t n) {
 }
 
 // The deep pass: a grid stride over the chunks handed to it, exactly as many
-// waves as are resident together (its LDS stack sets that: 14 per CU at 448
-// items).  A wave that does not fit would start only when another ends, with
+// waves as are resident together (its LDS stack sets that: 16 per CU at 504
+// 12-B items, 14 at round 5's 448 16-B items).  A wave that does not fit would start only when another ends, with
 // a whole share of chunks still to walk: C3 measured 59 ms at 10 waves per CU
 // and 640 items, 80 ms when an 11th was asked for, 53 ms at 14 waves of 448
 // items (r5 A/B).  EGM_DEEP_WAVES forces a count (A/B).
 #ifndef EGM_DEEP_WAVES
 #define EGM_DEEP_WAVES 0   // 0: the occupancy the runtime reports for k_walk<true>
 #endif
+// The runtime's figure is capped by what the LDS holds at a 1280-B allocation
+// granule (160 KB / 128): round 6 measured the deep pass with waves of 11 600 B
+// (the runtime said 14 per CU, 12 fit) at 65.6 ms against 48.8 ms at 11 344 B
+// (14 fit), and 10 320 B (said 15, 14 fit) at 63.3 ms — the waves that did not
+// fit ran as a tail (gpurun_out r6am, r6an).
+constexpr int LDS_PER_CU = 160 * 1024;
+constexpr int LDS_GRANULE = 1280;
 static uint32_t deep_waves_per_cu() {
   static const uint32_t v = [] {
     int nb = EGM_DEEP_WAVES;
     if (nb <= 0 &&
         (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_walk<true>, 64, 0) != hipSuccess || nb <= 0))
       nb = 8;
+    hipFuncAttributes fa;
+    if (EGM_DEEP_WAVES <= 0 && hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_walk<true>)) == hipSuccess &&
+        fa.sharedSizeBytes > 0) {
+      const int per = (int)((fa.sharedSizeBytes + LDS_GRANULE - 1) / LDS_GRANULE) * LDS_GRANULE;
+      nb = std::max(1, std::min(nb, LDS_PER_CU / per));
+    }
     return (uint32_t)std::min(nb, 32);
   }();
   return v;
