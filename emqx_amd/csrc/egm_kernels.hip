@@ -39,9 +39,10 @@ constexpr int TOK_BLOCK = 256;
 #endif
 constexpr int TOK_LDS = EGM_TOK_LDS;
 #ifndef EGM_TOK_WORDS
-#define EGM_TOK_WORDS 2560   // words per tokenise block (5 B of LDS each; 31.4 KB per block -> 5 blocks per CU,
-                             // 4 with round 5's 7 B: C2 0.892 -> 0.877 ms, C3 2.63 -> 2.58, gpurun_out r6al;
-                             // 2048 made C3's segments of 128 depth-16 topics retry as two of 64)
+#define EGM_TOK_WORDS 2528   // words per tokenise block (5 B of LDS each): 32 000 B per block, 25 of LDS's 1 280-B
+                             // allocation granules, so 5 blocks fit per CU (2 560 words took 26 granules: 4 blocks,
+                             // as with round 5's 7 B per word) — C2 0.882 -> 0.773 ms, C3 2.57 -> 2.27 (r6av);
+                             // 2048 made C3's segments of 128 depth-16 topics retry as two of 64
 #endif
 constexpr int TOK_WORDS = EGM_TOK_WORDS;
 #ifndef EGM_TOK_U
