@@ -422,6 +422,7 @@ class PrefixLeg:
         self.d_off = torch.from_numpy(t.off.view(np.int32)).to(dev)
         self.d_vr = torch.from_numpy(vr).to(dev)
         self.ids_per_topic = 64
+        self.settled = False
         self._make(ps)
 
     def _make(self, ps):
@@ -443,8 +444,15 @@ class PrefixLeg:
         return self.ex.match_slot.ids[0].numel()
 
     def step(self):
-        """One step that always completes (PrefixExchange.run: an overflowed
-        slot is redone with grown slots; one 24-byte all-reduce per step)."""
+        """One step.  Until size() has settled the layout it is
+        PrefixExchange.run (an overflowed slot is redone with grown slots: one
+        24-byte all-reduce and a host readback per step).  After that the batch
+        and the slot layout are fixed, so a step is PrefixExchange.step with no
+        host sync — consecutive steps queue back to back at N > 1 — and the
+        received slots' overflow flags accumulate on the device for check(),
+        which fails loudly on any (run() serialised the steps)."""
+        if self.settled:
+            return self.ex.step(self.d_blob, self.d_off, self.n)
         return self.ex.run(self.d_blob, self.d_off, self.n, self.nbytes)
 
     def size(self):
@@ -456,6 +464,7 @@ class PrefixLeg:
             torch.cuda.synchronize(self.dev)
             need = max(int(r[self.ps.cap_topics].item()) for r in self.rows)
             if need <= self.cap:
+                self.settled = True
                 return
             self.ids_per_topic = int(need * 1.25 / max(self.ps.cap_topics, 1)) + 1
             self._make(self.ps)
@@ -466,8 +475,11 @@ class PrefixLeg:
 
     def check(self):
         """After the timed steps (the caller has synced): no slot overflow left
-        unredone, ids fit."""
-        assert not self.ex.overflowed(), "prefix slot overflow"
+        unredone on any rank, ids fit."""
+        flag = self.ex.overflow_flag.clone()
+        if self.world > 1:
+            flag = self.ex.comm.all_max(flag)
+        assert int(flag.item()) == 0, "prefix slot overflow"
         ids = [int(r[self.ps.cap_topics].item()) for r in self.rows]
         assert max(ids) <= self.cap, (ids, self.cap)
         return sum(ids)
